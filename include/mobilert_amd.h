@@ -1,0 +1,113 @@
+/*
+ * mobilert_amd.h - C-ABI of the MI355X (gfx950) render hot path of MobileRT.
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int status codes (0 = ok, < 0 = error,
+ * message from mrt_last_error()).  Every entry point names the reference interface it
+ * replaces (paths relative to TiagoMSSantos/MobileRayTracer):
+ *
+ *   mrt_create                Shader ctor + Renderer ctor as assembled by work_thread
+ *                             (app/System_dependent/Native/C_wrapper.cpp:36-211) and by
+ *                             JNI rtInitialize (app/System_dependent/Android_JNI/JNI_layer.cpp:464-716)
+ *   mrt_render_frame          Renderer::renderFrame(int32_t *bitmap, int32_t numThreads)
+ *                             (app/MobileRT/Renderer.hpp:57, Renderer.cpp:53-88)
+ *   mrt_render_frame_device   the same, bitmap resident in device memory (no PCIe in the window)
+ *   mrt_stop_render           Renderer::stopRender (Renderer.cpp:93-99); JNI rtStopRender
+ *   mrt_get_sample            Renderer::getSample (Renderer.cpp:177-179); JNI rtGetSample
+ *   mrt_get_total_casted_rays Renderer::getTotalCastedRays (Renderer.cpp:204-207)
+ *   mrt_get_scene_info        Shader::getTriangles/getLights/getPlanes/getSpheres/getMaterials
+ *                             sizes (Shader.hpp:92-100); C_wrapper.cpp:199-202 log lines
+ *   mrt_primary_hits          first closest hit of every camera ray (config C2 parity dump)
+ *   mrt_destroy               renderer_.reset() (C_wrapper.cpp:265)
+ *
+ * The desktop symbols RayTrace(Config&, bool) / stopRender() of
+ * app/System_dependent/Native/C_wrapper.h:12-20 are declared in mobilert_amd.hpp (they take
+ * a C++ reference) and exported by the same library.
+ */
+#ifndef MOBILERT_AMD_H
+#define MOBILERT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mrt_renderer mrt_renderer;
+
+/* Mirrors MobileRT::Config (app/MobileRT/Config.hpp:12-83) field for field, minus the
+ * bitmap vector, plus the GPU-only knobs at the end. */
+typedef struct mrt_config {
+    int32_t width;
+    int32_t height;
+    int32_t threads;      /* kept for API parity; the GPU path does not use it */
+    int32_t shader;       /* 1 Whitted, 2 PathTracer (C_wrapper.cpp:154-193) */
+    int32_t sceneIndex;   /* 0 built-in Cornell box, < 0 or > 3 OBJ (C_wrapper.cpp:76-140) */
+    int32_t samplesPixel;
+    int32_t samplesLight;
+    int32_t repeats;
+    int32_t accelerator;  /* 3 BVH (Shader.hpp:20-24); other values are served by the BVH */
+    int32_t printStdOut;
+    const char *objFilePath;
+    const char *mtlFilePath;
+    const char *camFilePath;
+    /* GPU-only */
+    int32_t maxDepth;     /* RayDepthMax (Constants.hpp:45); <= 0 -> 6 */
+    int32_t rankIndex;    /* screen-tile shard owned by this process */
+    int32_t rankCount;    /* number of shards (GPUs); <= 0 -> 1 */
+    int32_t device;       /* HIP device ordinal, -1 = current device */
+    int32_t cull;         /* 1 (default): near-first traversal + conservative t-culling */
+    int32_t maxPathsPerPass; /* <= 0 -> automatic chunk size */
+} mrt_config;
+
+typedef struct mrt_scene_info {
+    int64_t triangles;
+    int64_t lights;
+    int64_t planes;
+    int64_t spheres;
+    int64_t materials;
+    int64_t triangleNodes;
+    int64_t triangleBvhDepth;
+    int64_t pixelSlots;      /* pixels rendered by this shard per sample */
+    int64_t pixelSlotsMax;   /* max over shards (size of a gather slot) */
+    int64_t deviceBytes;     /* device memory held by the renderer */
+} mrt_scene_info;
+
+typedef struct mrt_frame_stats {
+    uint64_t rays;          /* camera + diffuse + specular + transmission rays */
+    uint64_t shadowRays;
+    uint64_t primaryRays;
+    uint64_t nodeRecords;   /* counting pass only: BVH child records fetched */
+    uint64_t triTests;      /* counting pass only: ray/triangle tests */
+    double traceMs;         /* profiling: summed duration of closest-hit trace launches */
+    double shadowMs;        /* profiling: summed duration of any-hit trace launches */
+    double frameMs;         /* profiling: whole frame on the render stream */
+    int64_t traceLaunches;
+    int64_t shadowLaunches;
+} mrt_frame_stats;
+
+const char *mrt_last_error(void);
+int mrt_create(const mrt_config *cfg, mrt_renderer **out);
+void mrt_destroy(mrt_renderer *r);
+/* bitmap: host array of width*height int32 ABGR pixels, updated in place */
+int mrt_render_frame(mrt_renderer *r, int32_t *bitmap);
+/* d_bitmap: device array (width*height) or NULL; d_packed: device array of pixelSlots
+ * entries (this shard's pixels in slot order) or NULL; stream: hipStream_t or NULL */
+int mrt_render_frame_device(mrt_renderer *r, int32_t *d_bitmap, int32_t *d_packed, void *stream);
+/* rank 0 frame assembly: d_gathered holds rankCount slices of pixelSlotsMax entries */
+int mrt_unpack_gathered(mrt_renderer *r, const int32_t *d_gathered, int32_t *d_bitmap, void *stream);
+int mrt_stop_render(mrt_renderer *r);
+int32_t mrt_get_sample(const mrt_renderer *r);
+uint64_t mrt_get_total_casted_rays(const mrt_renderer *r);
+int mrt_get_scene_info(const mrt_renderer *r, mrt_scene_info *info);
+/* enable per-launch HIP event timing (1) and/or node/triangle counting (2) */
+int mrt_set_profiling(mrt_renderer *r, int32_t flags);
+int mrt_get_frame_stats(const mrt_renderer *r, mrt_frame_stats *stats);
+/* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /
+ * 4 light; index in the scene's input order (-1 on miss); t = hit distance */
+int mrt_primary_hits(mrt_renderer *r, int32_t *kind, int32_t *index, float *t);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MOBILERT_AMD_H */

@@ -1,0 +1,191 @@
+"""MI355X-native render hot path of MobileRT (TiagoMSSantos/MobileRayTracer).
+
+Python mirror of the reference's native surface for this path:
+
+* ``Config``            — ``MobileRT::Config`` (app/MobileRT/Config.hpp:12-83)
+* ``Renderer``          — ``MobileRT::Renderer`` (app/MobileRT/Renderer.hpp:41-63) as built by
+                          ``work_thread`` (app/System_dependent/Native/C_wrapper.cpp:36-211):
+                          the constructor assembles scene + shader + BVH + camera, then
+                          ``render_frame`` / ``stop_render`` / ``get_sample`` /
+                          ``get_total_casted_rays`` keep the reference's meaning.
+* ``ray_trace``         — ``RayTrace(Config&, bool)`` (C_wrapper.cpp:268-290).
+
+Everything computes in the HIP kernels of ``libmobilert_amd.so``; there is no CPU path.
+"""
+import ctypes
+import dataclasses
+import threading
+import time
+from typing import List, Optional
+
+import numpy as np
+
+from . import _native
+
+SHADER_WHITTED = 1      # C_wrapper.cpp:155
+SHADER_PATH_TRACER = 2  # C_wrapper.cpp:162
+ACC_BVH = 3             # Shader.hpp:20-24
+RAY_DEPTH_MAX = 6       # Constants.hpp:45
+
+
+@dataclasses.dataclass
+class Config:
+    """MobileRT::Config plus the GPU-only knobs of mrt_config."""
+    width: int = 256
+    height: int = 256
+    threads: int = 1
+    shader: int = SHADER_WHITTED
+    sceneIndex: int = 0
+    samplesPixel: int = 1
+    samplesLight: int = 1
+    repeats: int = 1
+    accelerator: int = ACC_BVH
+    printStdOut: bool = False
+    objFilePath: str = ""
+    mtlFilePath: str = ""
+    camFilePath: str = ""
+    bitmap: Optional[np.ndarray] = None
+    maxDepth: int = RAY_DEPTH_MAX
+    rankIndex: int = 0
+    rankCount: int = 1
+    device: int = -1
+    cull: int = 1
+    maxPathsPerPass: int = 0
+
+    def to_c(self):
+        c = _native.MrtConfig()
+        for f in ("width", "height", "threads", "shader", "sceneIndex", "samplesPixel", "samplesLight",
+                  "repeats", "accelerator", "maxDepth", "rankIndex", "rankCount", "device", "cull",
+                  "maxPathsPerPass"):
+            setattr(c, f, int(getattr(self, f)))
+        c.printStdOut = int(bool(self.printStdOut))
+        self._keep = [s.encode() for s in (self.objFilePath, self.mtlFilePath, self.camFilePath)]
+        c.objFilePath, c.mtlFilePath, c.camFilePath = self._keep
+        return c
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Renderer:
+    def __init__(self, config: Config):
+        self._lib = _native.lib()
+        self.config = config
+        handle = ctypes.c_void_p()
+        _native.check(self._lib.mrt_create(ctypes.byref(config.to_c()), ctypes.byref(handle)))
+        self._h = handle
+
+    # -- reference Renderer surface ------------------------------------------------------
+    def render_frame(self, bitmap: np.ndarray, num_threads: int = 1) -> None:
+        """Renderer::renderFrame(int32_t *bitmap, int32_t numThreads); numThreads is unused."""
+        del num_threads
+        assert bitmap.dtype == np.int32 and bitmap.size == self.config.width * self.config.height
+        assert bitmap.flags["C_CONTIGUOUS"]
+        _native.check(self._lib.mrt_render_frame(self._h, _ptr(bitmap)))
+
+    def render_frame_device(self, d_bitmap: int = 0, d_packed: int = 0, stream: int = 0) -> None:
+        """Frame into device memory (pointers as ints, e.g. torch ``data_ptr()``)."""
+        _native.check(self._lib.mrt_render_frame_device(
+            self._h, ctypes.c_void_p(d_bitmap or None), ctypes.c_void_p(d_packed or None),
+            ctypes.c_void_p(stream or None)))
+
+    def unpack_gathered(self, d_gathered: int, d_bitmap: int, stream: int = 0) -> None:
+        _native.check(self._lib.mrt_unpack_gathered(self._h, ctypes.c_void_p(d_gathered),
+                                                     ctypes.c_void_p(d_bitmap), ctypes.c_void_p(stream or None)))
+
+    def stop_render(self) -> None:
+        _native.check(self._lib.mrt_stop_render(self._h))
+
+    def get_sample(self) -> int:
+        return int(self._lib.mrt_get_sample(self._h))
+
+    def get_total_casted_rays(self) -> int:
+        return int(self._lib.mrt_get_total_casted_rays(self._h))
+
+    # -- extras --------------------------------------------------------------------------
+    def scene_info(self) -> dict:
+        info = _native.MrtSceneInfo()
+        _native.check(self._lib.mrt_get_scene_info(self._h, ctypes.byref(info)))
+        return {f: getattr(info, f) for f, _ in info._fields_}
+
+    def set_profiling(self, timing: bool = False, counting: bool = False) -> None:
+        _native.check(self._lib.mrt_set_profiling(self._h, int(timing) | (2 * int(counting))))
+
+    def frame_stats(self) -> dict:
+        s = _native.MrtFrameStats()
+        _native.check(self._lib.mrt_get_frame_stats(self._h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
+    def primary_hits(self):
+        """(kind, index, t) per pixel, index in the scene's input order (config C2)."""
+        n = self.config.width * self.config.height
+        kind = np.empty(n, np.int32)
+        index = np.empty(n, np.int32)
+        t = np.empty(n, np.float32)
+        _native.check(self._lib.mrt_primary_hits(self._h, _ptr(kind), _ptr(index), _ptr(t)))
+        return kind, index, t
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.mrt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+_active: List[Renderer] = []
+
+
+def ray_trace(config: Config, async_: bool = False):
+    """RayTrace(Config&, bool) (C_wrapper.cpp:36-290): build, render `repeats` frames into
+    config.bitmap, print the reference's summary lines."""
+    def work():
+        if config.bitmap is None:
+            config.bitmap = np.zeros(config.width * config.height, np.int32)
+        t0 = time.perf_counter()
+        r = Renderer(config)
+        t1 = time.perf_counter()
+        _active.append(r)
+        try:
+            repeats = config.repeats
+            t2 = time.perf_counter()
+            while True:
+                r.render_frame(config.bitmap, config.threads)
+                repeats -= 1
+                if repeats <= 0:
+                    break
+            secs = time.perf_counter() - t2
+            rays = r.get_total_casted_rays()
+            if config.printStdOut:
+                info = r.scene_info()
+                print(f"TRIANGLES = {info['triangles']}")
+                print(f"LIGHTS = {info['lights']}")
+                print(f"Creating Time in secs = {t1 - t0}")
+                print(f"Rendering Time in secs = {secs}")
+                print(f"Casted rays = {rays}")
+                print(f"width = {config.width}")
+                print(f"height = {config.height}")
+                print(f"Total Millions rays per second = {rays / secs / 1e6}")
+        finally:
+            _active.remove(r)
+            r.close()
+    if async_:
+        th = threading.Thread(target=work, daemon=True)
+        th.start()
+        return th
+    work()
+    return None
+
+
+def stop_render():
+    """stopRender() (C_wrapper.cpp:271-275)."""
+    for r in list(_active):
+        r.stop_render()

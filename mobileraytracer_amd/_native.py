@@ -1,0 +1,92 @@
+"""ctypes binding of libmobilert_amd.so (include/mobilert_amd.h).
+
+This is the stub a Python front end (or the test-suite) uses in place of the reference's
+native bindings; INTEGRATION.md shows the JNI / Qt equivalents.  The library is built
+in-tree by ``__graft_entry__.build()`` (``make -C mobileraytracer_amd/csrc``).  There is no
+CPU fallback: if the shared object is missing, importing this module raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmobilert_amd.so")
+
+# Symbols the C-ABI exports (include/mobilert_amd.h + mobilert_amd.hpp).
+EXPORTED_SYMBOLS = (
+    "mrt_last_error", "mrt_create", "mrt_destroy", "mrt_render_frame", "mrt_render_frame_device",
+    "mrt_unpack_gathered", "mrt_stop_render", "mrt_get_sample", "mrt_get_total_casted_rays",
+    "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits",
+    "RayTrace", "stopRender",
+)
+
+
+class MrtConfig(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("threads", ctypes.c_int32),
+        ("shader", ctypes.c_int32), ("sceneIndex", ctypes.c_int32), ("samplesPixel", ctypes.c_int32),
+        ("samplesLight", ctypes.c_int32), ("repeats", ctypes.c_int32), ("accelerator", ctypes.c_int32),
+        ("printStdOut", ctypes.c_int32),
+        ("objFilePath", ctypes.c_char_p), ("mtlFilePath", ctypes.c_char_p), ("camFilePath", ctypes.c_char_p),
+        ("maxDepth", ctypes.c_int32), ("rankIndex", ctypes.c_int32), ("rankCount", ctypes.c_int32),
+        ("device", ctypes.c_int32), ("cull", ctypes.c_int32), ("maxPathsPerPass", ctypes.c_int32),
+    ]
+
+
+class MrtSceneInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        "triangles", "lights", "planes", "spheres", "materials", "triangleNodes", "triangleBvhDepth",
+        "pixelSlots", "pixelSlotsMax", "deviceBytes")]
+
+
+class MrtFrameStats(ctypes.Structure):
+    _fields_ = [
+        ("rays", ctypes.c_uint64), ("shadowRays", ctypes.c_uint64), ("primaryRays", ctypes.c_uint64),
+        ("nodeRecords", ctypes.c_uint64), ("triTests", ctypes.c_uint64),
+        ("traceMs", ctypes.c_double), ("shadowMs", ctypes.c_double), ("frameMs", ctypes.c_double),
+        ("traceLaunches", ctypes.c_int64), ("shadowLaunches", ctypes.c_int64),
+    ]
+
+
+def load_library(path=LIB_PATH):
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the MI355X path has no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    sig = {
+        "mrt_last_error": (ctypes.c_char_p, []),
+        "mrt_create": (ctypes.c_int, [P(MrtConfig), P(vp)]),
+        "mrt_destroy": (None, [vp]),
+        "mrt_render_frame": (ctypes.c_int, [vp, vp]),
+        "mrt_render_frame_device": (ctypes.c_int, [vp, vp, vp, vp]),
+        "mrt_unpack_gathered": (ctypes.c_int, [vp, vp, vp, vp]),
+        "mrt_stop_render": (ctypes.c_int, [vp]),
+        "mrt_get_sample": (ctypes.c_int32, [vp]),
+        "mrt_get_total_casted_rays": (ctypes.c_uint64, [vp]),
+        "mrt_get_scene_info": (ctypes.c_int, [vp, P(MrtSceneInfo)]),
+        "mrt_set_profiling": (ctypes.c_int, [vp, ctypes.c_int32]),
+        "mrt_get_frame_stats": (ctypes.c_int, [vp, P(MrtFrameStats)]),
+        "mrt_primary_hits": (ctypes.c_int, [vp, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = load_library()
+    return _LIB
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(lib().mrt_last_error().decode(errors="replace"))

@@ -1,0 +1,307 @@
+// mrt_device.hpp - device-side scene view, BVH traversal and primitive tests for gfx950.
+//
+// Reachability and tie semantics follow SURVEY.md Appendix A.7:
+//   * a primitive is tested only if every ancestor box passes the reference slab predicate
+//     (AABB.cpp:34-54, reproduced with libstdc++ min/max operand order);
+//   * the closest hit is the lexicographic minimum of (t, kind, BVH index), which equals the
+//     reference's "first visited wins on equal t" because its left-first DFS visits leaves in
+//     ascending BVH primitive index (BVH.hpp:252-268, 357-373) and kinds in the order
+//     planes, spheres, triangles, lights (Shader.cpp:104-111);
+//   * boxes are visited near-first and culled against the current best t with a relative
+//     margin (kCullMargin) that keeps every box that could hold an equal or rounding-adjacent t.
+#pragma once
+
+#include "mrt_common.hpp"
+
+namespace mrt {
+
+constexpr int kBlock = 256;         // threads per workgroup for every trace kernel
+constexpr int kLdsStack = 16;       // per-thread short stack in LDS (entries of 8 bytes)
+constexpr float kCullMargin = 0x1p-10f;
+
+struct DScene {
+    const float4* triGeom;     // 3 per triangle (BVH order): A, AB, AC  (xyz)
+    const float4* triShade;    // 3 per triangle: nA (w = material index bits), nB, nC
+    const GNode* triNodes;
+    const float4* planes;      // 2 per plane: normal (w = material bits), point
+    const GNode* planeNodes;
+    const float4* spheres;     // 2 per sphere: center (w = sqRadius), (x = material bits)
+    const GNode* sphereNodes;
+    const float4* lights;      // 4 per light: A or position (w = kind bits), AB, AC, Le
+    const float4* mats;        // 4 per material: Le (w = ior), Kd, Ks, Kt
+    const float* shaderTable;  // 2^20 shuffled Halton values (Shader.cpp:23)
+    const float* samplerTable; // 2^20 shuffled Halton values (StaticHaltonSeq.cpp)
+    GRoot triRoot, planeRoot, sphereRoot;
+    int32_t nLights;
+    int32_t nMats;
+    int32_t cull;              // 1: near-first + conservative t-culling, 0: reference visit set
+    int32_t pad;
+};
+
+__device__ __forceinline__ float4 ld4(const float4* p) { return *p; }
+__device__ __forceinline__ v3 xyz(float4 a) { return v3{a.x, a.y, a.z}; }
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
+
+// AABB.cpp:34-54 with the ray's reciprocal direction precomputed (same value: 1.0F / d[axis]).
+// Returns the reference predicate; *tEntry = max(tMin, 0) for ordering / culling.
+__device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, v3 o, v3 inv,
+                                     float* tEntry) {
+    const float t1x = (mnx - o.x) * inv.x;
+    const float t2x = (mxx - o.x) * inv.x;
+    float tMin = stdmin(t1x, t2x);
+    float tMax = stdmax(t1x, t2x);
+    const float t1y = (mny - o.y) * inv.y;
+    const float t2y = (mxy - o.y) * inv.y;
+    tMin = stdmax(tMin, stdmin(t1y, t2y));
+    tMax = stdmin(tMax, stdmax(t1y, t2y));
+    const float t1z = (mnz - o.z) * inv.z;
+    const float t2z = (mxz - o.z) * inv.z;
+    tMin = stdmax(tMin, stdmin(t1z, t2z));
+    tMax = stdmin(tMax, stdmax(t1z, t2z));
+    const float e = stdmax(tMin, 0.0F);
+    *tEntry = e;
+    return tMax >= e;
+}
+
+// Short traversal stack: the top kLdsStack entries live in LDS (conflict-free layout
+// [slot][thread]), deeper entries spill to a per-thread global area.
+struct TStack {
+    int2* lds;   // &ldsBase[threadIdx.x]; slot s at lds[s * kBlock]
+    int2* glob;  // per-thread overflow area
+    int sp;
+    __device__ __forceinline__ void push(int ref, float t) {
+        const int slot = sp & (kLdsStack - 1);
+        if (sp >= kLdsStack) glob[sp - kLdsStack] = lds[slot * kBlock];
+        lds[slot * kBlock] = make_int2(ref, __float_as_int(t));
+        ++sp;
+    }
+    __device__ __forceinline__ int2 pop() {
+        --sp;
+        const int slot = sp & (kLdsStack - 1);
+        const int2 v = lds[slot * kBlock];
+        if (sp >= kLdsStack) lds[slot * kBlock] = glob[sp - kLdsStack];
+        return v;
+    }
+};
+
+struct Best {
+    float t, u, v;
+    uint32_t code;  // encodePrim(kind, index) or kNoPrim
+};
+
+// Triangle.cpp:63-109 (without the hit-record construction); returns t, u, v.
+__device__ __forceinline__ bool triTest(float4 a4, float4 ab4, float4 ac4, v3 o, v3 d, float* tOut, float* uOut,
+                                        float* vOut) {
+    const v3 A = xyz(a4), AB = xyz(ab4), AC = xyz(ac4);
+    const v3 p = cross(d, AC);
+    const float det = dot(AB, p);
+    if (fabsf(det) < kEpsilon) return false;
+    const float inv = 1.0F / det;
+    const v3 s = o - A;
+    const float u = inv * dot(s, p);
+    if (u < 0.0F || u > 1.0F) return false;
+    const v3 q = cross(s, AB);
+    const float v = inv * dot(d, q);
+    if (v < 0.0F || (u + v) > 1.0F) return false;
+    *tOut = inv * dot(AC, q);
+    *uOut = u;
+    *vOut = v;
+    return true;
+}
+
+// lexicographic (t, kind, index) acceptance; `same` = candidate kind equals best kind
+__device__ __forceinline__ bool better(float t, uint32_t code, const Best& b) {
+    return !(t >= b.t) || (t == b.t && primKind(b.code) == primKind(code) && primIndex(code) < primIndex(b.code));
+}
+
+template <bool kAny>
+__device__ __forceinline__ bool leafTriangles(const DScene& s, int first, int count, v3 o, v3 d, uint32_t src,
+                                              Best* b, uint32_t* nTri) {
+    for (int k = 0; k < count; ++k) {
+        const int j = first + k;
+        const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
+        if (code == src) continue;  // Triangle.cpp:64-66 self-exclusion
+        const float4* g = s.triGeom + 3 * j;
+        float t, u, v;
+        ++*nTri;
+        if (!triTest(ld4(g), ld4(g + 1), ld4(g + 2), o, d, &t, &u, &v)) continue;
+        if (t < kEpsilon) continue;
+        if (kAny) {
+            if (!(t >= b->t)) return true;
+        } else if (better(t, code, *b)) {
+            b->t = t;
+            b->u = u;
+            b->v = v;
+            b->code = code;
+        }
+    }
+    return false;
+}
+
+template <bool kAny>
+__device__ __forceinline__ bool leafPlanes(const DScene& s, int first, int count, v3 o, v3 d, uint32_t src, Best* b) {
+    for (int k = 0; k < count; ++k) {  // Plane.cpp:38-72
+        const int j = first + k;
+        const uint32_t code = encodePrim(kPlane, static_cast<uint32_t>(j));
+        if (code == src) continue;
+        const v3 n = xyz(s.planes[2 * j]);
+        const v3 p0 = xyz(s.planes[2 * j + 1]);
+        const float den = dot(n, d);
+        if (fabsf(den) < kEpsilon) continue;
+        const v3 vtp = p0 - o;
+        const float num = dot(n, vtp);
+        const float t = num / den;
+        if (t < kEpsilon) continue;
+        if (kAny) {
+            if (!(t >= b->t)) return true;
+        } else if (better(t, code, *b)) {
+            b->t = t;
+            b->u = 0.0F;
+            b->v = 0.0F;
+            b->code = code;
+        }
+    }
+    return false;
+}
+
+template <bool kAny>
+__device__ __forceinline__ bool leafSpheres(const DScene& s, int first, int count, v3 o, v3 d, Best* b) {
+    for (int k = 0; k < count; ++k) {  // Sphere.cpp:42-81 (no self-exclusion)
+        const int j = first + k;
+        const float4 c4 = s.spheres[2 * j];
+        const v3 oc = xyz(c4) - o;
+        const float proj = dot(oc, d);
+        const float ocMag = length(oc);
+        const float a = dot(d, d);
+        const float bq = 2.0F * -proj;
+        const float c = ocMag * ocMag - c4.w;
+        const float disc = bq * bq - 4.0F * a * c;
+        if (disc < 0.0F) continue;
+        const float r = sqrtf(disc);
+        const float d1 = -bq + r;
+        const float d2 = -bq - r;
+        const float t = stdmin(d1, d2) / (2.0F * a);
+        if (t < kEpsilonLarge) continue;
+        const uint32_t code = encodePrim(kSphere, static_cast<uint32_t>(j));
+        if (kAny) {
+            if (!(t >= b->t)) return true;
+        } else if (better(t, code, *b)) {
+            b->t = t;
+            b->u = 0.0F;
+            b->v = 0.0F;
+            b->code = code;
+        }
+    }
+    return false;
+}
+
+struct TravCount {
+    uint32_t nodes;  // child records fetched (2 per inner visit)
+    uint32_t tris;   // triangle tests
+};
+
+// Generic BVH walk.  kKind selects the leaf routine.  Returns true on an any-hit.
+template <int kKind, bool kAny>
+__device__ __forceinline__ bool traverse(const DScene& s, const GNode* nodes, const GRoot& root, v3 o, v3 d, v3 inv,
+                                         uint32_t src, Best* b, TStack& st, TravCount* cnt) {
+    if (root.count == 0) return false;  // BVH.hpp:328-330
+    float te;
+    if (!slab(root.bmin[0], root.bmin[1], root.bmin[2], root.bmax[0], root.bmax[1], root.bmax[2], o, inv, &te))
+        return false;
+    const int base = st.sp;
+    int ref = root.ref;
+    while (true) {
+        if (ref >= 0) {
+            const float4* np = reinterpret_cast<const float4*>(nodes + ref);
+            const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+            const int4 n3 = reinterpret_cast<const int4*>(np)[3];
+            cnt->nodes += 2;
+            float tl, tr;
+            bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
+            bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+            if (s.cull) {
+                const float lim = b->t + b->t * kCullMargin;
+                hl = hl && !(tl > lim);
+                hr = hr && !(tr > lim);
+            }
+            if (hl && hr) {
+                int nearRef = n3.x, farRef = n3.y;
+                float farT = tr;
+                if (s.cull && tr < tl) {
+                    nearRef = n3.y;
+                    farRef = n3.x;
+                    farT = tl;
+                }
+                st.push(farRef, farT);
+                ref = nearRef;
+                continue;
+            }
+            if (hl) {
+                ref = n3.x;
+                continue;
+            }
+            if (hr) {
+                ref = n3.y;
+                continue;
+            }
+        } else {
+            const int first = leafFirst(ref), count = leafCount(ref);
+            bool any = false;
+            if (kKind == kTriangle) any = leafTriangles<kAny>(s, first, count, o, d, src, b, &cnt->tris);
+            if (kKind == kPlane) any = leafPlanes<kAny>(s, first, count, o, d, src, b);
+            if (kKind == kSphere) any = leafSpheres<kAny>(s, first, count, o, d, b);
+            if (kAny && any) {
+                st.sp = base;
+                return true;
+            }
+        }
+        // pop (skipping entries the current best has culled)
+        while (true) {
+            if (st.sp == base) return false;
+            const int2 e = st.pop();
+            const float et = __int_as_float(e.y);
+            if (!s.cull || !(et > b->t + b->t * kCullMargin)) {
+                ref = e.x;
+                break;
+            }
+        }
+    }
+}
+
+// Shader::rayTrace intersection part (Shader.cpp:86-111): planes, spheres, triangles, lights.
+__device__ __forceinline__ Best closestHit(const DScene& s, v3 o, v3 d, uint32_t src, TStack& st, TravCount* cnt) {
+    const v3 inv = v3{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
+    Best b{kRayLengthMax, 0.0F, 0.0F, kNoPrim};
+    traverse<kPlane, false>(s, s.planeNodes, s.planeRoot, o, d, inv, src, &b, st, cnt);
+    traverse<kSphere, false>(s, s.sphereNodes, s.sphereRoot, o, d, inv, src, &b, st, cnt);
+    traverse<kTriangle, false>(s, s.triNodes, s.triRoot, o, d, inv, src, &b, st, cnt);
+    for (int j = 0; j < s.nLights; ++j) {  // Shader.cpp:166-171, AreaLight.cpp:32-41
+        const float4* l = s.lights + 4 * j;
+        const float4 a4 = l[0];
+        if (__float_as_int(a4.w) != 1) continue;  // point lights are never hit
+        float t, u, v;
+        if (!triTest(a4, l[1], l[2], o, d, &t, &u, &v)) continue;
+        if (t < kEpsilon) continue;
+        const uint32_t code = encodePrim(kLight, static_cast<uint32_t>(j));
+        if (better(t, code, b)) {
+            b.t = t;
+            b.u = u;
+            b.v = v;
+            b.code = code;
+        }
+    }
+    return b;
+}
+
+// Shader::shadowTrace (Shader.cpp:132-158): any hit closer than `dist`, lights excluded.
+__device__ __forceinline__ bool anyHit(const DScene& s, v3 o, v3 d, uint32_t src, float dist, TStack& st,
+                                       TravCount* cnt) {
+    const v3 inv = v3{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
+    Best b{dist, 0.0F, 0.0F, kNoPrim};
+    if (traverse<kPlane, true>(s, s.planeNodes, s.planeRoot, o, d, inv, src, &b, st, cnt)) return true;
+    if (traverse<kSphere, true>(s, s.sphereNodes, s.sphereRoot, o, d, inv, src, &b, st, cnt)) return true;
+    return traverse<kTriangle, true>(s, s.triNodes, s.triRoot, o, d, inv, src, &b, st, cnt);
+}
+
+}  // namespace mrt

@@ -1,0 +1,535 @@
+// mrt_kernels.hip - the wavefront render pipeline for gfx950 (MI355X).
+//
+// One "path" = one (pixel, sample) camera ray and the ray tree the shader grows from it.
+// A frame is processed level by level (level == ray depth, Ray.hpp depth_):
+//
+//   raygen (level 1)                       Renderer.cpp:130-141, Perspective.cpp:16-28
+//   for L = 1 .. maxDepth+1:
+//     trace    closest hit of level L      Shader.cpp:86-111, BVH.hpp:327-384
+//     shade    vertex records, shadow rays, child rays of level L+1 (wave-aggregated
+//              compaction: one atomic per wave)           Whitted.cpp / PathTracer.cpp
+//     shadow   any-hit of the shadow rays  Shader.cpp:132-158
+//   for L = maxDepth+1 .. 1:
+//     resolve  bottom-up radiance of every vertex, in the reference's float-op order
+//   accumulate incrementalAvg per pixel, sample by sample   Utils.cpp:66-90
+//
+// Evaluating the ray tree bottom-up (instead of forward throughput) keeps every float
+// operation in the order of the recursive reference, which is what makes the Whitted
+// Cornell image bit-exact.
+#include "mrt_kernels.hpp"
+
+namespace mrt {
+
+// ---------------------------------------------------------------------------------------
+// wave helpers (wave64)
+__device__ __forceinline__ int laneId() { return static_cast<int>(threadIdx.x & 63u); }
+
+__device__ __forceinline__ int waveExclusiveScan(int v, int* total) {
+    const int lane = laneId();
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+// Allocates n slots per lane from *counter with ONE atomic per wave; every lane of the
+// wave must call it (n = 0 for idle lanes).
+__device__ __forceinline__ int waveAlloc(int* counter, int n) {
+    int total;
+    const int excl = waveExclusiveScan(n, &total);
+    int base = 0;
+    if (laneId() == 63 && total > 0) base = atomicAdd(counter, total);
+    base = __shfl(base, 63, 64);
+    return base + excl;
+}
+
+// ---------------------------------------------------------------------------------------
+// pixel mapping: path p -> (pixel slot, sample); slot -> (x, y) through the unit table
+__device__ __forceinline__ void slotToXY(const PixelMap& m, int slot, int* x, int* y) {
+    int lo = 0, hi = m.nUnits - 1;
+    while (lo < hi) {  // last unit whose prefix <= slot
+        const int mid = (lo + hi + 1) >> 1;
+        if (m.prefix[mid] <= slot) lo = mid; else hi = mid - 1;
+    }
+    const int4 r = m.rect[lo];
+    const int off = slot - m.prefix[lo];
+    *x = r.x + off / r.w;  // column-major inside the unit: 8 rows per column
+    *y = r.y + off % r.w;
+}
+// rect.z = unit width (columns), rect.w = unit height (rows)
+
+__global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* counters) {
+    const int p = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p == 0) counters[kCntRays + 1] = a.nPaths;
+    if (p >= a.nPaths) return;
+    const int slot = a.slotBase + p / a.spp;
+    const int s = p % a.spp;
+    int x, y;
+    slotToXY(a.map, slot, &x, &y);
+    const uint32_t pixelIndex = static_cast<uint32_t>(y * a.width + x);
+    const uint32_t key = pathKey(pixelIndex, static_cast<uint32_t>(a.sampleBase + s));
+    // Renderer.cpp:108-111, 131-140
+    const float invW = 1.0F / static_cast<float>(a.width);
+    const float invH = 1.0F / static_cast<float>(a.height);
+    const float pixW = 0.5F / static_cast<float>(a.width);
+    const float pixH = 0.5F / static_cast<float>(a.height);
+    const float u = static_cast<float>(x) * invW;
+    const float v = static_cast<float>(y) * invH;
+    float r1 = 0.5F, r2 = 0.5F;  // Constant(0.5) when spp <= 1 (C_wrapper.cpp:144-148)
+    if (a.sppTotal > 1) {
+        r1 = a.samplerTable[sampleIndex(key, 0u, kPJitterU)];
+        r2 = a.samplerTable[sampleIndex(key, 0u, kPJitterV)];
+    }
+    const float devU = (r1 - 0.5F) * 2.0F * pixW;
+    const float devV = (r2 - 0.5F) * 2.0F * pixH;
+    // Perspective.cpp:16-28
+    const GCamera& c = a.cam;
+    const float rf = fastArcTan(c.hFov * (u - 0.5F)) + devU;
+    const v3 right = c.right * rf;
+    const float uf = fastArcTan(c.vFov * (0.5F - v)) + devV;
+    const v3 up = c.up * uf;
+    const v3 dest = ((c.position + c.direction) + right) + up;
+    const v3 dir = normalize(dest - c.position);
+    lv.rO[p] = make_float4(c.position.x, c.position.y, c.position.z, bitsf(key));
+    lv.rD[p] = make_float4(dir.x, dir.y, dir.z, bitsf(kNoPrim));
+    lv.tree[p] = 1u;
+}
+
+// ---------------------------------------------------------------------------------------
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* counters, int level, int2* gstack,
+                                                  int gdepth, unsigned long long* stats) {
+    __shared__ int2 ldsStack[kLdsStack * kBlock];
+    TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0};
+    const int count = min(counters[kCntRays + level], lv.cap);
+    int* fetch = counters + kCntFetchTrace + level;
+    TravCount cnt{0u, 0u};
+    while (true) {
+        int base = 0;
+        if (laneId() == 0) base = atomicAdd(fetch, 64);
+        base = __shfl(base, 0, 64);
+        if (base >= count) break;
+        const int i = base + laneId();
+        if (i < count) {
+            const float4 o4 = lv.rO[i];
+            const float4 d4 = lv.rD[i];
+            const Best b = closestHit(s, xyz(o4), xyz(d4), fbits(d4.w), st, &cnt);
+            lv.hit[i] = make_float4(b.t, b.u, b.v, bitsf(b.code));
+        }
+    }
+    if (kCount) {
+        unsigned long long n = cnt.nodes, t = cnt.tris;
+        for (int off = 32; off > 0; off >>= 1) {
+            n += __shfl_down(n, off, 64);
+            t += __shfl_down(t, off, 64);
+        }
+        if (laneId() == 0) {
+            atomicAdd(stats + kStatNodes, n);
+            atomicAdd(stats + kStatTris, t);
+        }
+    }
+}
+
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void k_shadow(DScene s, Level lv, int* counters, int level, int2* gstack,
+                                                   int gdepth, unsigned long long* stats) {
+    __shared__ int2 ldsStack[kLdsStack * kBlock];
+    TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0};
+    const int count = min(counters[kCntShadows + level], lv.shadowCap);
+    int* fetch = counters + kCntFetchShadow + level;
+    TravCount cnt{0u, 0u};
+    while (true) {
+        int base = 0;
+        if (laneId() == 0) base = atomicAdd(fetch, 64);
+        base = __shfl(base, 0, 64);
+        if (base >= count) break;
+        const int i = base + laneId();
+        if (i < count) {
+            const float4 o4 = lv.sO[i];
+            const float4 d4 = lv.sD[i];
+            const bool occ = anyHit(s, xyz(o4), xyz(d4), fbits(o4.w), d4.w, st, &cnt);
+            lv.sC[i].w = occ ? 1.0F : 0.0F;
+        }
+    }
+    if (kCount) {
+        unsigned long long n = cnt.nodes, t = cnt.tris;
+        for (int off = 32; off > 0; off >>= 1) {
+            n += __shfl_down(n, off, 64);
+            t += __shfl_down(t, off, 64);
+        }
+        if (laneId() == 0) {
+            atomicAdd(stats + kStatNodes, n);
+            atomicAdd(stats + kStatTris, t);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+struct HitGeom {
+    v3 P, N;
+    uint32_t src;  // primitive the child rays start from (spheres: none, Sphere.cpp:77)
+};
+
+__device__ __forceinline__ HitGeom hitGeometry(const DScene& s, v3 o, v3 d, float4 h) {
+    const uint32_t code = fbits(h.w);
+    const uint32_t kind = primKind(code);
+    const uint32_t j = primIndex(code);
+    HitGeom g;
+    g.P = o + d * h.x;  // Triangle.cpp:99, Plane.cpp:62, Sphere.cpp:71
+    g.src = code;
+    if (kind == kTriangle) {
+        const float4* sh = s.triShade + 3 * j;
+        const float w = 1.0F - h.y - h.z;  // Triangle.cpp:96-97
+        g.N = normalize(xyz(sh[0]) * w + xyz(sh[1]) * h.y + xyz(sh[2]) * h.z);
+    } else if (kind == kPlane) {
+        g.N = xyz(s.planes[2 * j]);
+    } else {  // sphere
+        g.N = normalize(g.P - xyz(s.spheres[2 * j]));
+        g.src = kNoPrim;
+    }
+    return g;
+}
+
+__device__ __forceinline__ int hitMaterial(const DScene& s, uint32_t code) {
+    const uint32_t kind = primKind(code);
+    const uint32_t j = primIndex(code);
+    if (kind == kTriangle) return __float_as_int(s.triShade[3 * j].w);
+    if (kind == kPlane) return __float_as_int(s.planes[2 * j].w);
+    return __float_as_int(s.spheres[2 * j + 1].x);
+}
+
+// Shader::getCosineSampleHemisphere (Shader.cpp:188-216); cos/sin evaluated in double and
+// rounded, which agrees with glibc cosf/sinf except in rare last-ulp cases.
+__device__ __forceinline__ v3 cosineHemisphere(const DScene& s, v3 n, uint32_t key, uint32_t tc) {
+    const float r1 = s.shaderTable[sampleIndex(key, tc, kPHemi1)];
+    const float r2 = s.shaderTable[sampleIndex(key, tc, kPHemi2)];
+    const float phi = kTwoPi * r1;
+    const float cosTheta = sqrtf(r2);
+    v3 u = fabsf(n.x) > 0.1F ? v3{0.0F, 1.0F, 0.0F} : v3{1.0F, 0.0F, 0.0F};
+    u = normalize(cross(u, n));
+    const v3 v = cross(n, u);
+    const float cphi = static_cast<float>(cos(static_cast<double>(phi)));
+    const float sphi = static_cast<float>(sin(static_cast<double>(phi)));
+    const v3 dir = (u * (cphi * cosTheta) + v * (sphi * cosTheta)) + n * sqrtf(1.0F - r2);
+    return normalize(dir);
+}
+
+// Light sample i of a shading point (Whitted.cpp:41-53, PathTracer.cpp:53-67):
+// returns false when cos <= 0 (no shadow ray is built).
+__device__ __forceinline__ bool lightSample(const DScene& s, const HitGeom& g, uint32_t key, uint32_t tc, int i,
+                                           v3* dirOut, float* distOut, v3* contribOut) {
+    const float pick = s.shaderTable[sampleIndex(key, tc, purposeLightPick(i))];
+    const uint32_t chosen = static_cast<uint32_t>(floorf(pick * static_cast<float>(s.nLights) * 0.99999F));
+    const float4* l = s.lights + 4 * chosen;
+    const float4 a4 = l[0];
+    v3 pos;
+    if (__float_as_int(a4.w) == 1) {  // AreaLight::getPosition (AreaLight.cpp:17-26)
+        float r = s.samplerTable[sampleIndex(key, tc, purposeLightR(i))];
+        float q = s.samplerTable[sampleIndex(key, tc, purposeLightS(i))];
+        if (r + q >= 1.0F) {
+            r = 1.0F - r;
+            q = 1.0F - q;
+        }
+        pos = (xyz(a4) + r * xyz(l[1])) + q * xyz(l[2]);
+    } else {
+        pos = xyz(a4);
+    }
+    v3 toLight = pos - g.P;
+    const float dist = length(toLight);
+    toLight = normalize(toLight);
+    const float cosNl = dot(g.N, toLight);
+    if (!(cosNl > 0.0F)) return false;
+    *dirOut = toLight;
+    *distOut = dist;
+    *contribOut = xyz(l[3]) * cosNl;
+    return true;
+}
+
+template <int kShader>
+__global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
+    const int count = min(counters[kCntRays + level], lv.cap);
+    int* nextCount = counters + kCntRays + level + 1;
+    int* shadowCount = counters + kCntShadows + level;
+    for (int base = static_cast<int>(blockIdx.x * blockDim.x); base < count;
+         base += static_cast<int>(gridDim.x * blockDim.x)) {
+        const int i = base + static_cast<int>(threadIdx.x);
+        const bool active = i < count;
+        int nShadow = 0, nChild = 0;
+        bool terminal = true;
+        float4 leaf = make_float4(0.0F, 0.0F, 0.0F, 0.0F);
+        HitGeom g{};
+        v3 d{0, 0, 0}, Kd{0, 0, 0}, Ks{0, 0, 0}, Kt{0, 0, 0};
+        float ior = 1.0F;
+        int mat = -1;
+        uint32_t key = 0, tc = 0;
+        bool wantD = false, wantS = false, wantT = false, direct = false;
+        if (active) {
+            const float4 o4 = lv.rO[i];
+            const float4 d4 = lv.rD[i];
+            const float4 h = lv.hit[i];
+            key = fbits(o4.w);
+            tc = lv.tree[i];
+            d = xyz(d4);
+            const uint32_t code = fbits(h.w);
+            const uint32_t kind = primKind(code);
+            // Shader.cpp:122: shade only if hit; Whitted.cpp:14-17 / PathTracer.cpp:25-28: depth cap
+            if (kind != kMiss && level <= a.maxDepth) {
+                v3 Le;
+                if (kind == kLight) {
+                    Le = xyz(s.lights[4 * primIndex(code) + 3]);
+                } else {
+                    mat = hitMaterial(s, code);
+                    const float4* m = s.mats + 4 * mat;
+                    const float4 le4 = m[0];
+                    Le = xyz(le4);
+                    ior = le4.w;
+                    Kd = xyz(m[1]);
+                    Ks = xyz(m[2]);
+                    Kt = xyz(m[3]);
+                }
+                if (hasPositive(Le)) {  // Whitted.cpp:19-24
+                    leaf = make_float4(Le.x, Le.y, Le.z, 1.0F);
+                } else {
+                    terminal = false;
+                    g = hitGeometry(s, xyz(o4), d, h);
+                    direct = hasPositive(Kd) && s.nLights > 0;
+                    if (direct) {
+                        for (int k = 0; k < a.samplesLight; ++k) {
+                            v3 ld, lc;
+                            float dist;
+                            if (lightSample(s, g, key, tc, k, &ld, &dist, &lc)) ++nShadow;
+                        }
+                    }
+                    if (kShader == kShaderPathTracer && hasPositive(Kd)) {  // PathTracer.cpp:89
+                        wantD = level <= kRayDepthMin || s.samplerTable[sampleIndex(key, tc, kPRussian)] > 0.5F;
+                    }
+                    wantS = hasPositive(Ks);
+                    wantT = hasPositive(Kt);
+                    nChild = static_cast<int>(wantD) + static_cast<int>(wantS) + static_cast<int>(wantT);
+                }
+            }
+        }
+        const int shadowBase = waveAlloc(shadowCount, nShadow);
+        const int childBase = waveAlloc(nextCount, nChild);
+        if (!active) continue;
+        if (terminal) {
+            lv.res[i] = leaf;
+            lv.vtxA[i] = make_int4(-1, 0, 0, 0);
+            continue;
+        }
+        // shadow rays (Whitted.cpp:53, PathTracer.cpp:67)
+        int written = 0;
+        if (direct) {
+            for (int k = 0; k < a.samplesLight; ++k) {
+                v3 ld, lc;
+                float dist;
+                if (!lightSample(s, g, key, tc, k, &ld, &dist, &lc)) continue;
+                const int j = shadowBase + written;
+                ++written;
+                if (j < lv.shadowCap) {
+                    lv.sO[j] = make_float4(g.P.x, g.P.y, g.P.z, bitsf(g.src));
+                    lv.sD[j] = make_float4(ld.x, ld.y, ld.z, dist);
+                    lv.sC[j] = make_float4(lc.x, lc.y, lc.z, 0.0F);
+                } else {
+                    atomicOr(counters + kCntOverflow, 1);
+                }
+            }
+        }
+        // child rays: diffuse (PathTracer.cpp:90-91), specular (:118-120), transmission (:129-131)
+        int4 child = make_int4(-1, -1, -1, 0);
+        int c = childBase;
+        auto emit = [&](v3 dir, uint32_t slot) -> int {
+            const int j = c++;
+            if (j >= nx.cap) {
+                atomicOr(counters + kCntOverflow, 1);
+                return -1;
+            }
+            nx.rO[j] = make_float4(g.P.x, g.P.y, g.P.z, bitsf(key));
+            nx.rD[j] = make_float4(dir.x, dir.y, dir.z, bitsf(g.src));
+            nx.tree[j] = tc * 4u + slot;
+            return j;
+        };
+        if (wantD) child.x = emit(cosineHemisphere(s, g.N, key, tc), 1u);
+        if (wantS) child.y = emit(reflect(d, g.N), 2u);
+        if (wantT) child.z = emit(refract(d, g.N, 1.0F / ior), 3u);
+        lv.vtxA[i] = make_int4(mat, shadowBase, nShadow, 0);
+        lv.vtxB[i] = child;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+template <int kShader>
+__global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
+    const int count = min(counters[kCntRays + level], lv.cap);
+    for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
+         i += static_cast<int>(gridDim.x * blockDim.x)) {
+        const int4 va = lv.vtxA[i];
+        if (va.x < 0) continue;  // terminal: res written by k_shade
+        const int4 vb = lv.vtxB[i];
+        const float4* m = s.mats + 4 * va.x;
+        const v3 Kd = xyz(m[1]), Ks = xyz(m[2]), Kt = xyz(m[3]);
+        const bool direct = hasPositive(Kd) && s.nLights > 0;
+        v3 Ld{0.0F, 0.0F, 0.0F};
+        if (direct) {
+            for (int k = 0; k < va.z; ++k) {
+                const int j = va.y + k;
+                if (j >= lv.shadowCap) break;
+                const float4 c = lv.sC[j];
+                if (c.w == 0.0F) Ld = Ld + xyz(c);
+            }
+            Ld = Ld * Kd;
+            Ld = Ld / static_cast<float>(a.samplesLight);
+        }
+        float4 out;
+        if (kShader == kShaderWhitted) {  // Whitted.cpp:36-92
+            v3 rgb = Ld;
+            if (hasPositive(Ks) && vb.y >= 0) rgb = rgb + Ks * xyz(nx.res[vb.y]);
+            if (hasPositive(Kt) && vb.z >= 0) rgb = rgb + Kt * xyz(nx.res[vb.z]);
+            rgb = rgb + Kd * 0.1F;
+            out = make_float4(rgb.x, rgb.y, rgb.z, 0.0F);
+        } else {  // PathTracer.cpp:127-142
+            v3 LiD{0.0F, 0.0F, 0.0F}, LiS{0.0F, 0.0F, 0.0F}, LiT{0.0F, 0.0F, 0.0F};
+            bool hitLight = false;
+            if (vb.x >= 0) {
+                const float4 r = nx.res[vb.x];
+                hitLight = r.w != 0.0F;
+                LiD = LiD + Kd * xyz(r);
+                if (level > kRayDepthMin) LiD = LiD / (0.5F * 0.5F);
+                if (hasPositive(Ld) && hitLight) LiD = v3{0.0F, 0.0F, 0.0F};
+            }
+            if (hasPositive(Ks) && vb.y >= 0) LiS = LiS + Ks * xyz(nx.res[vb.y]);
+            if (hasPositive(Kt) && vb.z >= 0) LiT = LiT + Kt * xyz(nx.res[vb.z]);
+            v3 rgb{0.0F, 0.0F, 0.0F};
+            rgb = rgb + Ld;
+            rgb = rgb + LiD;
+            rgb = rgb + LiS;
+            rgb = rgb + LiT;
+            out = make_float4(rgb.x, rgb.y, rgb.z, hitLight ? 1.0F : 0.0F);
+        }
+        lv.res[i] = out;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_accumulate(AccumArgs a, const float4* res, int32_t* bitmap, int32_t* packed) {
+    const int q = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= a.nSlots) return;
+    const int slot = a.slotBase + q;
+    int x, y;
+    slotToXY(a.map, slot, &x, &y);
+    const int idx = y * a.width + x;
+    int32_t c = (a.sampleBase > 0 && bitmap != nullptr) ? bitmap[idx] : 0;
+    for (int s = 0; s < a.spp; ++s) {
+        const float4 r = res[q * a.spp + s];
+        c = incrementalAvg(v3{r.x, r.y, r.z}, c, a.sampleBase + s + 1);
+    }
+    if (bitmap != nullptr) bitmap[idx] = c;
+    if (packed != nullptr) packed[slot] = c;
+}
+
+// scatter a gathered, rank-packed buffer into the bitmap (multi-GPU frame assembly)
+__global__ __launch_bounds__(256) void k_unpack(PixelMap map, int width, int nSlots, const int32_t* packed,
+                                                int32_t* bitmap) {
+    const int q = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= nSlots) return;
+    int x, y;
+    slotToXY(map, q, &x, &y);
+    bitmap[y * width + x] = packed[q];
+}
+
+// primary-hit dump (config C2): per path slot (kind, index, t)
+__global__ __launch_bounds__(256) void k_dump_hits(Level lv, int n, int32_t* kind, int32_t* index, float* t) {
+    const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const float4 h = lv.hit[i];
+    const uint32_t code = fbits(h.w);
+    kind[i] = static_cast<int32_t>(primKind(code));
+    index[i] = primKind(code) == kMiss ? -1 : static_cast<int32_t>(primIndex(code));
+    t[i] = h.x;
+}
+
+__global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats) {
+    unsigned long long rays = 0, shadows = 0;
+    for (int l = 1; l <= maxLevel; ++l) {
+        rays += static_cast<unsigned long long>(counters[kCntRays + l]);
+        shadows += static_cast<unsigned long long>(counters[kCntShadows + l]);
+    }
+    stats[kStatRays] += rays;
+    stats[kStatShadowRays] += shadows;
+    stats[kStatPrimary] += static_cast<unsigned long long>(counters[kCntRays + 1]);
+    if (counters[kCntOverflow] != 0) stats[kStatOverflow] = 1ull;
+}
+
+// ---------------------------------------------------------------------------------------
+// launch wrappers
+void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st) {
+    const int blocks = (a.nPaths + 255) / 256;
+    hipLaunchKernelGGL(k_raygen, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, a, lv, counters);
+}
+
+void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
+                 unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
+    if (countStats) {
+        hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+    } else {
+        hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+    }
+}
+
+void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
+                  unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
+    if (countStats) {
+        hipLaunchKernelGGL(k_shadow<true>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+    } else {
+        hipLaunchKernelGGL(k_shadow<false>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+    }
+}
+
+void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
+                 const ShadeArgs& a, int grid, hipStream_t st) {
+    if (shader == kShaderWhitted) {
+        hipLaunchKernelGGL(k_shade<kShaderWhitted>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+    } else {
+        hipLaunchKernelGGL(k_shade<kShaderPathTracer>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+    }
+}
+
+void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
+                   const ShadeArgs& a, int grid, hipStream_t st) {
+    if (shader == kShaderWhitted) {
+        hipLaunchKernelGGL(k_resolve<kShaderWhitted>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+    } else {
+        hipLaunchKernelGGL(k_resolve<kShaderPathTracer>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+    }
+}
+
+void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, int32_t* packed, hipStream_t st) {
+    const int blocks = (a.nSlots + 255) / 256;
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, a, res, bitmap, packed);
+}
+
+void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st) {
+    const int blocks = (nSlots + 255) / 256;
+    hipLaunchKernelGGL(k_unpack, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, map, width, nSlots, packed, bitmap);
+}
+
+void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st) {
+    const int blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_dump_hits, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, lv, n, kind, index, t);
+}
+
+void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st) {
+    hipLaunchKernelGGL(k_tally, dim3(1), dim3(1), 0, st, counters, maxLevel, stats);
+}
+
+int traceOccupancyBlocksPerCU() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false>, kBlock, 0) != hipSuccess) n = 4;
+    return n > 0 ? n : 1;
+}
+
+}  // namespace mrt

@@ -1,0 +1,98 @@
+// mrt_kernels.hpp - queue layouts, kernel argument blocks and launch wrappers.
+#pragma once
+
+#include "mrt_device.hpp"
+
+namespace mrt {
+
+constexpr int kShaderWhitted = 1;     // C_wrapper.cpp:155-160
+constexpr int kShaderPathTracer = 2;  // C_wrapper.cpp:162-172
+constexpr int kMaxLevels = 16;        // max ray depth + 2
+
+// device counters (ints): [kCntRays + L] rays of level L, [kCntShadows + L] shadow rays of
+// level L, work-fetch cursors of the persistent trace kernels, overflow flag
+constexpr int kCntRays = 0;
+constexpr int kCntShadows = kMaxLevels;
+constexpr int kCntFetchTrace = 2 * kMaxLevels;
+constexpr int kCntFetchShadow = 3 * kMaxLevels;
+constexpr int kCntOverflow = 4 * kMaxLevels;
+constexpr int kNumCounters = 4 * kMaxLevels + 4;  // 16-byte multiple
+
+// 64-bit statistics accumulated on the device across a frame
+constexpr int kStatRays = 0;        // rays of every level (camera + diffuse + specular + transmission)
+constexpr int kStatShadowRays = 1;  // shadow rays
+constexpr int kStatPrimary = 2;
+constexpr int kStatNodes = 3;       // child node records fetched (counting pass only)
+constexpr int kStatTris = 4;        // triangle tests (counting pass only)
+constexpr int kStatOverflow = 5;
+constexpr int kNumStats = 8;
+
+// One level of the wavefront (SoA queues).
+struct Level {
+    float4* rO;      // origin xyz, w = path key bits
+    float4* rD;      // direction xyz, w = source primitive code bits
+    uint32_t* tree;  // vertex code in the ray tree
+    float4* hit;     // t, u, v, hit primitive code bits
+    int4* vtxA;      // material (-1 terminal), first shadow ray, shadow ray count
+    int4* vtxB;      // child indices in the next level: diffuse, specular, transmission
+    float4* res;     // resolved radiance xyz, w = "intersected light" flag
+    float4* sO;      // shadow ray origin, w = source primitive bits
+    float4* sD;      // shadow ray direction, w = distance to the light
+    float4* sC;      // light contribution Le*cos, w = occluded flag
+    int cap;
+    int shadowCap;
+};
+
+// Work units: rectangles of pixels (a reference tile cut into 8-row bands).  prefix[u] is
+// the first pixel slot of unit u; slots inside a unit are column-major.
+struct PixelMap {
+    const int4* rect;    // x0, y0, width, height
+    const int* prefix;   // nUnits entries
+    int nUnits;
+    int pad;
+};
+
+struct RaygenArgs {
+    GCamera cam;
+    PixelMap map;
+    const float* samplerTable;
+    int width, height;
+    int slotBase;    // first pixel slot of this chunk
+    int nPaths;      // slots in chunk * spp
+    int spp;         // samples processed in this pass
+    int sppTotal;    // samplesPixel of the renderer (decides the pixel sampler)
+    int sampleBase;  // global index of the first sample of this pass
+    int pad;
+};
+
+struct ShadeArgs {
+    int maxDepth;      // RayDepthMax
+    int samplesLight;  // Config::samplesLight
+};
+
+struct AccumArgs {
+    PixelMap map;
+    int width;
+    int slotBase;
+    int nSlots;
+    int spp;
+    int sampleBase;
+    int pad;
+};
+
+void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
+void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
+                 unsigned long long* stats, bool countStats, int grid, hipStream_t st);
+void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
+                  unsigned long long* stats, bool countStats, int grid, hipStream_t st);
+void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
+                 const ShadeArgs& a, int grid, hipStream_t st);
+void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
+                   const ShadeArgs& a, int grid, hipStream_t st);
+void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, int32_t* packed, hipStream_t st);
+void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st);
+void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);
+void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st);
+int traceOccupancyBlocksPerCU();
+
+}  // namespace mrt

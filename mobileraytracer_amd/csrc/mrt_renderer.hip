@@ -1,0 +1,733 @@
+// mrt_renderer.hip - the Renderer (Renderer.cpp) and desktop C-ABI (C_wrapper.cpp) of the
+// MI355X render path: scene upload, wavefront queue memory, the per-frame launch sequence,
+// stop / progress / ray-count bookkeeping and the exported symbols of include/mobilert_amd.h(pp).
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mobilert_amd.h"
+#include "mobilert_amd.hpp"
+#include "mrt_kernels.hpp"
+#include "mrt_scene.hpp"
+
+namespace {
+
+#define MRT_HIP(x)                                                                              \
+    do {                                                                                        \
+        const hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+thread_local std::string gLastError;
+
+struct DeviceMem {
+    std::vector<void*> ptrs;
+    size_t total = 0;
+    template <class T>
+    T* alloc(size_t n) {
+        if (n == 0) n = 1;
+        void* p = nullptr;
+        MRT_HIP(hipMalloc(&p, n * sizeof(T)));
+        ptrs.push_back(p);
+        total += n * sizeof(T);
+        return static_cast<T*>(p);
+    }
+    template <class T>
+    T* upload(const std::vector<T>& v, hipStream_t st) {
+        T* p = alloc<T>(v.size());
+        if (!v.empty()) MRT_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
+        return p;
+    }
+    void release() {
+        for (void* p : ptrs) (void)hipFree(p);
+        ptrs.clear();
+        total = 0;
+    }
+    ~DeviceMem() { release(); }
+};
+
+int bvhDepth(const std::vector<mrt::HBVHNode>& nodes) {
+    if (nodes.empty()) return 0;
+    int best = 0;
+    std::vector<std::pair<int, int>> st{{0, 1}};
+    while (!st.empty()) {
+        const auto [i, d] = st.back();
+        st.pop_back();
+        best = std::max(best, d);
+        const mrt::HBVHNode& n = nodes[static_cast<size_t>(i)];
+        if (n.numPrimitives == 0 && nodes.size() > 1) {
+            st.push_back({n.indexOffset, d + 1});
+            st.push_back({n.indexOffset + 1, d + 1});
+        }
+    }
+    return best;
+}
+
+float4 f4(mrt::v3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
+float asFloat(int32_t i) {
+    float f;
+    std::memcpy(&f, &i, 4);
+    return f;
+}
+
+}  // namespace
+
+struct mrt_renderer {
+    mrt_config cfg{};
+    std::string objPath, mtlPath, camPath;
+    int maxDepth = mrt::kRayDepthMaxDefault;
+    int rankIndex = 0, rankCount = 1;
+    int device = 0;
+
+    // scene
+    mrt::GCamera cam{};
+    mrt::DScene ds{};
+    std::vector<int32_t> triOrder, planeOrder, sphereOrder;
+    int64_t nTri = 0, nLights = 0, nPlanes = 0, nSpheres = 0, nMats = 0, nTriNodes = 0;
+    int triDepth = 0, maxBvhDepth = 0;
+
+    // pixel units of every shard (rank r uses unitsByRank[r])
+    std::vector<std::vector<int4>> unitsByRank;
+    std::vector<std::vector<int>> prefixByRank;
+    std::vector<mrt::PixelMap> mapByRank;
+    int nSlots = 0, maxSlots = 0;
+
+    // queues
+    DeviceMem sceneMem, queueMem;
+    mrt::Level levels[mrt::kMaxLevels]{};
+    int chunkSlots = 0;
+    int* counters = nullptr;
+    unsigned long long* stats = nullptr;
+    int2* gstack = nullptr;
+    int gdepth = 0;
+    int traceGrid = 0, workGrid = 0;
+    int32_t* dBitmap = nullptr;  // for the host-bitmap entry point
+    hipStream_t stream = nullptr;
+
+    // state (Renderer.hpp:30-40)
+    std::atomic<bool> stopFlag{false};
+    std::atomic<int32_t> sample{0};
+    std::atomic<uint64_t> totalRays{0};
+    int profileFlags = 0;
+    mrt_frame_stats last{};
+    std::vector<hipEvent_t> evPool;
+
+    ~mrt_renderer() {
+        for (hipEvent_t e : evPool) (void)hipEventDestroy(e);
+        if (stream != nullptr) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+void buildUnits(mrt_renderer* r) {
+    const int W = r->cfg.width, H = r->cfg.height;
+    const int tilesPerSide = static_cast<int>(std::sqrt(static_cast<double>(mrt::kNumberOfTiles)));
+    const int bx = W / tilesPerSide, by = H / tilesPerSide;  // Renderer.cpp:33-34
+    if (bx <= 0 || by <= 0) throw std::runtime_error("width and height must be >= 16 (Renderer.cpp:33-38)");
+    const int domainSize = (W / bx) * (H / by);
+    const int resolution = W * H;
+    // The reference claims the 256 tiles in a shuffled Halton order; their values are j/256,
+    // so roundBlock = roundf(j/256 * domainSize) (Renderer.cpp:125).  Order is irrelevant here
+    // (per-pixel sample streams), duplicates are rendered once.
+    std::vector<int> blocks;
+    for (int j = 0; j < mrt::kNumberOfTiles; ++j) {
+        const float tile = static_cast<float>(j) / static_cast<float>(mrt::kNumberOfTiles);
+        const int rb = static_cast<int>(::roundf(tile * static_cast<float>(domainSize)));
+        if (std::find(blocks.begin(), blocks.end(), rb) == blocks.end()) blocks.push_back(rb);
+    }
+    std::vector<int4> all;
+    for (int rb : blocks) {
+        const int pixel = rb * bx % resolution;               // Renderer.cpp:126
+        const int startY = ((pixel / W) * by) % H;            // :127
+        const int startX = pixel % W;                         // :133 ((pixel + y*W) % W)
+        for (int b = 0; b * 8 < by; ++b) {
+            int h = std::min(8, by - 8 * b);
+            const int y0 = startY + 8 * b;
+            while (h > 0 && (y0 + h - 1) * W + startX + bx - 1 >= resolution) --h;  // stay inside the bitmap
+            if (h > 0) all.push_back(make_int4(startX, y0, bx, h));
+        }
+    }
+    r->unitsByRank.assign(static_cast<size_t>(r->rankCount), {});
+    r->prefixByRank.assign(static_cast<size_t>(r->rankCount), {});
+    for (size_t u = 0; u < all.size(); ++u) r->unitsByRank[u % static_cast<size_t>(r->rankCount)].push_back(all[u]);
+    r->maxSlots = 0;
+    for (int k = 0; k < r->rankCount; ++k) {
+        int acc = 0;
+        for (const int4& u : r->unitsByRank[static_cast<size_t>(k)]) {
+            r->prefixByRank[static_cast<size_t>(k)].push_back(acc);
+            acc += u.z * u.w;
+        }
+        if (k == r->rankIndex) r->nSlots = acc;
+        r->maxSlots = std::max(r->maxSlots, acc);
+    }
+    r->mapByRank.clear();
+    for (int k = 0; k < r->rankCount; ++k) {
+        mrt::PixelMap m{};
+        m.rect = r->sceneMem.upload(r->unitsByRank[static_cast<size_t>(k)], r->stream);
+        m.prefix = r->sceneMem.upload(r->prefixByRank[static_cast<size_t>(k)], r->stream);
+        m.nUnits = static_cast<int>(r->unitsByRank[static_cast<size_t>(k)].size());
+        r->mapByRank.push_back(m);
+    }
+}
+
+void slotToXYHost(const std::vector<int4>& units, const std::vector<int>& prefix, int slot, int* x, int* y) {
+    const auto it = std::upper_bound(prefix.begin(), prefix.end(), slot);
+    const size_t u = static_cast<size_t>(it - prefix.begin()) - 1;
+    const int off = slot - prefix[u];
+    *x = units[u].x + off / units[u].w;
+    *y = units[u].y + off % units[u].w;
+}
+
+void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
+    using namespace mrt;
+    hipStream_t st = r->stream;
+    std::vector<HBVHNode> pn = buildBVH(&sc.planes, &r->planeOrder);
+    std::vector<HBVHNode> sn = buildBVH(&sc.spheres, &r->sphereOrder);
+    std::vector<HBVHNode> tn = buildBVH(&sc.triangles, &r->triOrder);
+    r->nTri = static_cast<int64_t>(sc.triangles.size());
+    r->nPlanes = static_cast<int64_t>(sc.planes.size());
+    r->nSpheres = static_cast<int64_t>(sc.spheres.size());
+    r->nLights = static_cast<int64_t>(sc.lights.size());
+    r->nMats = static_cast<int64_t>(sc.materials.size());
+    r->nTriNodes = static_cast<int64_t>(tn.size());
+    r->triDepth = bvhDepth(tn);
+    r->maxBvhDepth = std::max({r->triDepth, bvhDepth(pn), bvhDepth(sn)});
+
+    std::vector<GNode> g;
+    DScene& d = r->ds;
+    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot);
+    d.triNodes = r->sceneMem.upload(g, st);
+    toDeviceBVH(pn, sc.planes.size(), &g, &d.planeRoot);
+    d.planeNodes = r->sceneMem.upload(g, st);
+    toDeviceBVH(sn, sc.spheres.size(), &g, &d.sphereRoot);
+    d.sphereNodes = r->sceneMem.upload(g, st);
+
+    std::vector<float4> v;
+    v.reserve(sc.triangles.size() * 3);
+    for (const HTriangle& t : sc.triangles) {
+        v.push_back(f4(t.A, 0.0F));
+        v.push_back(f4(t.AB, 0.0F));
+        v.push_back(f4(t.AC, 0.0F));
+    }
+    d.triGeom = r->sceneMem.upload(v, st);
+    v.clear();
+    for (const HTriangle& t : sc.triangles) {
+        v.push_back(f4(t.nA, asFloat(t.mat)));
+        v.push_back(f4(t.nB, 0.0F));
+        v.push_back(f4(t.nC, 0.0F));
+    }
+    d.triShade = r->sceneMem.upload(v, st);
+    v.clear();
+    for (const HPlane& p : sc.planes) {
+        v.push_back(f4(p.normal, asFloat(p.mat)));
+        v.push_back(f4(p.point, 0.0F));
+    }
+    d.planes = r->sceneMem.upload(v, st);
+    v.clear();
+    for (const HSphere& s : sc.spheres) {
+        v.push_back(f4(s.center, s.sqRadius));
+        v.push_back(make_float4(asFloat(s.mat), 0.0F, 0.0F, 0.0F));
+    }
+    d.spheres = r->sceneMem.upload(v, st);
+    v.clear();
+    for (const HLight& l : sc.lights) {
+        if (l.kind == kAreaLight) {
+            v.push_back(f4(l.tri.A, asFloat(1)));
+            v.push_back(f4(l.tri.AB, 0.0F));
+            v.push_back(f4(l.tri.AC, 0.0F));
+        } else {
+            v.push_back(f4(l.position, asFloat(0)));
+            v.push_back(make_float4(0, 0, 0, 0));
+            v.push_back(make_float4(0, 0, 0, 0));
+        }
+        v.push_back(f4(l.radiance.Le, 0.0F));
+    }
+    d.lights = r->sceneMem.upload(v, st);
+    v.clear();
+    for (const HMaterial& m : sc.materials) {
+        v.push_back(f4(m.Le, m.ior));
+        v.push_back(f4(m.Kd, 0.0F));
+        v.push_back(f4(m.Ks, 0.0F));
+        v.push_back(f4(m.Kt, 0.0F));
+    }
+    d.mats = r->sceneMem.upload(v, st);
+    d.nLights = static_cast<int32_t>(sc.lights.size());
+    d.nMats = static_cast<int32_t>(sc.materials.size());
+    d.cull = r->cfg.cull;
+
+    std::vector<float> table;
+    fillHaltonTable(&table, kSeedShaderTable);
+    d.shaderTable = r->sceneMem.upload(table, st);
+    fillHaltonTable(&table, kSeedSamplerTable);
+    d.samplerTable = r->sceneMem.upload(table, st);
+    MRT_HIP(hipStreamSynchronize(st));
+}
+
+void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
+    using namespace mrt;
+    r->queueMem.release();
+    const int spp = std::max(1, r->cfg.samplesPixel);
+    const int spl = std::max(1, r->cfg.samplesLight);
+    r->chunkSlots = chunkSlots;
+    const size_t n1 = static_cast<size_t>(chunkSlots) * static_cast<size_t>(spp);
+    const size_t capN = n1 * static_cast<size_t>(growth);
+    const int nLevels = r->maxDepth + 1;
+    // ping-pong ray / hit buffers (dead after k_shade of their level)
+    float4* rO[2];
+    float4* rD[2];
+    uint32_t* tree[2];
+    float4* hit[2];
+    for (int k = 0; k < 2; ++k) {
+        rO[k] = r->queueMem.alloc<float4>(capN);
+        rD[k] = r->queueMem.alloc<float4>(capN);
+        tree[k] = r->queueMem.alloc<uint32_t>(capN);
+        hit[k] = r->queueMem.alloc<float4>(capN);
+    }
+    float4* sO = r->queueMem.alloc<float4>(capN * spl);
+    float4* sD = r->queueMem.alloc<float4>(capN * spl);
+    for (int l = 1; l <= nLevels + 1 && l < kMaxLevels; ++l) {
+        Level& lv = r->levels[l];
+        const size_t cap = (l == 1) ? n1 : capN;
+        const bool real = l <= nLevels;
+        lv.cap = real ? static_cast<int>(cap) : 0;
+        lv.shadowCap = real ? static_cast<int>(cap * spl) : 0;
+        lv.rO = rO[l & 1];
+        lv.rD = rD[l & 1];
+        lv.tree = tree[l & 1];
+        lv.hit = hit[l & 1];
+        lv.sO = sO;
+        lv.sD = sD;
+        if (real) {
+            lv.vtxA = r->queueMem.alloc<int4>(cap);
+            lv.vtxB = r->queueMem.alloc<int4>(cap);
+            lv.res = r->queueMem.alloc<float4>(cap);
+            lv.sC = r->queueMem.alloc<float4>(cap * spl);
+        } else {
+            lv.vtxA = nullptr;
+            lv.vtxB = nullptr;
+            lv.res = nullptr;
+            lv.sC = nullptr;
+        }
+    }
+    r->counters = r->queueMem.alloc<int>(kNumCounters);
+    r->stats = r->queueMem.alloc<unsigned long long>(kNumStats);
+    r->gdepth = std::max(1, r->maxBvhDepth + 2 - kLdsStack);
+    r->gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceGrid) * kBlock * static_cast<size_t>(r->gdepth));
+    r->dBitmap = r->queueMem.alloc<int32_t>(static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height));
+    MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * static_cast<size_t>(r->cfg.width) * r->cfg.height, r->stream));
+}
+
+hipEvent_t poolEvent(mrt_renderer* r, size_t i) {
+    while (r->evPool.size() <= i) {
+        hipEvent_t e;
+        MRT_HIP(hipEventCreate(&e));
+        r->evPool.push_back(e);
+    }
+    return r->evPool[i];
+}
+
+// One pass over this shard's pixel slots: samples [sampleBase, sampleBase + spp).
+// Returns false if the queues overflowed (caller grows them and re-renders).
+bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp,
+                size_t* evCount) {
+    using namespace mrt;
+    const int shader = r->cfg.shader == kShaderWhitted ? kShaderWhitted : kShaderPathTracer;
+    const bool timing = (r->profileFlags & 1) != 0;
+    const bool counting = (r->profileFlags & 2) != 0;
+    ShadeArgs sa{r->maxDepth, std::max(1, r->cfg.samplesLight)};
+    const int nLevels = r->maxDepth + 1;
+    const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
+    for (int slot0 = 0; slot0 < r->nSlots; slot0 += r->chunkSlots) {
+        if (r->stopFlag.load()) return true;
+        const int nChunk = std::min(r->chunkSlots, r->nSlots - slot0);
+        MRT_HIP(hipMemsetAsync(r->counters, 0, sizeof(int) * kNumCounters, st));
+        RaygenArgs ra{};
+        ra.cam = r->cam;
+        ra.map = map;
+        ra.samplerTable = r->ds.samplerTable;
+        ra.width = r->cfg.width;
+        ra.height = r->cfg.height;
+        ra.slotBase = slot0;
+        ra.nPaths = nChunk * spp;
+        ra.spp = spp;
+        ra.sppTotal = r->cfg.samplesPixel;
+        ra.sampleBase = sampleBase;
+        launchRaygen(ra, r->levels[1], r->counters, st);
+        for (int l = 1; l <= nLevels; ++l) {
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
+            launchTrace(r->ds, r->levels[l], r->counters, l, r->gstack, r->gdepth, r->stats, counting, r->traceGrid, st);
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
+            launchShade(shader, r->ds, r->levels[l], r->levels[l + 1], r->counters, l, sa, r->workGrid, st);
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
+            launchShadow(r->ds, r->levels[l], r->counters, l, r->gstack, r->gdepth, r->stats, counting, r->traceGrid, st);
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
+        }
+        for (int l = nLevels; l >= 1; --l) {
+            launchResolve(shader, r->ds, r->levels[l], r->levels[l + 1], r->counters, l, sa, r->workGrid, st);
+        }
+        AccumArgs aa{};
+        aa.map = map;
+        aa.width = r->cfg.width;
+        aa.slotBase = slot0;
+        aa.nSlots = nChunk;
+        aa.spp = spp;
+        aa.sampleBase = sampleBase;
+        launchAccumulate(aa, r->levels[1].res, dBitmap, dPacked, st);
+        launchTally(r->counters, nLevels, r->stats, st);
+    }
+    return true;
+}
+
+// Renderer::renderFrame (Renderer.cpp:53-88): samples 0..spp-1, progressive average.
+void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st) {
+    using namespace mrt;
+    r->sample.store(0);
+    if (r->stopFlag.load()) return;  // stopRender zeroes samplesPixel_ (Renderer.cpp:97)
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        MRT_HIP(hipMemsetAsync(r->stats, 0, sizeof(unsigned long long) * kNumStats, st));
+        size_t evCount = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        renderPass(r, dBitmap, dPacked, st, 0, std::max(1, r->cfg.samplesPixel), &evCount);
+        unsigned long long hs[kNumStats];
+        MRT_HIP(hipMemcpyAsync(hs, r->stats, sizeof(hs), hipMemcpyDeviceToHost, st));
+        MRT_HIP(hipStreamSynchronize(st));
+        const auto t1 = std::chrono::steady_clock::now();
+        if (hs[kStatOverflow] != 0) {
+            // wavefront queues overflowed: halve the chunk (more passes, same results) and redo
+            const int slots = std::max(1, r->chunkSlots / 2);
+            allocQueues(r, slots, 2);
+            continue;
+        }
+        mrt_frame_stats fs{};
+        fs.rays = hs[kStatRays];
+        fs.shadowRays = hs[kStatShadowRays];
+        fs.primaryRays = hs[kStatPrimary];
+        fs.nodeRecords = hs[kStatNodes];
+        fs.triTests = hs[kStatTris];
+        fs.frameMs = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if (r->profileFlags & 1) {
+            for (size_t e = 0; e + 3 < evCount; e += 4) {
+                float a = 0.0F, b = 0.0F;
+                MRT_HIP(hipEventElapsedTime(&a, r->evPool[e], r->evPool[e + 1]));
+                MRT_HIP(hipEventElapsedTime(&b, r->evPool[e + 2], r->evPool[e + 3]));
+                fs.traceMs += a;
+                fs.shadowMs += b;
+                fs.traceLaunches += 1;
+                fs.shadowLaunches += 1;
+            }
+        }
+        r->last = fs;
+        r->totalRays.fetch_add(fs.rays + fs.shadowRays);
+        if (!r->stopFlag.load()) r->sample.store(r->cfg.samplesPixel);
+        return;
+    }
+    throw std::runtime_error("wavefront queue overflow persists after shrinking the chunk");
+}
+
+mrt_renderer* createRenderer(const mrt_config* cfg) {
+    using namespace mrt;
+    auto r = std::make_unique<mrt_renderer>();
+    r->cfg = *cfg;
+    r->objPath = cfg->objFilePath ? cfg->objFilePath : "";
+    r->mtlPath = cfg->mtlFilePath ? cfg->mtlFilePath : "";
+    r->camPath = cfg->camFilePath ? cfg->camFilePath : "";
+    r->cfg.objFilePath = r->objPath.c_str();
+    r->cfg.mtlFilePath = r->mtlPath.c_str();
+    r->cfg.camFilePath = r->camPath.c_str();
+    r->maxDepth = cfg->maxDepth > 0 ? cfg->maxDepth : kRayDepthMaxDefault;
+    if (r->maxDepth + 2 >= kMaxLevels) throw std::runtime_error("maxDepth too large");
+    r->rankCount = cfg->rankCount > 0 ? cfg->rankCount : 1;
+    r->rankIndex = cfg->rankIndex;
+    if (r->rankIndex < 0 || r->rankIndex >= r->rankCount) throw std::runtime_error("rankIndex out of range");
+    if (cfg->shader != kShaderWhitted && cfg->shader != kShaderPathTracer)
+        throw std::runtime_error("the GPU path implements shader 1 (Whitted) and 2 (PathTracer)");
+    if (cfg->width < 16 || cfg->height < 16) throw std::runtime_error("width/height must be >= 16");
+    if (cfg->samplesPixel < 1 || cfg->samplesLight < 1) throw std::runtime_error("samplesPixel/samplesLight must be >= 1");
+    if (cfg->device >= 0) MRT_HIP(hipSetDevice(cfg->device));
+    MRT_HIP(hipGetDevice(&r->device));
+    MRT_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    MRT_HIP(hipGetDeviceProperties(&prop, r->device));
+    r->traceGrid = prop.multiProcessorCount * traceOccupancyBlocksPerCU();
+    r->workGrid = prop.multiProcessorCount * 8;
+
+    // scene (C_wrapper.cpp:68-141)
+    const float ratio = static_cast<float>(cfg->width) / static_cast<float>(cfg->height);
+    HScene sc;
+    if (cfg->sceneIndex == 0) {
+        sc = cornellBoxScene();
+        r->cam = cornellBoxCamera(ratio);
+    } else if (cfg->sceneIndex >= 1 && cfg->sceneIndex <= 3) {
+        throw std::runtime_error("built-in scenes 1-3 are outside this path's scope (SURVEY.md section 2)");
+    } else {
+        std::string err;
+        if (!loadObjScene(r->objPath, r->mtlPath, &sc, &err)) throw std::runtime_error(err);
+        if (!loadCameraFile(r->camPath, ratio, &r->cam, &err)) throw std::runtime_error(err);
+    }
+    uploadScene(r.get(), sc);
+    buildUnits(r.get());
+    const size_t spp = static_cast<size_t>(cfg->samplesPixel);
+    size_t maxPaths = cfg->maxPathsPerPass > 0 ? static_cast<size_t>(cfg->maxPathsPerPass) : (size_t{1} << 24);
+    size_t slots = std::max<size_t>(1, std::min<size_t>(static_cast<size_t>(r->nSlots), maxPaths / spp));
+    allocQueues(r.get(), static_cast<int>(slots), 2);
+    MRT_HIP(hipStreamSynchronize(r->stream));
+    return r.release();
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return 0;
+    } catch (const std::exception& e) {
+        gLastError = e.what();
+    } catch (...) {
+        gLastError = "unknown error";
+    }
+    return -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mrt_last_error(void) { return gLastError.c_str(); }
+
+int mrt_create(const mrt_config* cfg, mrt_renderer** out) {
+    *out = nullptr;
+    return guarded([&] { *out = createRenderer(cfg); });
+}
+
+void mrt_destroy(mrt_renderer* r) {
+    if (r != nullptr) {
+        (void)hipStreamSynchronize(r->stream);
+        delete r;
+    }
+}
+
+int mrt_render_frame(mrt_renderer* r, int32_t* bitmap) {
+    return guarded([&] {
+        const size_t n = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
+        MRT_HIP(hipMemcpyAsync(r->dBitmap, bitmap, n * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
+        renderFrameDevice(r, r->dBitmap, nullptr, r->stream);
+        MRT_HIP(hipMemcpyAsync(bitmap, r->dBitmap, n * sizeof(int32_t), hipMemcpyDeviceToHost, r->stream));
+        MRT_HIP(hipStreamSynchronize(r->stream));
+    });
+}
+
+int mrt_render_frame_device(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, void* stream) {
+    return guarded([&] {
+        hipStream_t st = stream != nullptr ? static_cast<hipStream_t>(stream) : r->stream;
+        renderFrameDevice(r, dBitmap, dPacked, st);
+    });
+}
+
+int mrt_unpack_gathered(mrt_renderer* r, const int32_t* dGathered, int32_t* dBitmap, void* stream) {
+    return guarded([&] {
+        hipStream_t st = stream != nullptr ? static_cast<hipStream_t>(stream) : r->stream;
+        for (int k = 0; k < r->rankCount; ++k) {
+            const auto& pre = r->prefixByRank[static_cast<size_t>(k)];
+            const auto& un = r->unitsByRank[static_cast<size_t>(k)];
+            int n = 0;
+            if (!un.empty()) n = pre.back() + un.back().z * un.back().w;
+            mrt::launchUnpack(r->mapByRank[static_cast<size_t>(k)], r->cfg.width, n,
+                              dGathered + static_cast<size_t>(k) * static_cast<size_t>(r->maxSlots), dBitmap, st);
+        }
+        MRT_HIP(hipStreamSynchronize(st));
+    });
+}
+
+int mrt_stop_render(mrt_renderer* r) {
+    r->stopFlag.store(true);
+    return 0;
+}
+
+int32_t mrt_get_sample(const mrt_renderer* r) { return r->sample.load(); }
+
+uint64_t mrt_get_total_casted_rays(const mrt_renderer* r) { return r->totalRays.load(); }
+
+int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
+    info->triangles = r->nTri;
+    info->lights = r->nLights;
+    info->planes = r->nPlanes;
+    info->spheres = r->nSpheres;
+    info->materials = r->nMats;
+    info->triangleNodes = r->nTriNodes;
+    info->triangleBvhDepth = r->triDepth;
+    info->pixelSlots = r->nSlots;
+    info->pixelSlotsMax = r->maxSlots;
+    info->deviceBytes = static_cast<int64_t>(r->sceneMem.total + r->queueMem.total);
+    return 0;
+}
+
+int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
+    r->profileFlags = flags;
+    return 0;
+}
+
+int mrt_get_frame_stats(const mrt_renderer* r, mrt_frame_stats* s) {
+    *s = r->last;
+    return 0;
+}
+
+int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
+    return guarded([&] {
+        using namespace mrt;
+        hipStream_t st = r->stream;
+        const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
+        for (size_t i = 0; i < npx; ++i) {
+            kind[i] = -1;
+            index[i] = -1;
+            t[i] = 0.0F;
+        }
+        const auto& units = r->unitsByRank[static_cast<size_t>(r->rankIndex)];
+        const auto& prefix = r->prefixByRank[static_cast<size_t>(r->rankIndex)];
+        const int cap = r->levels[1].cap;
+        int32_t* dk = static_cast<int32_t*>(nullptr);
+        int32_t* di = nullptr;
+        float* dt = nullptr;
+        MRT_HIP(hipMalloc(&dk, sizeof(int32_t) * static_cast<size_t>(cap)));
+        MRT_HIP(hipMalloc(&di, sizeof(int32_t) * static_cast<size_t>(cap)));
+        MRT_HIP(hipMalloc(&dt, sizeof(float) * static_cast<size_t>(cap)));
+        std::vector<int32_t> hk(static_cast<size_t>(cap)), hi(static_cast<size_t>(cap));
+        std::vector<float> ht(static_cast<size_t>(cap));
+        try {
+            for (int slot0 = 0; slot0 < r->nSlots; slot0 += cap) {
+                const int n = std::min(cap, r->nSlots - slot0);
+                MRT_HIP(hipMemsetAsync(r->counters, 0, sizeof(int) * kNumCounters, st));
+                RaygenArgs ra{};
+                ra.cam = r->cam;
+                ra.map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
+                ra.samplerTable = r->ds.samplerTable;
+                ra.width = r->cfg.width;
+                ra.height = r->cfg.height;
+                ra.slotBase = slot0;
+                ra.nPaths = n;
+                ra.spp = 1;
+                ra.sppTotal = r->cfg.samplesPixel;
+                ra.sampleBase = 0;
+                launchRaygen(ra, r->levels[1], r->counters, st);
+                launchTrace(r->ds, r->levels[1], r->counters, 1, r->gstack, r->gdepth, r->stats, false, r->traceGrid, st);
+                launchDumpHits(r->levels[1], n, dk, di, dt, st);
+                MRT_HIP(hipMemcpyAsync(hk.data(), dk, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+                MRT_HIP(hipMemcpyAsync(hi.data(), di, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+                MRT_HIP(hipMemcpyAsync(ht.data(), dt, sizeof(float) * n, hipMemcpyDeviceToHost, st));
+                MRT_HIP(hipStreamSynchronize(st));
+                for (int q = 0; q < n; ++q) {
+                    int x, y;
+                    slotToXYHost(units, prefix, slot0 + q, &x, &y);
+                    const size_t pix = static_cast<size_t>(y) * static_cast<size_t>(r->cfg.width) + static_cast<size_t>(x);
+                    int32_t k = hk[static_cast<size_t>(q)], idx = hi[static_cast<size_t>(q)];
+                    if (k == kTriangle) idx = r->triOrder[static_cast<size_t>(idx)];
+                    if (k == kPlane) idx = r->planeOrder[static_cast<size_t>(idx)];
+                    if (k == kSphere) idx = r->sphereOrder[static_cast<size_t>(idx)];
+                    kind[pix] = k;
+                    index[pix] = idx;
+                    t[pix] = ht[static_cast<size_t>(q)];
+                }
+            }
+        } catch (...) {
+            (void)hipFree(dk);
+            (void)hipFree(di);
+            (void)hipFree(dt);
+            throw;
+        }
+        (void)hipFree(dk);
+        (void)hipFree(di);
+        (void)hipFree(dt);
+    });
+}
+
+}  // extern "C"
+
+// ---- desktop C-ABI (C_wrapper.cpp:268-290) ---------------------------------------------------
+namespace {
+std::mutex gRendererMutex;
+mrt_renderer* gRenderer = nullptr;
+
+void workThread(::MobileRT::Config& config) {
+    try {
+        mrt_config c{};
+        c.width = config.width;
+        c.height = config.height;
+        c.threads = config.threads;
+        c.shader = config.shader;
+        c.sceneIndex = config.sceneIndex;
+        c.samplesPixel = config.samplesPixel;
+        c.samplesLight = config.samplesLight;
+        c.repeats = config.repeats;
+        c.accelerator = config.accelerator;
+        c.printStdOut = config.printStdOut ? 1 : 0;
+        c.objFilePath = config.objFilePath.c_str();
+        c.mtlFilePath = config.mtlFilePath.c_str();
+        c.camFilePath = config.camFilePath.c_str();
+        const char* md = std::getenv("MOBILERT_MAX_DEPTH");
+        c.maxDepth = md != nullptr ? std::atoi(md) : 0;
+        const char* dev = std::getenv("MOBILERT_DEVICE");
+        c.device = dev != nullptr ? std::atoi(dev) : -1;
+        c.rankCount = 1;
+        c.cull = 1;
+        const auto tc0 = std::chrono::steady_clock::now();
+        mrt_renderer* r = createRenderer(&c);
+        const auto tc1 = std::chrono::steady_clock::now();
+        {
+            std::lock_guard<std::mutex> lock(gRendererMutex);
+            gRenderer = r;
+        }
+        int32_t repeats = config.repeats;
+        const auto t0 = std::chrono::steady_clock::now();
+        do {  // C_wrapper.cpp:227-233
+            const size_t n = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
+            MRT_HIP(hipMemcpyAsync(r->dBitmap, config.bitmap.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
+            renderFrameDevice(r, r->dBitmap, nullptr, r->stream);
+            MRT_HIP(hipMemcpyAsync(config.bitmap.data(), r->dBitmap, n * sizeof(int32_t), hipMemcpyDeviceToHost, r->stream));
+            MRT_HIP(hipStreamSynchronize(r->stream));
+            repeats--;
+        } while (repeats > 0);
+        const auto t1 = std::chrono::steady_clock::now();
+        const double secs = std::chrono::duration<double>(t1 - t0).count();
+        const uint64_t rays = r->totalRays.load();
+        if (config.printStdOut) {
+            std::printf("TRIANGLES = %lld\nLIGHTS = %lld\n", static_cast<long long>(r->nTri), static_cast<long long>(r->nLights));
+            std::printf("Creating Time in secs = %f\n", std::chrono::duration<double>(tc1 - tc0).count());
+            std::printf("Rendering Time in secs = %f\n", secs);
+            std::printf("Casted rays = %llu\n", static_cast<unsigned long long>(rays));
+            std::printf("width = %d\nheight = %d\n", config.width, config.height);
+            std::printf("Total Millions rays per second = %f\n", (static_cast<double>(rays) / secs) / 1000000.0);
+            std::fflush(stdout);
+        }
+        {
+            std::lock_guard<std::mutex> lock(gRendererMutex);
+            gRenderer = nullptr;
+        }
+        mrt_destroy(r);  // C_wrapper.cpp:265
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "exception: %s\n", e.what());  // C_wrapper.cpp:257-263
+    }
+}
+}  // namespace
+
+extern "C" void RayTrace(::MobileRT::Config& config, bool async) {
+    if (async) {
+        std::thread th(workThread, std::ref(config));
+        th.detach();
+    } else {
+        workThread(config);
+    }
+}
+
+extern "C" void stopRender() {
+    std::lock_guard<std::mutex> lock(gRendererMutex);
+    if (gRenderer != nullptr) gRenderer->stopFlag.store(true);
+}

@@ -1,0 +1,754 @@
+// mrt_scene.cpp - host-side scene assembly (see mrt_scene.hpp).
+#include "mrt_scene.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <random>
+#include <sstream>
+#include <unordered_map>
+
+namespace mrt {
+
+// ---- materials ----------------------------------------------------------------------------
+namespace {
+bool feq(float a, float b) { return std::fabs(a - b) < kEpsilon; }  // Utils.cpp:133-137
+bool veq(v3 a, v3 b) { return feq(a.x, b.x) && feq(a.y, b.y) && feq(a.z, b.z); }
+}  // namespace
+
+bool materialEqual(const HMaterial& a, const HMaterial& b) {
+    return veq(a.Kd, b.Kd) && veq(a.Ks, b.Ks) && veq(a.Kt, b.Kt) && veq(a.Le, b.Le) && feq(a.ior, b.ior) &&
+           a.texture == b.texture;
+}
+
+static HMaterial material(v3 kd, v3 ks = v3{0, 0, 0}, v3 kt = v3{0, 0, 0}, float ior = 1.0F, v3 le = v3{0, 0, 0}) {
+    HMaterial m;
+    m.Kd = kd;
+    m.Ks = ks;
+    m.Kt = kt;
+    m.ior = ior;
+    m.Le = le;
+    return m;
+}
+
+// ---- primitives -----------------------------------------------------------------------
+HTriangle makeTriangle(v3 a, v3 b, v3 c) {
+    const v3 ac = c - a;
+    const v3 ab = b - a;
+    const v3 n = normalize(cross(ac, ab));  // Triangle.cpp:336-338
+    return makeTriangle(a, b, c, n, n, n, v2{-1, -1}, v2{-1, -1}, v2{-1, -1}, -1);
+}
+
+HTriangle makeTriangle(v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc, v2 ta, v2 tb, v2 tc, int32_t mat) {
+    HTriangle t;
+    t.AC = c - a;
+    t.AB = b - a;
+    t.A = a;
+    t.nA = normalize(na);  // Triangle.cpp:18-20: the ctor normalises again
+    t.nB = normalize(nb);
+    t.nC = normalize(nc);
+    t.tA = ta;
+    t.tB = tb;
+    t.tC = tc;
+    t.mat = mat;
+    return t;
+}
+
+HPlane makePlane(v3 point, v3 normal, int32_t mat) { return HPlane{normalize(normal), point, mat}; }
+
+HSphere makeSphere(v3 center, float radius, int32_t mat) { return HSphere{center, radius * radius, mat}; }
+
+HAABB aabbOf(const HTriangle& t) {
+    const v3 b = t.A + t.AB;
+    const v3 c = t.A + t.AC;
+    return HAABB{vmin(t.A, vmin(b, c)), vmax(t.A, vmax(b, c))};
+}
+
+HAABB aabbOf(const HPlane& p) {
+    v3 right{0, 0, 0};  // Plane.cpp:79-96 getRightVector
+    const v3 n = p.normal;
+    if (n.x >= 1) {
+        right = v3{0, 1, 1};
+    } else if (n.y >= 1) {
+        right = v3{1, 0, 1};
+    } else if (n.z >= 1) {
+        right = v3{1, 1, 0};
+    } else if (n.x <= -1) {
+        right = v3{0, 1, 1};
+    } else if (n.y <= -1) {
+        right = v3{1, 0, 1};
+    } else if (n.z <= -1) {
+        right = v3{1, 1, 0};
+    }
+    right = normalize(right);
+    return HAABB{p.point + right * -100.0F, p.point + right * 100.0F};
+}
+
+HAABB aabbOf(const HSphere& s) {
+    const float r = std::sqrt(s.sqRadius);
+    return HAABB{v3{s.center.x - r, s.center.y - r, s.center.z - r}, v3{s.center.x + r, s.center.y + r, s.center.z + r}};
+}
+
+bool aabbIntersect(const HAABB& b, v3 o, v3 d) {
+    const float invX = 1.0F / d.x;
+    const float t1x = (b.mn.x - o.x) * invX;
+    const float t2x = (b.mx.x - o.x) * invX;
+    float tMin = stdmin(t1x, t2x);
+    float tMax = stdmax(t1x, t2x);
+    for (int axis = 1; axis < 3; ++axis) {
+        const float inv = 1.0F / comp(d, axis);
+        const float org = comp(o, axis);
+        const float t1 = (comp(b.mn, axis) - org) * inv;
+        const float t2 = (comp(b.mx, axis) - org) * inv;
+        tMin = stdmax(tMin, stdmin(t1, t2));
+        tMax = stdmin(tMax, stdmax(t1, t2));
+    }
+    return tMax >= stdmax(tMin, 0.0F);
+}
+
+// ---- built-in Cornell box (Scenes.cpp:19-150) -----------------------------------------
+HScene cornellBoxScene() {
+    HScene s;
+    const HMaterial lightMat = material(v3{0, 0, 0}, v3{0, 0, 0}, v3{0, 0, 0}, 1.0F, v3{0.9F, 0.9F, 0.9F});
+    const HMaterial mirrorMat = material(v3{0, 0, 0}, v3{0.9F, 0.9F, 0.9F}, v3{0, 0, 0}, 1.0F);
+    const HMaterial lightGrayMat = material(v3{0.7F, 0.7F, 0.7F});
+    const HMaterial redMat = material(v3{0.9F, 0.0F, 0.0F});
+    const HMaterial yellowMat = material(v3{0.9F, 0.9F, 0.0F});
+    const HMaterial greenMat = material(v3{0.0F, 0.9F, 0.0F});
+    const HMaterial blueMat = material(v3{0.0F, 0.0F, 0.9F});
+    const HMaterial lightBlueMat = material(v3{0.0F, 0.9F, 0.9F});
+
+    HLight light;
+    light.kind = kPointLight;
+    light.radiance = lightMat;
+    light.position = v3{0.0F, 0.99F, 0.0F};
+    s.lights.push_back(light);
+
+    HTriangle tri = makeTriangle(v3{0.5F, -0.5F, 0.99F}, v3{0.5F, 0.5F, 1.001F}, v3{-0.5F, -0.5F, 0.99F});
+    tri.mat = static_cast<int32_t>(s.materials.size());
+    s.triangles.push_back(tri);
+    s.materials.push_back(yellowMat);
+
+    s.spheres.push_back(makeSphere(v3{0.45F, -0.65F, 0.4F}, 0.35F, static_cast<int32_t>(s.materials.size())));
+    s.materials.push_back(mirrorMat);
+    s.spheres.push_back(makeSphere(v3{-0.45F, -0.1F, 0.0F}, 0.35F, static_cast<int32_t>(s.materials.size())));
+    s.materials.push_back(greenMat);
+
+    const v3 back{0, 0, 1}, front{0, 0, -1}, bottom{0, -1, 0}, top{0, 1, 0};
+    auto addPlane = [&s](v3 p, v3 n, const HMaterial& m) {
+        s.planes.push_back(makePlane(p, n, static_cast<int32_t>(s.materials.size())));
+        s.materials.push_back(m);
+    };
+    addPlane(back, front, lightGrayMat);
+    addPlane(v3{0.0F, 0.0F, -3.5F}, v3{0.0F, 0.0F, 1.0F}, lightBlueMat);
+    addPlane(bottom, top, lightGrayMat);
+    addPlane(top, bottom, lightGrayMat);
+    addPlane(v3{-1.0F, 0.0F, 0.0F}, v3{1.0F, 0.0F, 0.0F}, redMat);
+    addPlane(v3{1.0F, 0.0F, 0.0F}, v3{-1.0F, 0.0F, 0.0F}, blueMat);
+    return s;
+}
+
+GCamera makePerspective(v3 position, v3 lookAt, v3 up, float hFovDeg, float vFovDeg) {
+    GCamera c{};
+    c.position = position;
+    c.direction = normalize(lookAt - position);  // Camera.cpp:14-19
+    c.right = cross(up, c.direction);
+    c.up = cross(c.direction, c.right);
+    c.hFov = (hFovDeg * kPi) / 180.0F;  // Camera.cpp:30-33 degToRad
+    c.vFov = (vFovDeg * kPi) / 180.0F;
+    c.kind = 0;
+    return c;
+}
+
+GCamera cornellBoxCamera(float ratio) {
+    const float fovX = 45.0F * ratio;
+    return makePerspective(v3{0.0F, 0.0F, -3.4F}, v3{0.0F, 0.0F, 1.0F}, v3{0.0F, 1.0F, 0.0F}, fovX, 45.0F);
+}
+
+// ---- camera file (CameraFactory.cpp, PerspectiveLoader.cpp:18-64) ---------------------
+static bool parseFloats(const std::string& s, float* out, int n) {
+    std::istringstream ss(s);
+    for (int i = 0; i < n; ++i) {
+        float v = 0.0F;
+        if (!(ss >> v)) {
+            return false;
+        }
+        out[i] = v;
+    }
+    return true;
+}
+
+bool loadCameraFile(const std::string& path, float ratio, GCamera* out, std::string* err) {
+    std::ifstream f(path);
+    if (!f) {
+        *err = "cannot open camera file " + path;
+        return false;
+    }
+    std::string line;
+    bool perspective = false;
+    while (std::getline(f, line)) {
+        if (!line.empty() && line[0] == 't' && line.find("perspective") != std::string::npos) {
+            perspective = true;
+            break;
+        }
+    }
+    if (!perspective) {
+        *err = "camera file has no perspective camera: " + path;
+        return false;
+    }
+    float p[3] = {0, 0, 0}, l[3] = {0, 0, 0}, u[3] = {0, 0, 0}, fov[2] = {0, 0};
+    while (std::getline(f, line)) {
+        if (line.empty()) continue;
+        const char key = line[0];
+        const std::string rest = line.substr(1);
+        switch (key) {
+            case 'p': parseFloats(rest, p, 3); break;
+            case 'l': parseFloats(rest, l, 3); break;
+            case 'u': parseFloats(rest, u, 3); break;
+            case 'f': parseFloats(rest, fov, 2); break;
+            default: break;
+        }
+    }
+    p[0] = -p[0];  // PerspectiveLoader.cpp:52 "Invert X axis"
+    *out = makePerspective(v3{p[0], p[1], p[2]}, v3{l[0], l[1], l[2]}, v3{u[0], u[1], u[2]}, fov[0] * ratio, fov[1]);
+    return true;
+}
+
+// ---- Wavefront OBJ/MTL (tinyobjloader v1.0.7 semantics, OBJLoader.cpp) ----------------
+namespace {
+
+bool isSpace(char c) { return c == ' ' || c == '\t'; }
+bool isDigit(char c) { return c >= '0' && c <= '9'; }
+
+// tinyobjloader tryParseDouble: digits accumulated into a double mantissa, fraction digits
+// added with a power-of-ten lookup table, exponent applied with ldexp/pow(5).
+bool tryParseDouble(const char* s, const char* end, double* result) {
+    if (s >= end) return false;
+    double mantissa = 0.0;
+    int exponent = 0;
+    char sign = '+';
+    char expSign = '+';
+    const char* curr = s;
+    int read = 0;
+    bool endNotReached = false;
+    if (*curr == '+' || *curr == '-') {
+        sign = *curr;
+        curr++;
+    } else if (!isDigit(*curr) && *curr != '.') {
+        return false;
+    }
+    endNotReached = (curr != end);
+    while (endNotReached && isDigit(*curr)) {
+        mantissa *= 10;
+        mantissa += static_cast<int>(*curr - 0x30);
+        curr++;
+        read++;
+        endNotReached = (curr != end);
+    }
+    if (!endNotReached) goto assemble;
+    if (*curr == '.') {
+        curr++;
+        read = 1;
+        endNotReached = (curr != end);
+        while (endNotReached && isDigit(*curr)) {
+            static const double powLut[] = {1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001};
+            const int lutEntries = sizeof powLut / sizeof powLut[0];
+            mantissa += static_cast<int>(*curr - 0x30) * (read < lutEntries ? powLut[read] : std::pow(10.0, -read));
+            read++;
+            curr++;
+            endNotReached = (curr != end);
+        }
+    } else if (*curr == 'e' || *curr == 'E') {
+    } else {
+        goto assemble;
+    }
+    if (!endNotReached) goto assemble;
+    if (*curr == 'e' || *curr == 'E') {
+        curr++;
+        endNotReached = (curr != end);
+        if (endNotReached && (*curr == '+' || *curr == '-')) {
+            expSign = *curr;
+            curr++;
+        } else if (endNotReached && isDigit(*curr)) {
+        } else {
+            return false;
+        }
+        read = 0;
+        endNotReached = (curr != end);
+        while (endNotReached && isDigit(*curr)) {
+            exponent *= 10;
+            exponent += static_cast<int>(*curr - 0x30);
+            curr++;
+            read++;
+            endNotReached = (curr != end);
+        }
+        exponent *= (expSign == '+' ? 1 : -1);
+        if (read == 0) return false;
+    }
+assemble:
+    *result = (sign == '+' ? 1 : -1) *
+              (exponent ? std::ldexp(mantissa * std::pow(5.0, exponent), exponent) : mantissa);
+    return true;
+}
+
+// tinyobj parseReal: skip spaces, token until space/end, tryParseDouble, cast to float
+float parseReal(const char** token, double def = 0.0) {
+    const char* t = *token;
+    while (isSpace(*t)) t++;
+    const char* end = t;
+    while (*end && !isSpace(*end) && *end != '\r' && *end != '\n') end++;
+    double val = def;
+    tryParseDouble(t, end, &val);
+    *token = end;
+    return static_cast<float>(val);
+}
+
+// tinyobj fixIndex: 1-based -> 0-based, negative -> relative
+int fixIndex(int idx, int n) {
+    if (idx > 0) return idx - 1;
+    if (idx == 0) return 0;
+    return n + idx;
+}
+
+struct RawMat {
+    std::string name;
+    float diffuse[3] = {0, 0, 0}, specular[3] = {0, 0, 0}, transmittance[3] = {0, 0, 0}, emission[3] = {0, 0, 0};
+    float ior = 1.0F, dissolve = 1.0F;
+    std::string diffuseTex;
+};
+
+void parseMtl(std::istream& in, std::vector<RawMat>* mats, std::unordered_map<std::string, int>* names) {
+    RawMat m;
+    bool hasName = false;
+    bool hasD = false;
+    std::string line;
+    while (std::getline(in, line)) {
+        while (!line.empty() && (line.back() == '\r' || line.back() == '\n')) line.pop_back();
+        const char* t = line.c_str();
+        while (isSpace(*t)) t++;
+        if (*t == '\0' || *t == '#') continue;
+        auto key = [&t](const char* k) {
+            const size_t n = std::strlen(k);
+            return std::strncmp(t, k, n) == 0 && isSpace(t[n]);
+        };
+        auto real3 = [](const char* p, float* v) {
+            v[0] = parseReal(&p);
+            v[1] = parseReal(&p);
+            v[2] = parseReal(&p);
+        };
+        if (key("newmtl")) {
+            if (hasName) {
+                (*names)[m.name] = static_cast<int>(mats->size());
+                mats->push_back(m);
+            }
+            m = RawMat();
+            hasD = false;
+            const char* p = t + 7;
+            while (isSpace(*p)) p++;
+            m.name = p;
+            hasName = true;
+        } else if (key("Kd")) {
+            real3(t + 3, m.diffuse);
+        } else if (key("Ks")) {
+            real3(t + 3, m.specular);
+        } else if (key("Kt") || key("Tf")) {
+            real3(t + 3, m.transmittance);
+        } else if (key("Ke")) {
+            real3(t + 3, m.emission);
+        } else if (key("Ni")) {
+            const char* p = t + 3;
+            m.ior = parseReal(&p);
+        } else if (key("d")) {
+            const char* p = t + 2;
+            m.dissolve = parseReal(&p);
+            hasD = true;
+        } else if (key("Tr")) {
+            const char* p = t + 3;
+            if (!hasD) m.dissolve = 1.0F - parseReal(&p);
+        } else if (key("map_Kd")) {
+            const char* p = t + 7;
+            while (isSpace(*p)) p++;
+            m.diffuseTex = p;
+        }
+    }
+    if (hasName) {
+        (*names)[m.name] = static_cast<int>(mats->size());
+        mats->push_back(m);
+    }
+}
+
+struct FaceIdx {
+    int v, vt, vn;
+};
+
+// Utils.cpp:189-196 normalize(color)
+v3 normalizeColor(v3 c) {
+    const float mx = stdmax(stdmax(c.x, c.y), c.z);
+    if (mx > 1.0F) return c / mx;
+    return c;
+}
+
+}  // namespace
+
+bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene* scene, std::string* err) {
+    std::vector<RawMat> mats;
+    std::unordered_map<std::string, int> names;
+    {
+        std::ifstream mf(mtlPath);
+        if (mf) parseMtl(mf, &mats, &names);
+    }
+    std::ifstream f(objPath);
+    if (!f) {
+        *err = "cannot open OBJ file " + objPath;
+        return false;
+    }
+    std::vector<float> vs, vns, vts, cols;
+    vs.reserve(1 << 20);
+    cols.reserve(1 << 20);
+    struct Tri {
+        FaceIdx i[3];
+        int mat;
+    };
+    std::vector<Tri> tris;
+    tris.reserve(1 << 20);
+    int currentMat = -1;
+    std::string line;
+    std::vector<FaceIdx> face;
+    while (std::getline(f, line)) {
+        while (!line.empty() && (line.back() == '\r' || line.back() == '\n')) line.pop_back();
+        const char* t = line.c_str();
+        while (isSpace(*t)) t++;
+        if (*t == '\0' || *t == '#') continue;
+        if (t[0] == 'v' && isSpace(t[1])) {
+            const char* p = t + 2;
+            const float x = parseReal(&p), y = parseReal(&p), z = parseReal(&p);
+            // parseVertexWithColor: colours default to 1 when absent
+            const float r = parseReal(&p, 1.0), g = parseReal(&p, 1.0), b = parseReal(&p, 1.0);
+            vs.push_back(x);
+            vs.push_back(y);
+            vs.push_back(z);
+            cols.push_back(r);
+            cols.push_back(g);
+            cols.push_back(b);
+        } else if (t[0] == 'v' && t[1] == 'n' && isSpace(t[2])) {
+            const char* p = t + 3;
+            vns.push_back(parseReal(&p));
+            vns.push_back(parseReal(&p));
+            vns.push_back(parseReal(&p));
+        } else if (t[0] == 'v' && t[1] == 't' && isSpace(t[2])) {
+            const char* p = t + 3;
+            vts.push_back(parseReal(&p));
+            vts.push_back(parseReal(&p));
+        } else if (t[0] == 'f' && isSpace(t[1])) {
+            face.clear();
+            const char* p = t + 2;
+            const int nv = static_cast<int>(vs.size() / 3), nt = static_cast<int>(vts.size() / 2),
+                      nn = static_cast<int>(vns.size() / 3);
+            while (true) {
+                while (isSpace(*p)) p++;
+                if (*p == '\0') break;
+                FaceIdx fi{-1, -1, -1};
+                fi.v = fixIndex(std::atoi(p), nv);
+                while (*p && *p != '/' && !isSpace(*p)) p++;
+                if (*p == '/') {
+                    p++;
+                    if (*p == '/') {
+                        p++;
+                        fi.vn = fixIndex(std::atoi(p), nn);
+                        while (*p && !isSpace(*p)) p++;
+                    } else {
+                        fi.vt = fixIndex(std::atoi(p), nt);
+                        while (*p && *p != '/' && !isSpace(*p)) p++;
+                        if (*p == '/') {
+                            p++;
+                            fi.vn = fixIndex(std::atoi(p), nn);
+                            while (*p && !isSpace(*p)) p++;
+                        }
+                    }
+                }
+                face.push_back(fi);
+            }
+            // tinyobjloader v1.0.7 triangulation: fan around the first vertex
+            for (size_t k = 2; k < face.size(); ++k) {
+                tris.push_back(Tri{{face[0], face[k - 1], face[k]}, currentMat});
+            }
+        } else if (std::strncmp(t, "usemtl", 6) == 0 && isSpace(t[6])) {
+            const char* p = t + 7;
+            while (isSpace(*p)) p++;
+            std::string name(p);
+            while (!name.empty() && isSpace(name.back())) name.pop_back();
+            auto it = names.find(name);
+            currentMat = (it == names.end()) ? -1 : it->second;
+        }
+    }
+
+    const bool hasNormals = !vns.empty();
+    auto vert = [&vs](int i) { return v3{-vs[3 * i], vs[3 * i + 1], vs[3 * i + 2]}; };  // OBJLoader.cpp:139-141
+    auto nrm = [&vns](int i) { return v3{-vns[3 * i], vns[3 * i + 1], vns[3 * i + 2]}; }; // :170-172
+    const v2 noTex{-1.0F, -1.0F};
+    scene->triangles.reserve(scene->triangles.size() + tris.size());
+    for (const Tri& tr : tris) {
+        const v3 a = vert(tr.i[0].v), b = vert(tr.i[1].v), c = vert(tr.i[2].v);
+        v3 na, nb, nc;
+        if (hasNormals && tr.i[0].vn >= 0 && tr.i[1].vn >= 0 && tr.i[2].vn >= 0) {
+            na = nrm(tr.i[0].vn);
+            nb = nrm(tr.i[1].vn);
+            nc = nrm(tr.i[2].vn);
+        } else {
+            const v3 ab = b - a, ac = c - a;
+            na = nb = nc = normalize(cross(ac, ab));  // OBJLoader.cpp:176-182
+        }
+        HMaterial m;
+        if (tr.mat >= 0) {
+            const RawMat& rm = mats[static_cast<size_t>(tr.mat)];
+            m.Kd = v3{rm.diffuse[0], rm.diffuse[1], rm.diffuse[2]};
+            m.Ks = v3{rm.specular[0], rm.specular[1], rm.specular[2]};
+            m.Kt = v3{rm.transmittance[0], rm.transmittance[1], rm.transmittance[2]} * (1.0F - rm.dissolve);
+            m.Le = normalizeColor(v3{rm.emission[0], rm.emission[1], rm.emission[2]});
+            m.ior = rm.ior;
+            m.texture = "";  // textures are not sampled on this path
+        } else {
+            const int vi = tr.i[0].v;  // OBJLoader.cpp:423-433 vertex colour of the first vertex
+            m.Kd = v3{cols[3 * vi], cols[3 * vi + 1], cols[3 * vi + 2]};
+        }
+        if (tr.mat >= 0 && hasPositive(m.Le)) {
+            HLight l;
+            l.kind = kAreaLight;
+            l.radiance = m;
+            l.position = v3{0, 0, 0};
+            l.tri = makeTriangle(a, b, c, na, nb, nc, noTex, noTex, noTex, -1);
+            scene->lights.push_back(l);
+            continue;
+        }
+        int32_t matIndex = -1;
+        for (size_t k = 0; k < scene->materials.size(); ++k) {  // OBJLoader.cpp:406-418
+            if (materialEqual(scene->materials[k], m)) {
+                matIndex = static_cast<int32_t>(k);
+                break;
+            }
+        }
+        if (matIndex < 0) {
+            matIndex = static_cast<int32_t>(scene->materials.size());
+            scene->materials.push_back(m);
+        }
+        scene->triangles.push_back(makeTriangle(a, b, c, na, nb, nc, noTex, noTex, noTex, matIndex));
+    }
+    return true;
+}
+
+// ---- BVH build (BVH.hpp:126-283, 398-460) ------------------------------------------------
+namespace {
+
+float surfaceArea(const HAABB& b) {  // AABB.cpp:61-71
+    const v3 l = b.mx - b.mn;
+    const float bottomTop = 2.0F * l.x * l.z;
+    const float sideXY = 2.0F * l.x * l.y;
+    const float sideZY = 2.0F * l.z * l.y;
+    return bottomTop + sideXY + sideZY;
+}
+
+v3 centroid(const HAABB& b) {  // AABB.cpp:81-85
+    const v3 len = (b.mx - b.mn) / 2.0F;
+    return b.mn + len;
+}
+
+HAABB surrounding(const HAABB& a, const HAABB& b) { return HAABB{vmin(a.mn, b.mn), vmax(a.mx, b.mx)}; }
+
+int32_t splitIndexSah(const std::vector<HAABB>& boxes) {  // BVH.hpp:398-439
+    const long numberBoxes = static_cast<long>(boxes.size());
+    const long numBoxes = numberBoxes - 1;
+    std::vector<float> leftArea(static_cast<size_t>(numBoxes));
+    HAABB leftBox = boxes[0];
+    leftArea[0] = surfaceArea(leftBox);
+    for (long i = 1; i < numBoxes; ++i) {
+        leftBox = surrounding(leftBox, boxes[static_cast<size_t>(i)]);
+        leftArea[static_cast<size_t>(i)] = surfaceArea(leftBox);
+    }
+    std::vector<float> rightArea(static_cast<size_t>(numBoxes));
+    HAABB rightBox = boxes[static_cast<size_t>(numBoxes)];
+    rightArea[static_cast<size_t>(numBoxes - 1)] = surfaceArea(rightBox);
+    for (long i = numBoxes - 2; i >= 0; --i) {
+        rightBox = surrounding(rightBox, boxes[static_cast<size_t>(i + 1)]);
+        rightArea[static_cast<size_t>(i)] = surfaceArea(rightBox);
+    }
+    int32_t splitIndex = 1;
+    float minSah = leftArea[0] + static_cast<float>(numBoxes) * rightArea[0];
+    for (long i = 1; i < numBoxes; ++i) {
+        const long nL = i + 1;
+        const long nR = numberBoxes - nL;
+        const float sah = static_cast<float>(nL) * leftArea[static_cast<size_t>(i)] +
+                          static_cast<float>(nR) * rightArea[static_cast<size_t>(i)];
+        if (sah < minSah) {
+            splitIndex = static_cast<int32_t>(i + 1);
+            minSah = sah;
+        }
+    }
+    return splitIndex;
+}
+
+struct BuildNode {
+    HAABB box;
+    v3 c;
+    int32_t oldIndex;
+};
+
+}  // namespace
+
+template <class T>
+std::vector<HBVHNode> buildBVH(std::vector<T>* primsPtr, std::vector<int32_t>* order) {
+    std::vector<T>& prims = *primsPtr;
+    std::vector<HBVHNode> nodes;
+    order->clear();
+    if (prims.empty()) {
+        nodes.push_back(HBVHNode{HAABB{v3{0, 0, 0}, v3{0, 0, 0}}, 0, 0});
+        return nodes;
+    }
+    const int32_t n = static_cast<int32_t>(prims.size());
+    nodes.assign(static_cast<size_t>(2 * n - 1), HBVHNode{HAABB{v3{0, 0, 0}, v3{0, 0, 0}}, 0, 0});
+    std::vector<BuildNode> bn;
+    bn.reserve(prims.size());
+    for (int32_t i = 0; i < n; ++i) {
+        const HAABB b = aabbOf(prims[static_cast<size_t>(i)]);
+        bn.push_back(BuildNode{b, centroid(b), i});
+    }
+    std::vector<int32_t> stIdx(64, 0), stBegin(64, 0), stEnd(64, 0);
+    size_t sp = 1;
+    int32_t cur = 0, begin = 0, end = n, maxNode = 0;
+    std::vector<HAABB> boxes;
+    do {
+        // getSurroundingBox (BVH.hpp:451-460)
+        HAABB sur{bn[static_cast<size_t>(begin)].box.mn, bn[static_cast<size_t>(begin)].box.mx};
+        for (int32_t i = begin + 1; i < end; ++i) sur = surrounding(sur, bn[static_cast<size_t>(i)].box);
+        const v3 maxDist = sur.mx - sur.mn;
+        const int axis = (maxDist.x >= maxDist.y && maxDist.x >= maxDist.z)
+                             ? 0
+                             : ((maxDist.y >= maxDist.x && maxDist.y >= maxDist.z) ? 1 : 2);
+        const int numBuckets = 10;
+        const v3 step = maxDist / static_cast<float>(numBuckets);
+        const float stepAxis = comp(step, axis);
+        const float startBox = comp(sur.mn, axis);
+        const float limit1 = startBox + stepAxis;
+        auto first = bn.begin() + begin;
+        auto last = bn.begin() + end;
+        auto itBucket = pinnedPartition(first, last, [axis, limit1](const BuildNode& x) { return comp(x.c, axis) < limit1; });
+        for (int32_t bi = 2; bi < numBuckets; ++bi) {
+            const float limit = startBox + stepAxis * static_cast<float>(bi);
+            itBucket = pinnedPartition(itBucket, last, [axis, limit](const BuildNode& x) { return comp(x.c, axis) < limit; });
+        }
+        HBVHNode& node = nodes[static_cast<size_t>(cur)];
+        node.box = bn[static_cast<size_t>(begin)].box;
+        boxes.clear();
+        boxes.push_back(node.box);
+        for (int32_t i = begin + 1; i < end; ++i) {
+            const HAABB nb = bn[static_cast<size_t>(i)].box;
+            node.box = surrounding(nb, node.box);
+            boxes.push_back(nb);
+        }
+        const int32_t count = end - begin;
+        if (count <= 4) {  // maxPrimitivesInBoxLeaf (BVH.hpp:239-251)
+            node.indexOffset = begin;
+            node.numPrimitives = count;
+            --sp;
+            cur = stIdx[sp];
+            begin = stBegin[sp];
+            end = stEnd[sp];
+        } else {
+            const int32_t left = maxNode + 1;
+            const int32_t right = left + 1;
+            const int32_t split = splitIndexSah(boxes);
+            node.indexOffset = left;
+            maxNode = std::max(right, maxNode);
+            if (sp >= stIdx.size()) {
+                stIdx.resize(sp * 2);
+                stBegin.resize(sp * 2);
+                stEnd.resize(sp * 2);
+            }
+            stIdx[sp] = right;
+            stBegin[sp] = begin + split;
+            stEnd[sp] = end;
+            ++sp;
+            cur = left;
+            end = begin + split;
+        }
+    } while (sp > 0);
+    nodes.resize(static_cast<size_t>(maxNode + 1));
+    std::vector<T> permuted;
+    permuted.reserve(prims.size());
+    order->reserve(prims.size());
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t old = bn[static_cast<size_t>(i)].oldIndex;
+        permuted.push_back(prims[static_cast<size_t>(old)]);
+        order->push_back(old);
+    }
+    prims.swap(permuted);
+    return nodes;
+}
+
+template std::vector<HBVHNode> buildBVH<HTriangle>(std::vector<HTriangle>*, std::vector<int32_t>*);
+template std::vector<HBVHNode> buildBVH<HPlane>(std::vector<HPlane>*, std::vector<int32_t>*);
+template std::vector<HBVHNode> buildBVH<HSphere>(std::vector<HSphere>*, std::vector<int32_t>*);
+
+static int32_t encodeRef(const std::vector<HBVHNode>& nodes, int32_t j) {
+    const HBVHNode& c = nodes[static_cast<size_t>(j)];
+    return c.numPrimitives > 0 ? leafRef(c.indexOffset, c.numPrimitives) : j;
+}
+
+void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root) {
+    out->assign(nodes.size(), GNode{});
+    const HBVHNode& r = nodes[0];
+    root->bmin[0] = r.box.mn.x;
+    root->bmin[1] = r.box.mn.y;
+    root->bmin[2] = r.box.mn.z;
+    root->bmax[0] = r.box.mx.x;
+    root->bmax[1] = r.box.mx.y;
+    root->bmax[2] = r.box.mx.z;
+    root->count = static_cast<int32_t>(numPrims);
+    root->ref = numPrims == 0 ? 0 : encodeRef(nodes, 0);
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        const HBVHNode& nd = nodes[i];
+        if (numPrims == 0 || nd.numPrimitives > 0) continue;
+        const int32_t l = nd.indexOffset;
+        const HBVHNode& L = nodes[static_cast<size_t>(l)];
+        const HBVHNode& R = nodes[static_cast<size_t>(l + 1)];
+        GNode g{};
+        g.lminx = L.box.mn.x;
+        g.lminy = L.box.mn.y;
+        g.lminz = L.box.mn.z;
+        g.lmaxx = L.box.mx.x;
+        g.lmaxy = L.box.mx.y;
+        g.lmaxz = L.box.mx.z;
+        g.rminx = R.box.mn.x;
+        g.rminy = R.box.mn.y;
+        g.rminz = R.box.mn.z;
+        g.rmaxx = R.box.mx.x;
+        g.rmaxy = R.box.mx.y;
+        g.rmaxz = R.box.mx.z;
+        g.refL = encodeRef(nodes, l);
+        g.refR = encodeRef(nodes, l + 1);
+        (*out)[i] = g;
+    }
+}
+
+// ---- sample tables (Utils.cpp:43-53, Utils.hpp:209-218) ----------------------------------
+float haltonSequence(uint32_t index, uint32_t base) {
+    float fraction = 1.0F;
+    float nextValue = 0.0F;
+    const float baseF = static_cast<float>(base);
+    while (index > 0) {
+        fraction /= baseF;
+        nextValue += fraction * static_cast<float>(index % base);
+        index = index / base;
+    }
+    return nextValue;
+}
+
+void fillHaltonTable(std::vector<float>* table, uint32_t seed) {
+    table->resize(kArraySize);
+    for (uint32_t i = 0; i < kArraySize; ++i) (*table)[i] = haltonSequence(i, 2);
+    std::mt19937 gen(seed);
+    std::shuffle(table->begin(), table->end(), gen);
+}
+
+}  // namespace mrt

@@ -1,0 +1,131 @@
+// mrt_scene.hpp - host-side scene assembly for the MI355X render path.
+//
+// This is the "Shader constructor" half of the reference (Shader.cpp:33-77): it gathers
+// planes / spheres / triangles / lights / materials, builds one BVH per primitive kind
+// with the reference's build algorithm (BVH.hpp:126-283), generates the two sample tables
+// (Utils.hpp:209-218 with fixed seeds) and flattens everything into the 16-byte aligned
+// records the gfx950 kernels read.  None of this runs inside the timed render window.
+#pragma once
+
+#include "mrt_common.hpp"
+
+#include <string>
+#include <vector>
+
+namespace mrt {
+
+struct v2 {
+    float x, y;
+};
+
+// Material.hpp:18-43
+struct HMaterial {
+    v3 Le{0, 0, 0}, Kd{0, 0, 0}, Ks{0, 0, 0}, Kt{0, 0, 0};
+    float ior{1.0F};
+    std::string texture;  // map_Kd file name ("" = none); textures are not sampled
+};
+bool materialEqual(const HMaterial& a, const HMaterial& b);  // Material.cpp:106-115
+
+// Triangle.hpp:18-27 (field order kept: AC, AB, A, normals, texcoords, material)
+struct HTriangle {
+    v3 AC, AB, A;
+    v3 nA, nB, nC;
+    v2 tA{-1, -1}, tB{-1, -1}, tC{-1, -1};
+    int32_t mat{-1};
+};
+// Triangle::Builder (Triangle.cpp:328-339) + Triangle ctor normalisation (Triangle.cpp:14-26)
+HTriangle makeTriangle(v3 a, v3 b, v3 c);
+HTriangle makeTriangle(v3 a, v3 b, v3 c, v3 na, v3 nb, v3 nc, v2 ta, v2 tb, v2 tc, int32_t mat);
+
+struct HPlane {  // Plane.cpp:14-19
+    v3 normal, point;
+    int32_t mat;
+};
+HPlane makePlane(v3 point, v3 normal, int32_t mat);
+
+struct HSphere {  // Sphere.cpp:14-19
+    v3 center;
+    float sqRadius;
+    int32_t mat;
+};
+HSphere makeSphere(v3 center, float radius, int32_t mat);
+
+enum LightKind : int32_t { kPointLight = 0, kAreaLight = 1 };
+struct HLight {  // PointLight.cpp / AreaLight.cpp
+    int32_t kind;
+    HMaterial radiance;
+    v3 position;  // point light
+    HTriangle tri; // area light
+};
+
+struct HAABB {
+    v3 mn, mx;
+};
+
+struct HScene {
+    std::vector<HPlane> planes;
+    std::vector<HSphere> spheres;
+    std::vector<HTriangle> triangles;
+    std::vector<HLight> lights;
+    std::vector<HMaterial> materials;
+};
+
+// Reference BVH node (BVH.hpp:56-60): box, indexOffset (leaf: first prim; inner: left),
+// numPrimitives (> 0 => leaf)
+struct HBVHNode {
+    HAABB box;
+    int32_t indexOffset;
+    int32_t numPrimitives;
+};
+
+// ---- scenes / loaders ------------------------------------------------------------------
+HScene cornellBoxScene();                                     // Scenes.cpp:63-137 (scene 0)
+GCamera cornellBoxCamera(float ratio);                        // Scenes.cpp:139-150
+GCamera makePerspective(v3 position, v3 lookAt, v3 up, float hFovDeg, float vFovDeg);
+// CameraFactory.cpp + PerspectiveLoader.cpp:18-64 (position.x negated, hFov = fov.u * ratio)
+bool loadCameraFile(const std::string& path, float ratio, GCamera* out, std::string* err);
+// OBJLoader.cpp:18-497 (+ tinyobjloader v1.0.7 parsing / fan triangulation); fills in file order
+bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene* scene, std::string* err);
+
+// ---- acceleration structure ------------------------------------------------------------
+// libstdc++ std::partition (bidirectional overload), restated so the build is pinned.
+template <class It, class Pred>
+It pinnedPartition(It first, It last, Pred pred) {
+    while (true) {
+        while (true) {
+            if (first == last) return first;
+            if (pred(*first)) ++first; else break;
+        }
+        --last;
+        while (true) {
+            if (first == last) return first;
+            if (!pred(*last)) --last; else break;
+        }
+        auto tmp = *first;
+        *first = *last;
+        *last = tmp;
+        ++first;
+    }
+}
+
+HAABB aabbOf(const HTriangle& t);  // Triangle.cpp:116-123
+HAABB aabbOf(const HPlane& p);     // Plane.cpp:79-109
+HAABB aabbOf(const HSphere& s);    // Sphere.cpp:88-94
+bool aabbIntersect(const HAABB& b, v3 origin, v3 dir);  // AABB.cpp:34-54 (host KAT helper)
+
+// Builds the reference BVH over `prims` (permuted in place to leaf order).  Returns nodes
+// in the reference numbering.  `order` receives the original index of every permuted prim.
+template <class T>
+std::vector<HBVHNode> buildBVH(std::vector<T>* prims, std::vector<int32_t>* order);
+
+// Converts reference nodes to the device child-box layout.
+void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root);
+
+// Utils.cpp:43-53 haltonSequence
+float haltonSequence(uint32_t index, uint32_t base);
+// Utils.hpp:209-218 with std::mt19937(seed) instead of random_device
+void fillHaltonTable(std::vector<float>* table, uint32_t seed);
+constexpr uint32_t kSeedShaderTable = 0x4D525400u;   // Shader.cpp:23,37
+constexpr uint32_t kSeedSamplerTable = 0x4D525401u;  // StaticHaltonSeq.cpp:7-22
+
+}  // namespace mrt
