@@ -76,8 +76,10 @@ typedef struct mrt_frame_stats {
     uint64_t rays;          /* camera + diffuse + specular + transmission rays */
     uint64_t shadowRays;
     uint64_t primaryRays;
-    uint64_t nodeRecords;   /* counting pass only: BVH child records fetched */
-    uint64_t triTests;      /* counting pass only: ray/triangle tests */
+    uint64_t nodeRecords;   /* counting pass only: BVH child records fetched by closest-hit rays */
+    uint64_t triTests;      /* counting pass only: ray/triangle tests of closest-hit rays */
+    uint64_t shadowNodeRecords; /* counting pass only: the same for shadow (any-hit) rays */
+    uint64_t shadowTriTests;
     double traceMs;         /* profiling: summed duration of closest-hit trace launches */
     double shadowMs;        /* profiling: summed duration of any-hit trace launches */
     double frameMs;         /* profiling: whole frame on the render stream */

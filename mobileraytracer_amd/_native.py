@@ -42,9 +42,23 @@ class MrtFrameStats(ctypes.Structure):
     _fields_ = [
         ("rays", ctypes.c_uint64), ("shadowRays", ctypes.c_uint64), ("primaryRays", ctypes.c_uint64),
         ("nodeRecords", ctypes.c_uint64), ("triTests", ctypes.c_uint64),
+        ("shadowNodeRecords", ctypes.c_uint64), ("shadowTriTests", ctypes.c_uint64),
         ("traceMs", ctypes.c_double), ("shadowMs", ctypes.c_double), ("frameMs", ctypes.c_double),
         ("traceLaunches", ctypes.c_int64), ("shadowLaunches", ctypes.c_int64),
     ]
+
+
+def _preload_torch_hip_runtime():
+    """One HIP runtime per process: if PyTorch-ROCm is installed, load its libamdhip64 first
+    (by full path, without importing torch) so this library and torch share it whichever is
+    imported first.  Both carry the SONAME libamdhip64.so.7."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    rt = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(rt):
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
 
 
 def load_library(path=LIB_PATH):
@@ -52,6 +66,7 @@ def load_library(path=LIB_PATH):
         raise ImportError(
             f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the MI355X path has no CPU fallback)")
+    _preload_torch_hip_runtime()
     lib = ctypes.CDLL(path)
     P = ctypes.POINTER
     vp = ctypes.c_void_p

@@ -162,8 +162,8 @@ __global__ __launch_bounds__(kBlock) void k_shadow(DScene s, Level lv, int* coun
             t += __shfl_down(t, off, 64);
         }
         if (laneId() == 0) {
-            atomicAdd(stats + kStatNodes, n);
-            atomicAdd(stats + kStatTris, t);
+            atomicAdd(stats + kStatNodesShadow, n);
+            atomicAdd(stats + kStatTrisShadow, t);
         }
     }
 }

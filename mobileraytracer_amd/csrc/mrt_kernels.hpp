@@ -22,9 +22,11 @@ constexpr int kNumCounters = 4 * kMaxLevels + 4;  // 16-byte multiple
 constexpr int kStatRays = 0;        // rays of every level (camera + diffuse + specular + transmission)
 constexpr int kStatShadowRays = 1;  // shadow rays
 constexpr int kStatPrimary = 2;
-constexpr int kStatNodes = 3;       // child node records fetched (counting pass only)
-constexpr int kStatTris = 4;        // triangle tests (counting pass only)
+constexpr int kStatNodes = 3;       // closest-hit kernel: child node records fetched (counting pass only)
+constexpr int kStatTris = 4;        // closest-hit kernel: triangle tests (counting pass only)
 constexpr int kStatOverflow = 5;
+constexpr int kStatNodesShadow = 6; // any-hit kernel: child node records fetched (counting pass only)
+constexpr int kStatTrisShadow = 7;  // any-hit kernel: triangle tests (counting pass only)
 constexpr int kNumStats = 8;
 
 // One level of the wavefront (SoA queues).

@@ -415,6 +415,8 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
         fs.primaryRays = hs[kStatPrimary];
         fs.nodeRecords = hs[kStatNodes];
         fs.triTests = hs[kStatTris];
+        fs.shadowNodeRecords = hs[kStatNodesShadow];
+        fs.shadowTriTests = hs[kStatTrisShadow];
         fs.frameMs = std::chrono::duration<double, std::milli>(t1 - t0).count();
         if (r->profileFlags & 1) {
             for (size_t e = 0; e + 3 < evCount; e += 4) {

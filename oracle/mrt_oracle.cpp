@@ -1100,16 +1100,17 @@ struct Engine {
         return camera.generateRay(u, v, deviationU, deviationV, &rays);
     }
 
-    // Renderer::renderScene (Renderer.cpp:107-170) over tiles [first, first+count)
-    void renderTiles(int32_t* bitmap, int threads, int first, int count) {
+    // Renderer::renderScene (Renderer.cpp:107-170) over a list of tiles
+    void renderTiles(int32_t* bitmap, int threads, const std::vector<int>& list) {
         const auto ts = tiles();
         const int W = cfg.width, H = cfg.height, bx = W / 16, by = H / 16;
-        const int last = std::min(static_cast<int>(ts.size()), first + count);
-        std::atomic<int> next{first};
+        std::atomic<size_t> next{0};
         auto worker = [&]() {
             while (true) {
-                const int k = next.fetch_add(1);
-                if (k >= last) break;
+                const size_t n = next.fetch_add(1);
+                if (n >= list.size()) break;
+                const int k = list[n];
+                if (k < 0 || k >= static_cast<int>(ts.size())) continue;
                 const int startX = ts[static_cast<size_t>(k)][0], startY = ts[static_cast<size_t>(k)][1];
                 for (int sample = 0; sample < cfg.samplesPixel; ++sample) {
                     for (int y = startY; y < startY + by; ++y) {
@@ -1185,7 +1186,18 @@ int oracle_num_tiles(void* h) { return static_cast<int>(static_cast<oracle::Engi
 uint64_t oracle_render(void* h, int32_t* bitmap, int threads, int first, int count) {
     auto* e = static_cast<oracle::Engine*>(h);
     const uint64_t before = e->rays.load();
-    e->renderTiles(bitmap, threads < 1 ? 1 : threads, first, count);
+    std::vector<int> list;
+    const int nt = static_cast<int>(e->tiles().size());
+    for (int k = first; k < nt && k - first < count; ++k) list.push_back(k);
+    e->renderTiles(bitmap, threads < 1 ? 1 : threads, list);
+    return e->rays.load() - before;
+}
+
+// the same over an explicit tile list (bounded CPU-baseline samples)
+uint64_t oracle_render_tiles(void* h, int32_t* bitmap, int threads, const int32_t* tiles, int n) {
+    auto* e = static_cast<oracle::Engine*>(h);
+    const uint64_t before = e->rays.load();
+    e->renderTiles(bitmap, threads < 1 ? 1 : threads, std::vector<int>(tiles, tiles + n));
     return e->rays.load() - before;
 }
 

@@ -41,6 +41,8 @@ def lib():
         L.oracle_num_tiles.argtypes = [vp]
         L.oracle_render.restype = ctypes.c_uint64
         L.oracle_render.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_render_tiles.restype = ctypes.c_uint64
+        L.oracle_render_tiles.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_int]
         L.oracle_counts.argtypes = [vp, vp]
         L.oracle_primary_hits.argtypes = [vp, vp, vp, vp]
         L.oracle_triangle_bvh.restype = ctypes.c_int64
@@ -92,6 +94,13 @@ class Oracle:
         if bitmap is None:
             bitmap = np.zeros(self.width * self.height, np.int32)
         rays = lib().oracle_render(self._h, bitmap.ctypes.data, threads, first_tile, num_tiles)
+        return bitmap, int(rays)
+
+    def render_tiles(self, tiles, bitmap=None, threads=1):
+        if bitmap is None:
+            bitmap = np.zeros(self.width * self.height, np.int32)
+        t = np.ascontiguousarray(np.asarray(tiles, np.int32))
+        rays = lib().oracle_render_tiles(self._h, bitmap.ctypes.data, threads, t.ctypes.data, len(t))
         return bitmap, int(rays)
 
     def counts(self):

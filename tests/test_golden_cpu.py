@@ -1,0 +1,105 @@
+"""CPU: the oracle reproduces the committed golden fixtures (tests/golden/make_golden.py), the
+conference stand-in file is the pinned one, and the C-ABI library loads and exports every
+symbol include/*.h declares (no compute without a GPU)."""
+import ctypes
+import hashlib
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", ["cornell256_whitted", "cornell512_whitted", "cornell256_pt4", "water128_whitted",
+                                  "water128_pt4", "teapot128_whitted", "conference96_whitted", "conference96_pt4"])
+def test_oracle_matches_golden(oracle_mod, golden, name):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    o = mg.oracle_for(mg.CASES[name])
+    bm, rays = o.render(threads=min(8, os.cpu_count() or 1))
+    k, i, t = o.primary_hits()
+    g = golden[name]
+    assert rays == g["rays"]
+    assert sha(bm) == g["bitmap_sha256"]
+    assert sha(np.stack([k, i, t.view(np.int32)])) == g["hits_sha256"]
+    assert o.counts() == g["counts"]
+
+
+def test_cornell_c1_bitmap_fixture(oracle_mod):
+    bm, _ = oracle_mod.Oracle(256, 256, 1, 0).render(threads=4)
+    ref = np.load(os.path.join(GOLDEN, "cornell256_whitted.npz"))["bitmap"]
+    assert np.array_equal(bm, ref)
+    assert len(np.unique(bm)) > 1  # ShaderTestEngine.cpp:46-48: the image is not uniform
+
+
+def test_conference_standin_is_pinned(golden):
+    from mobileraytracer_amd import scenes
+    obj = scenes.conference()[0]
+    if not scenes.is_standin(obj):
+        pytest.skip("a real conference.obj was supplied")
+    assert scenes.file_sha256(obj) == golden["conference_standin_obj_sha256"]
+
+
+def _declared_symbols():
+    names = set()
+    for hdr in ("mobilert_amd.h", "mobilert_amd.hpp"):
+        with open(os.path.join(REPO, "include", hdr)) as f:
+            src = f.read()
+        names |= set(re.findall(r"\b(mrt_[a-z_]+)\s*\(", src))
+        names |= set(re.findall(r'extern "C" void (\w+)\(', src))
+    return names
+
+
+def test_library_exports_every_declared_symbol(native_lib_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", native_lib_path], check=True, capture_output=True,
+                         text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    declared = _declared_symbols()
+    assert {"RayTrace", "stopRender", "mrt_create", "mrt_render_frame"} <= declared
+    missing = declared - exported
+    assert not missing, missing
+    from mobileraytracer_amd import _native
+    assert set(_native.EXPORTED_SYMBOLS) <= exported
+
+
+def test_library_loads_without_gpu(native_lib_path):
+    from mobileraytracer_amd import _native
+    lib = _native.load_library(native_lib_path)
+    assert lib.mrt_last_error() is not None
+
+
+def test_ctypes_layouts_match_header(tmp_path):
+    """The ctypes mirror of mrt_config / mrt_scene_info / mrt_frame_stats matches the C header."""
+    from mobileraytracer_amd import _native
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mobilert_amd.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu", sizeof(mrt_config), sizeof(mrt_scene_info),'
+                   ' sizeof(mrt_frame_stats), offsetof(mrt_config, maxDepth));return 0;}')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    sizes = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert sizes == [ctypes.sizeof(_native.MrtConfig), ctypes.sizeof(_native.MrtSceneInfo),
+                     ctypes.sizeof(_native.MrtFrameStats), _native.MrtConfig.maxDepth.offset]
+
+
+def test_library_built_for_gfx950(native_lib_path):
+    out = subprocess.run(["strings", native_lib_path], capture_output=True, text=True, check=True)
+    assert "amdgcn-amd-amdhsa--gfx950" in out.stdout
