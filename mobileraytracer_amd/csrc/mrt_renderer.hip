@@ -147,7 +147,9 @@ void buildUnits(mrt_renderer* r) {
         if (std::find(blocks.begin(), blocks.end(), rb) == blocks.end()) blocks.push_back(rb);
     }
     std::vector<int4> all;
-    for (int rb : blocks) {
+    std::vector<int> owner;  // unit (tile t, band b) -> rank (t + b) % rankCount: balances short bands
+    for (size_t t = 0; t < blocks.size(); ++t) {
+        const int rb = blocks[t];
         const int pixel = rb * bx % resolution;               // Renderer.cpp:126
         const int startY = ((pixel / W) * by) % H;            // :127
         const int startX = pixel % W;                         // :133 ((pixel + y*W) % W)
@@ -155,12 +157,15 @@ void buildUnits(mrt_renderer* r) {
             int h = std::min(8, by - 8 * b);
             const int y0 = startY + 8 * b;
             while (h > 0 && (y0 + h - 1) * W + startX + bx - 1 >= resolution) --h;  // stay inside the bitmap
-            if (h > 0) all.push_back(make_int4(startX, y0, bx, h));
+            if (h > 0) {
+                all.push_back(make_int4(startX, y0, bx, h));
+                owner.push_back(static_cast<int>((t + static_cast<size_t>(b)) % static_cast<size_t>(r->rankCount)));
+            }
         }
     }
     r->unitsByRank.assign(static_cast<size_t>(r->rankCount), {});
     r->prefixByRank.assign(static_cast<size_t>(r->rankCount), {});
-    for (size_t u = 0; u < all.size(); ++u) r->unitsByRank[u % static_cast<size_t>(r->rankCount)].push_back(all[u]);
+    for (size_t u = 0; u < all.size(); ++u) r->unitsByRank[static_cast<size_t>(owner[u])].push_back(all[u]);
     r->maxSlots = 0;
     for (int k = 0; k < r->rankCount; ++k) {
         int acc = 0;

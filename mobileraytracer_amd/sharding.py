@@ -1,8 +1,8 @@
 """Screen-tile sharding of a frame across GPUs (one process per GPU).
 
 Mirrors ``buildUnits`` in csrc/mrt_renderer.hip: the reference's 16x16 tiling
-(Renderer.cpp:33-38, 117-135) cut into 8-row bands ("units"); unit u belongs to rank
-u % world.  Pixel slots of a rank are its units' pixels in order, column-major inside a unit.
+(Renderer.cpp:33-38, 117-135) cut into 8-row bands ("units"); unit (tile t, band b) belongs
+to rank (t + b) % world.  Pixel slots of a rank are its units' pixels in order, column-major inside a unit.
 The renderer writes a rank's frame as a packed int32 array in slot order; rank 0 gathers the
 packed arrays (one RCCL gather of pixelSlotsMax int32 per rank) and scatters them into the
 bitmap.  Every pixel has exactly one owner, so no reduction is needed and the assembled frame
@@ -29,7 +29,7 @@ def units(width, height):
         if rb not in blocks:
             blocks.append(rb)
     out = []
-    for rb in blocks:
+    for t, rb in enumerate(blocks):
         pixel = rb * bx % res
         start_y = ((pixel // width) * by) % height
         start_x = pixel % width
@@ -40,13 +40,15 @@ def units(width, height):
             while h > 0 and (y0 + h - 1) * width + start_x + bx - 1 >= res:
                 h -= 1
             if h > 0:
-                out.append((start_x, y0, bx, h))
+                out.append((start_x, y0, bx, h, t + b))
             b += 1
     return out
 
 
 def rank_units(width, height, rank, world):
-    return [u for i, u in enumerate(units(width, height)) if i % world == rank]
+    """Unit (tile t, band b) belongs to rank (t + b) % world, which spreads the short last
+    band of every tile over the ranks."""
+    return [u[:4] for u in units(width, height) if u[4] % world == rank]
 
 
 def slot_pixels(width, height, rank, world):

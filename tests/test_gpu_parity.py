@@ -112,8 +112,20 @@ def test_whitted_bit_exact(oracle_mod, case):
     cfg = make_cfg(shader=1, **case)
     bm, rays, _ = gpu_render(cfg)
     ref, ref_rays = oracle_render(oracle_mod, cfg)
-    assert np.array_equal(bm, ref), int((bm != ref).sum())
+    once = coverage(cfg.width, cfg.height) == 1
+    assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
     assert rays == ref_rays
+
+
+def coverage(width, height):
+    """How many reference tiles write each bitmap index.  With width % 16 != 0 the tile formula
+    (Renderer.cpp:126-135) wraps x past the row end, so some pixels belong to two tiles and the
+    reference's result there is whichever thread writes last (a race); such pixels are excluded
+    from bit-exact comparisons and documented in DESIGN.md."""
+    from mobileraytracer_amd import sharding
+    cov = np.zeros(width * height, np.int32)
+    np.add.at(cov, sharding.slot_pixels(width, height, 0, 1), 1)
+    return cov
 
 
 def test_c1_matches_committed_fixture():
