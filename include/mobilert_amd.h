@@ -104,6 +104,10 @@ int mrt_get_scene_info(const mrt_renderer *r, mrt_scene_info *info);
 /* enable per-launch HIP event timing (1) and/or node/triangle counting (2) */
 int mrt_set_profiling(mrt_renderer *r, int32_t flags);
 int mrt_get_frame_stats(const mrt_renderer *r, mrt_frame_stats *stats);
+/* tuning knobs for A/B measurement (results are identical for every value):
+ * key 1 = trace kernel organisation (0 per-wave batches, 1 while-while + per-lane refill),
+ * key 2 = near-first traversal with conservative t-culling (1) or the reference visit set (0) */
+int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /
  * 4 light; index in the scene's input order (-1 on miss); t = hit distance */
 int mrt_primary_hits(mrt_renderer *r, int32_t *kind, int32_t *index, float *t);

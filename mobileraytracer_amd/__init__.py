@@ -112,6 +112,10 @@ class Renderer:
     def set_profiling(self, timing: bool = False, counting: bool = False) -> None:
         _native.check(self._lib.mrt_set_profiling(self._h, int(timing) | (2 * int(counting))))
 
+    def set_tuning(self, key: int, value: int) -> None:
+        """A/B knobs (identical results): 1 = trace kernel variant, 2 = t-culling."""
+        _native.check(self._lib.mrt_set_tuning(self._h, key, value))
+
     def frame_stats(self) -> dict:
         s = _native.MrtFrameStats()
         _native.check(self._lib.mrt_get_frame_stats(self._h, ctypes.byref(s)))

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libmobilert_amd.so")
 EXPORTED_SYMBOLS = (
     "mrt_last_error", "mrt_create", "mrt_destroy", "mrt_render_frame", "mrt_render_frame_device",
     "mrt_unpack_gathered", "mrt_stop_render", "mrt_get_sample", "mrt_get_total_casted_rays",
-    "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits",
+    "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits", "mrt_set_tuning",
     "RayTrace", "stopRender",
 )
 
@@ -84,6 +84,7 @@ def load_library(path=LIB_PATH):
         "mrt_set_profiling": (ctypes.c_int, [vp, ctypes.c_int32]),
         "mrt_get_frame_stats": (ctypes.c_int, [vp, P(MrtFrameStats)]),
         "mrt_primary_hits": (ctypes.c_int, [vp, vp, vp, vp]),
+        "mrt_set_tuning": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -35,7 +35,7 @@ struct DScene {
     int32_t nLights;
     int32_t nMats;
     int32_t cull;              // 1: near-first + conservative t-culling, 0: reference visit set
-    int32_t pad;
+    int32_t variant;           // trace kernel organisation: 0 per-wave batches, 1 while-while + refill
 };
 
 __device__ __forceinline__ float4 ld4(const float4* p) { return *p; }

@@ -17,6 +17,7 @@
 // operation in the order of the recursive reference, which is what makes the Whitted
 // Cornell image bit-exact.
 #include "mrt_kernels.hpp"
+#include "mrt_trace_ww.hpp"
 
 namespace mrt {
 
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
 }
 
 // ---------------------------------------------------------------------------------------
-template <bool kCount>
+template <bool kCount, int kVariant>
 __global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* counters, int level, int2* gstack,
                                                   int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kLdsStack * kBlock];
@@ -108,7 +109,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* count
     const int count = min(counters[kCntRays + level], lv.cap);
     int* fetch = counters + kCntFetchTrace + level;
     TravCount cnt{0u, 0u};
-    while (true) {
+    if (kVariant == 1) traceWhileWhile<false, kCount>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
+    while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
         base = __shfl(base, 0, 64);
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* count
     }
 }
 
-template <bool kCount>
+template <bool kCount, int kVariant>
 __global__ __launch_bounds__(kBlock) void k_shadow(DScene s, Level lv, int* counters, int level, int2* gstack,
                                                    int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kLdsStack * kBlock];
@@ -142,7 +144,8 @@ __global__ __launch_bounds__(kBlock) void k_shadow(DScene s, Level lv, int* coun
     const int count = min(counters[kCntShadows + level], lv.shadowCap);
     int* fetch = counters + kCntFetchShadow + level;
     TravCount cnt{0u, 0u};
-    while (true) {
+    if (kVariant == 1) traceWhileWhile<true, kCount>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
+    while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
         base = __shfl(base, 0, 64);
@@ -471,22 +474,29 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
     hipLaunchKernelGGL(k_raygen, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, a, lv, counters);
 }
 
+#define MRT_LAUNCH_TRACE(KERNEL)                                                                              \
+    do {                                                                                                     \
+        if (s.variant == 1) {                                                                                \
+            if (countStats)                                                                                  \
+                hipLaunchKernelGGL((KERNEL<true, 1>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+            else                                                                                             \
+                hipLaunchKernelGGL((KERNEL<false, 1>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        } else {                                                                                             \
+            if (countStats)                                                                                  \
+                hipLaunchKernelGGL((KERNEL<true, 0>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+            else                                                                                             \
+                hipLaunchKernelGGL((KERNEL<false, 0>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        }                                                                                                    \
+    } while (0)
+
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
-    if (countStats) {
-        hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats);
-    } else {
-        hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats);
-    }
+    MRT_LAUNCH_TRACE(k_trace);
 }
 
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
-    if (countStats) {
-        hipLaunchKernelGGL(k_shadow<true>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats);
-    } else {
-        hipLaunchKernelGGL(k_shadow<false>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats);
-    }
+    MRT_LAUNCH_TRACE(k_shadow);
 }
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
@@ -528,7 +538,7 @@ void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStre
 
 int traceOccupancyBlocksPerCU() {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false>, kBlock, 0) != hipSuccess) n = 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 1>, kBlock, 0) != hipSuccess) n = 4;
     return n > 0 ? n : 1;
 }
 

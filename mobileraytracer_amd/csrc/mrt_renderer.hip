@@ -270,6 +270,8 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.nLights = static_cast<int32_t>(sc.lights.size());
     d.nMats = static_cast<int32_t>(sc.materials.size());
     d.cull = r->cfg.cull;
+    const char* tv = std::getenv("MRT_TRACE_VARIANT");
+    d.variant = tv != nullptr ? std::atoi(tv) : 1;
 
     std::vector<float> table;
     fillHaltonTable(&table, kSeedShaderTable);
@@ -581,6 +583,19 @@ int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
 int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
     r->profileFlags = flags;
     return 0;
+}
+
+int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
+    if (key == 1 && (value == 0 || value == 1)) {
+        r->ds.variant = value;
+        return 0;
+    }
+    if (key == 2 && (value == 0 || value == 1)) {
+        r->ds.cull = value;
+        return 0;
+    }
+    gLastError = "unknown tuning key/value";
+    return -1;
 }
 
 int mrt_get_frame_stats(const mrt_renderer* r, mrt_frame_stats* s) {

@@ -1,0 +1,44 @@
+"""A/B the trace-kernel variants on the C4 frame in one process (interleaved rounds)."""
+import os, sys, json, time
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import mobileraytracer_amd as m
+from mobileraytracer_amd import scenes
+
+def main():
+    o, l, c = scenes.conference()
+    cfg = m.Config(width=1920, height=1080, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5,
+                   objFilePath=o, mtlFilePath=l, camFilePath=c)
+    r = m.Renderer(cfg)
+    d = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    variants = [int(v) for v in os.environ.get("VARIANTS", "0,1").split(",")]
+    imgs = {}
+    res = {v: [] for v in variants}
+    r.set_profiling(timing=True)
+    for rnd in range(4):
+        for v in variants:
+            r.set_tuning(1, v)
+            r.render_frame_device(d.data_ptr(), 0, sh)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n = 5
+            tr = shw = 0.0
+            for _ in range(n):
+                r.render_frame_device(d.data_ptr(), 0, sh)
+                st = r.frame_stats()
+                tr += st["traceMs"]; shw += st["shadowMs"]
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / n
+            rays = st["rays"] + st["shadowRays"]
+            res[v].append((dt * 1e3, tr / n, shw / n, rays / dt / 1e6))
+            imgs[v] = d.cpu().numpy().copy()
+    for v in variants:
+        a = np.array(res[v])
+        print(f"variant {v}: frame {np.median(a[:,0]):.2f} ms  trace {np.median(a[:,1]):.2f}  shadow {np.median(a[:,2]):.2f}  Mrays/s {np.median(a[:,3]):.0f}", flush=True)
+    base = imgs[variants[0]]
+    for v in variants[1:]:
+        print(f"variant {v} identical image: {np.array_equal(base, imgs[v])}")
+
+main()
