@@ -159,6 +159,21 @@ struct alignas(16) GNode {
 };
 static_assert(sizeof(GNode) == 64, "GNode must be 64 bytes");
 
+// 4-wide node collapsed from the reference BVH2 (one 128-byte record): component-major child
+// boxes so one float4 holds the same bound of all four children.  A collapsed child is reached
+// when its own box passes; its skipped BVH2 ancestors' boxes contain it (min/max are exact), and
+// the slab predicate is monotone in the bounds, so every ancestor test also passes - except in
+// the NaN-degenerate case (ray origin exactly on a bound with a zero direction component), the
+// divergence SURVEY.md Appendix A.7 allows and DESIGN.md documents.
+struct alignas(16) GNode4 {
+    float minx[4], miny[4], minz[4];
+    float maxx[4], maxy[4], maxz[4];
+    int32_t ref[4];    // inner node index, leaf ref, or kRefEmpty
+    int32_t pad[4];
+};
+static_assert(sizeof(GNode4) == 128, "GNode4 must be 128 bytes");
+constexpr int32_t kRefEmpty = 0x7FFFFFFF;
+
 // root box + root reference of one BVH (the reference tests the root box first,
 // BVH.hpp:340-342)
 struct GRoot {

@@ -23,6 +23,7 @@ struct DScene {
     const float4* triGeom;     // 3 per triangle (BVH order): A, AB, AC  (xyz)
     const float4* triShade;    // 3 per triangle: nA (w = material index bits), nB, nC
     const GNode* triNodes;
+    const GNode4* triNodes4;   // the same BVH collapsed to 4-wide nodes
     const float4* planes;      // 2 per plane: normal (w = material bits), point
     const GNode* planeNodes;
     const float4* spheres;     // 2 per sphere: center (w = sqRadius), (x = material bits)
@@ -31,11 +32,11 @@ struct DScene {
     const float4* mats;        // 4 per material: Le (w = ior), Kd, Ks, Kt
     const float* shaderTable;  // 2^20 shuffled Halton values (Shader.cpp:23)
     const float* samplerTable; // 2^20 shuffled Halton values (StaticHaltonSeq.cpp)
-    GRoot triRoot, planeRoot, sphereRoot;
+    GRoot triRoot, triRoot4, planeRoot, sphereRoot;
     int32_t nLights;
     int32_t nMats;
     int32_t cull;              // 1: near-first + conservative t-culling, 0: reference visit set
-    int32_t variant;           // trace kernel organisation: 0 per-wave batches, 1 while-while + refill
+    int32_t variant;           // trace kernels: 0 per-wave batches, 1 while-while + refill, 2 the same on BVH4
 };
 
 __device__ __forceinline__ float4 ld4(const float4* p) { return *p; }

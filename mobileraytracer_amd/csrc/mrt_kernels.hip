@@ -109,7 +109,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* count
     const int count = min(counters[kCntRays + level], lv.cap);
     int* fetch = counters + kCntFetchTrace + level;
     TravCount cnt{0u, 0u};
-    if (kVariant == 1) traceWhileWhile<false, kCount>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
+    if (kVariant == 1) traceWhileWhile<false, kCount, 2>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
+    if (kVariant == 2) traceWhileWhile<false, kCount, 4>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -144,7 +145,8 @@ __global__ __launch_bounds__(kBlock) void k_shadow(DScene s, Level lv, int* coun
     const int count = min(counters[kCntShadows + level], lv.shadowCap);
     int* fetch = counters + kCntFetchShadow + level;
     TravCount cnt{0u, 0u};
-    if (kVariant == 1) traceWhileWhile<true, kCount>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
+    if (kVariant == 1) traceWhileWhile<true, kCount, 2>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
+    if (kVariant == 2) traceWhileWhile<true, kCount, 4>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -476,7 +478,12 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
 
 #define MRT_LAUNCH_TRACE(KERNEL)                                                                              \
     do {                                                                                                     \
-        if (s.variant == 1) {                                                                                \
+        if (s.variant == 2) {                                                                                \
+            if (countStats)                                                                                  \
+                hipLaunchKernelGGL((KERNEL<true, 2>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+            else                                                                                             \
+                hipLaunchKernelGGL((KERNEL<false, 2>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        } else if (s.variant == 1) {                                                                         \
             if (countStats)                                                                                  \
                 hipLaunchKernelGGL((KERNEL<true, 1>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
             else                                                                                             \

@@ -93,8 +93,9 @@ struct mrt_renderer {
     mrt::GCamera cam{};
     mrt::DScene ds{};
     std::vector<int32_t> triOrder, planeOrder, sphereOrder;
-    int64_t nTri = 0, nLights = 0, nPlanes = 0, nSpheres = 0, nMats = 0, nTriNodes = 0;
+    int64_t nTri = 0, nLights = 0, nPlanes = 0, nSpheres = 0, nMats = 0, nTriNodes = 0, nTriNodes4 = 0;
     int triDepth = 0, maxBvhDepth = 0;
+    int stackNeed = 0;  // worst-case traversal stack entries over all node layouts
 
     // pixel units of every shard (rank r uses unitsByRank[r])
     std::vector<std::vector<int4>> unitsByRank;
@@ -208,11 +209,33 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     r->nTriNodes = static_cast<int64_t>(tn.size());
     r->triDepth = bvhDepth(tn);
     r->maxBvhDepth = std::max({r->triDepth, bvhDepth(pn), bvhDepth(sn)});
+    r->stackNeed = r->maxBvhDepth + 2;
 
     std::vector<GNode> g;
     DScene& d = r->ds;
     toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot);
     d.triNodes = r->sceneMem.upload(g, st);
+    {
+        std::vector<GNode4> g4;
+        toDeviceBVH4(tn, sc.triangles.size(), &g4, &d.triRoot4);
+        d.triNodes4 = r->sceneMem.upload(g4, st);
+        r->nTriNodes4 = static_cast<int64_t>(g4.size());
+        // depth of the 4-wide tree: a 4-wide walk pushes up to 3 entries per level
+        int depth4 = 0;
+        if (!g4.empty()) {
+            std::vector<std::pair<int, int>> stk{{0, 1}};
+            while (!stk.empty()) {
+                const auto [i, dd] = stk.back();
+                stk.pop_back();
+                depth4 = std::max(depth4, dd);
+                for (int k = 0; k < 4; ++k) {
+                    const int c = g4[static_cast<size_t>(i)].ref[k];
+                    if (c >= 0 && c != kRefEmpty) stk.push_back({c, dd + 1});
+                }
+            }
+        }
+        r->stackNeed = std::max(r->stackNeed, 3 * depth4 + 2);
+    }
     toDeviceBVH(pn, sc.planes.size(), &g, &d.planeRoot);
     d.planeNodes = r->sceneMem.upload(g, st);
     toDeviceBVH(sn, sc.spheres.size(), &g, &d.sphereRoot);
@@ -329,7 +352,7 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     }
     r->counters = r->queueMem.alloc<int>(kNumCounters);
     r->stats = r->queueMem.alloc<unsigned long long>(kNumStats);
-    r->gdepth = std::max(1, r->maxBvhDepth + 2 - kLdsStack);
+    r->gdepth = std::max(1, r->stackNeed - kLdsStack);
     r->gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceGrid) * kBlock * static_cast<size_t>(r->gdepth));
     r->dBitmap = r->queueMem.alloc<int32_t>(static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height));
     MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * static_cast<size_t>(r->cfg.width) * r->cfg.height, r->stream));
@@ -586,7 +609,7 @@ int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
 }
 
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
-    if (key == 1 && (value == 0 || value == 1)) {
+    if (key == 1 && value >= 0 && value <= 2) {
         r->ds.variant = value;
         return 0;
     }

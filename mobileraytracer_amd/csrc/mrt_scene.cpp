@@ -731,6 +731,75 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
     }
 }
 
+namespace {
+int32_t collapse4(const std::vector<HBVHNode>& nodes, int32_t b2, std::vector<GNode4>* out) {
+    std::vector<int32_t> ch{nodes[static_cast<size_t>(b2)].indexOffset, nodes[static_cast<size_t>(b2)].indexOffset + 1};
+    while (ch.size() < 4) {
+        int best = -1;
+        float bestArea = -1.0F;
+        for (size_t k = 0; k < ch.size(); ++k) {
+            const HBVHNode& c = nodes[static_cast<size_t>(ch[k])];
+            if (c.numPrimitives > 0) continue;
+            const v3 l = c.box.mx - c.box.mn;
+            const float area = l.x * l.y + l.y * l.z + l.z * l.x;
+            if (area > bestArea) {
+                bestArea = area;
+                best = static_cast<int>(k);
+            }
+        }
+        if (best < 0) break;
+        const int32_t open = ch[static_cast<size_t>(best)];
+        const int32_t l = nodes[static_cast<size_t>(open)].indexOffset;
+        ch[static_cast<size_t>(best)] = l;
+        ch.insert(ch.begin() + best + 1, l + 1);
+    }
+    const int32_t me = static_cast<int32_t>(out->size());
+    out->push_back(GNode4{});
+    GNode4 g{};
+    for (int k = 0; k < 4; ++k) {
+        if (k >= static_cast<int>(ch.size())) {
+            g.minx[k] = g.miny[k] = g.minz[k] = 1.0F;
+            g.maxx[k] = g.maxy[k] = g.maxz[k] = -1.0F;
+            g.ref[k] = kRefEmpty;
+            continue;
+        }
+        const HBVHNode& c = nodes[static_cast<size_t>(ch[static_cast<size_t>(k)])];
+        g.minx[k] = c.box.mn.x;
+        g.miny[k] = c.box.mn.y;
+        g.minz[k] = c.box.mn.z;
+        g.maxx[k] = c.box.mx.x;
+        g.maxy[k] = c.box.mx.y;
+        g.maxz[k] = c.box.mx.z;
+        g.ref[k] = c.numPrimitives > 0 ? leafRef(c.indexOffset, c.numPrimitives)
+                                       : collapse4(nodes, ch[static_cast<size_t>(k)], out);
+    }
+    (*out)[static_cast<size_t>(me)] = g;
+    return me;
+}
+}  // namespace
+
+void toDeviceBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode4>* out, GRoot* root) {
+    out->clear();
+    const HBVHNode& r = nodes[0];
+    root->bmin[0] = r.box.mn.x;
+    root->bmin[1] = r.box.mn.y;
+    root->bmin[2] = r.box.mn.z;
+    root->bmax[0] = r.box.mx.x;
+    root->bmax[1] = r.box.mx.y;
+    root->bmax[2] = r.box.mx.z;
+    root->count = static_cast<int32_t>(numPrims);
+    if (numPrims == 0) {
+        root->ref = 0;
+        return;
+    }
+    if (r.numPrimitives > 0) {
+        root->ref = leafRef(r.indexOffset, r.numPrimitives);
+        return;
+    }
+    out->reserve(nodes.size() / 2 + 1);
+    root->ref = collapse4(nodes, 0, out);
+}
+
 // ---- sample tables (Utils.cpp:43-53, Utils.hpp:209-218) ----------------------------------
 float haltonSequence(uint32_t index, uint32_t base) {
     float fraction = 1.0F;

@@ -26,13 +26,85 @@ __device__ __forceinline__ int popCulled(TStack& st, float lim, bool cull) {
 }
 
 // kAny = false: closest hit -> writes lv.hit;  kAny = true: shadow any-hit -> writes lv.sC.w
-template <bool kAny, bool kCount>
+// One BVH2 inner-node visit: returns the next node (near child, or a popped entry).
+__device__ __forceinline__ int innerStep2(const GNode* node, v3 o, v3 inv, float lim, bool cull, TStack& st,
+                                          TravCount* cnt, bool count) {
+    const float4* np = reinterpret_cast<const float4*>(node);
+    const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+    const int4 n3 = reinterpret_cast<const int4*>(np)[3];
+    if (count) cnt->nodes += 2;
+    float tl, tr;
+    bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
+    bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+    if (cull) {
+        hl = hl && !(tl > lim);
+        hr = hr && !(tr > lim);
+    }
+    if (hl && hr) {
+        int nearRef = n3.x, farRef = n3.y;
+        float farT = tr;
+        if (cull && tr < tl) {
+            nearRef = n3.y;
+            farRef = n3.x;
+            farT = tl;
+        }
+        st.push(farRef, farT);
+        return nearRef;
+    }
+    if (hl) return n3.x;
+    if (hr) return n3.y;
+    return popCulled(st, lim, cull);
+}
+
+__device__ __forceinline__ void cas(float& ka, int& ra, float& kb, int& rb) {
+    if (kb < ka) {
+        const float tk = ka;
+        ka = kb;
+        kb = tk;
+        const int tr = ra;
+        ra = rb;
+        rb = tr;
+    }
+}
+
+// One 4-wide visit: tests the four child boxes, pushes the hit children far-to-near.
+__device__ __forceinline__ int innerStep4(const GNode4* node, v3 o, v3 inv, float lim, bool cull, TStack& st,
+                                          TravCount* cnt, bool count) {
+    const float4* np = reinterpret_cast<const float4*>(node);
+    const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
+    const int4 cr = reinterpret_cast<const int4*>(np)[6];
+    if (count) cnt->nodes += (cr.x != kRefEmpty) + (cr.y != kRefEmpty) + (cr.z != kRefEmpty) + (cr.w != kRefEmpty);
+    constexpr float kInf = __builtin_huge_valf();
+    float t0, t1, t2, t3;
+    const bool h0 = cr.x != kRefEmpty && slab(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, &t0) && !(cull && t0 > lim);
+    const bool h1 = cr.y != kRefEmpty && slab(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, &t1) && !(cull && t1 > lim);
+    const bool h2 = cr.z != kRefEmpty && slab(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, &t2) && !(cull && t2 > lim);
+    const bool h3 = cr.w != kRefEmpty && slab(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, &t3) && !(cull && t3 > lim);
+    const int n = static_cast<int>(h0) + static_cast<int>(h1) + static_cast<int>(h2) + static_cast<int>(h3);
+    if (n == 0) return popCulled(st, lim, cull);
+    float k0 = h0 ? t0 : kInf, k1 = h1 ? t1 : kInf, k2 = h2 ? t2 : kInf, k3 = h3 ? t3 : kInf;
+    int r0 = cr.x, r1 = cr.y, r2 = cr.z, r3 = cr.w;
+    if (!h0) r0 = kRefEmpty;
+    if (!h1) r1 = kRefEmpty;
+    if (!h2) r2 = kRefEmpty;
+    if (!h3) r3 = kRefEmpty;
+    cas(k0, r0, k1, r1);  // 4-element sorting network, misses (inf) sink to the end
+    cas(k2, r2, k3, r3);
+    cas(k0, r0, k2, r2);
+    cas(k1, r1, k3, r3);
+    cas(k1, r1, k2, r2);
+    if (n > 3) st.push(r3, k3);
+    if (n > 2) st.push(r2, k2);
+    if (n > 1) st.push(r1, k1);
+    return r0;
+}
+
+template <bool kAny, bool kCount, int kWide>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                                 TStack& st, TravCount* cnt) {
     const int lane = static_cast<int>(threadIdx.x & 63u);
     const uint64_t lanesBelow = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const GNode* __restrict__ nodes = s.triNodes;
     int rayIdx = -1;
     bool exhausted = false;
     v3 o{0, 0, 0}, d{0, 0, 0}, inv{0, 0, 0};
@@ -97,7 +169,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     }
                     if (rayIdx >= 0) {
                         float te;
-                        const GRoot& r = s.triRoot;
+                        const GRoot& r = kWide == 4 ? s.triRoot4 : s.triRoot;
                         if (r.count > 0 &&
                             slab(r.bmin[0], r.bmin[1], r.bmin[2], r.bmax[0], r.bmax[1], r.bmax[2], o, inv, &te)) {
                             ref = r.ref;
@@ -116,34 +188,11 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         }
         // ---- inner nodes until every active lane holds a postponed leaf ----
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
-            const float4* np = reinterpret_cast<const float4*>(nodes + ref);
-            const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-            const int4 n3 = reinterpret_cast<const int4*>(np)[3];
-            if (kCount) cnt->nodes += 2;
-            float tl, tr;
-            bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
-            bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
             const float curLim = b.t + b.t * kCullMargin;
-            if (s.cull) {
-                hl = hl && !(tl > curLim);
-                hr = hr && !(tr > curLim);
-            }
-            if (hl && hr) {
-                int nearRef = n3.x, farRef = n3.y;
-                float farT = tr;
-                if (s.cull && tr < tl) {
-                    nearRef = n3.y;
-                    farRef = n3.x;
-                    farT = tl;
-                }
-                st.push(farRef, farT);
-                ref = nearRef;
-            } else if (hl) {
-                ref = n3.x;
-            } else if (hr) {
-                ref = n3.y;
+            if (kWide == 4) {
+                ref = innerStep4(s.triNodes4 + ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
             } else {
-                ref = popCulled(st, curLim, s.cull != 0);
+                ref = innerStep2(s.triNodes + ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
             }
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
