@@ -209,9 +209,7 @@ __device__ __forceinline__ int hitMaterial(const DScene& s, uint32_t code) {
 
 // Shader::getCosineSampleHemisphere (Shader.cpp:188-216); cos/sin evaluated in double and
 // rounded, which agrees with glibc cosf/sinf except in rare last-ulp cases.
-__device__ __forceinline__ v3 cosineHemisphere(const DScene& s, v3 n, uint32_t key, uint32_t tc) {
-    const float r1 = s.shaderTable[sampleIndex(key, tc, kPHemi1)];
-    const float r2 = s.shaderTable[sampleIndex(key, tc, kPHemi2)];
+__device__ __forceinline__ v3 cosineHemisphere(v3 n, float r1, float r2) {
     const float phi = kTwoPi * r1;
     const float cosTheta = sqrtf(r2);
     v3 u = fabsf(n.x) > 0.1F ? v3{0.0F, 1.0F, 0.0F} : v3{1.0F, 0.0F, 0.0F};
@@ -225,16 +223,14 @@ __device__ __forceinline__ v3 cosineHemisphere(const DScene& s, v3 n, uint32_t k
 
 // Light sample i of a shading point (Whitted.cpp:41-53, PathTracer.cpp:53-67):
 // returns false when cos <= 0 (no shadow ray is built).
-__device__ __forceinline__ bool lightSample(const DScene& s, const HitGeom& g, uint32_t key, uint32_t tc, int i,
+// pick / r / q: the three table draws of this sample (light choice, area-light point)
+__device__ __forceinline__ bool lightSample(const DScene& s, const HitGeom& g, float pick, float r, float q,
                                            v3* dirOut, float* distOut, v3* contribOut) {
-    const float pick = s.shaderTable[sampleIndex(key, tc, purposeLightPick(i))];
     const uint32_t chosen = static_cast<uint32_t>(floorf(pick * static_cast<float>(s.nLights) * 0.99999F));
     const float4* l = s.lights + 4 * chosen;
     const float4 a4 = l[0];
     v3 pos;
     if (__float_as_int(a4.w) == 1) {  // AreaLight::getPosition (AreaLight.cpp:17-26)
-        float r = s.samplerTable[sampleIndex(key, tc, purposeLightR(i))];
-        float q = s.samplerTable[sampleIndex(key, tc, purposeLightS(i))];
         if (r + q >= 1.0F) {
             r = 1.0F - r;
             q = 1.0F - q;
@@ -272,6 +268,11 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
         int mat = -1;
         uint32_t key = 0, tc = 0;
         bool wantD = false, wantS = false, wantT = false, direct = false;
+        // light sample 0 (kept in registers) and the prefetched table draws
+        v3 ld0{0, 0, 0}, lc0{0, 0, 0};
+        float dist0 = 0.0F;
+        bool ok0 = false;
+        float hemi1 = 0.0F, hemi2 = 0.0F;
         if (active) {
             const float4 o4 = lv.rO[i];
             const float4 d4 = lv.rD[i];
@@ -279,6 +280,13 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
             key = fbits(o4.w);
             tc = lv.tree[i];
             d = xyz(d4);
+            // issue every table gather of this vertex at once: their latencies overlap
+            const float pick0 = s.shaderTable[sampleIndex(key, tc, purposeLightPick(0))];
+            const float lr0 = s.samplerTable[sampleIndex(key, tc, purposeLightR(0))];
+            const float lq0 = s.samplerTable[sampleIndex(key, tc, purposeLightS(0))];
+            const float rr = s.samplerTable[sampleIndex(key, tc, kPRussian)];
+            hemi1 = s.shaderTable[sampleIndex(key, tc, kPHemi1)];
+            hemi2 = s.shaderTable[sampleIndex(key, tc, kPHemi2)];
             const uint32_t code = fbits(h.w);
             const uint32_t kind = primKind(code);
             // Shader.cpp:122: shade only if hit; Whitted.cpp:14-17 / PathTracer.cpp:25-28: depth cap
@@ -303,14 +311,19 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
                     g = hitGeometry(s, xyz(o4), d, h);
                     direct = hasPositive(Kd) && s.nLights > 0;
                     if (direct) {
-                        for (int k = 0; k < a.samplesLight; ++k) {
+                        ok0 = lightSample(s, g, pick0, lr0, lq0, &ld0, &dist0, &lc0);
+                        nShadow = static_cast<int>(ok0);
+                        for (int k = 1; k < a.samplesLight; ++k) {
                             v3 ld, lc;
                             float dist;
-                            if (lightSample(s, g, key, tc, k, &ld, &dist, &lc)) ++nShadow;
+                            if (lightSample(s, g, s.shaderTable[sampleIndex(key, tc, purposeLightPick(k))],
+                                            s.samplerTable[sampleIndex(key, tc, purposeLightR(k))],
+                                            s.samplerTable[sampleIndex(key, tc, purposeLightS(k))], &ld, &dist, &lc))
+                                ++nShadow;
                         }
                     }
                     if (kShader == kShaderPathTracer && hasPositive(Kd)) {  // PathTracer.cpp:89
-                        wantD = level <= kRayDepthMin || s.samplerTable[sampleIndex(key, tc, kPRussian)] > 0.5F;
+                        wantD = level <= kRayDepthMin || rr > 0.5F;
                     }
                     wantS = hasPositive(Ks);
                     wantT = hasPositive(Kt);
@@ -330,9 +343,15 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
         int written = 0;
         if (direct) {
             for (int k = 0; k < a.samplesLight; ++k) {
-                v3 ld, lc;
-                float dist;
-                if (!lightSample(s, g, key, tc, k, &ld, &dist, &lc)) continue;
+                v3 ld = ld0, lc = lc0;
+                float dist = dist0;
+                if (k == 0) {
+                    if (!ok0) continue;
+                } else if (!lightSample(s, g, s.shaderTable[sampleIndex(key, tc, purposeLightPick(k))],
+                                        s.samplerTable[sampleIndex(key, tc, purposeLightR(k))],
+                                        s.samplerTable[sampleIndex(key, tc, purposeLightS(k))], &ld, &dist, &lc)) {
+                    continue;
+                }
                 const int j = shadowBase + written;
                 ++written;
                 if (j < lv.shadowCap) {
@@ -358,7 +377,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
             nx.tree[j] = tc * 4u + slot;
             return j;
         };
-        if (wantD) child.x = emit(cosineHemisphere(s, g.N, key, tc), 1u);
+        if (wantD) child.x = emit(cosineHemisphere(g.N, hemi1, hemi2), 1u);
         if (wantS) child.y = emit(reflect(d, g.N), 2u);
         if (wantT) child.z = emit(refract(d, g.N, 1.0F / ior), 3u);
         lv.vtxA[i] = make_int4(mat, shadowBase, nShadow, 0);
