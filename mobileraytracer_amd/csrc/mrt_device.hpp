@@ -16,7 +16,8 @@
 namespace mrt {
 
 constexpr int kBlock = 256;         // threads per workgroup for every trace kernel
-constexpr int kLdsStack = 16;       // per-thread short stack in LDS (entries of 8 bytes)
+constexpr int kLdsStack = 16;       // max per-thread short stack in LDS (entries of 8 bytes)
+constexpr int kLdsStackMin = 8;     // smallest LDS stack a kernel variant uses (sizes the spill area)
 constexpr float kCullMargin = 0x1p-10f;
 
 struct DScene {
@@ -65,23 +66,24 @@ __device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx,
     return tMax >= e;
 }
 
-// Short traversal stack: the top kLdsStack entries live in LDS (conflict-free layout
-// [slot][thread]), deeper entries spill to a per-thread global area.
+// Short traversal stack: the top `depth` (power of two) entries live in LDS (conflict-free
+// layout [slot][thread]), deeper entries spill to a per-thread global area.
 struct TStack {
     int2* lds;   // &ldsBase[threadIdx.x]; slot s at lds[s * kBlock]
     int2* glob;  // per-thread overflow area
     int sp;
+    int depth;
     __device__ __forceinline__ void push(int ref, float t) {
-        const int slot = sp & (kLdsStack - 1);
-        if (sp >= kLdsStack) glob[sp - kLdsStack] = lds[slot * kBlock];
+        const int slot = sp & (depth - 1);
+        if (sp >= depth) glob[sp - depth] = lds[slot * kBlock];
         lds[slot * kBlock] = make_int2(ref, __float_as_int(t));
         ++sp;
     }
     __device__ __forceinline__ int2 pop() {
         --sp;
-        const int slot = sp & (kLdsStack - 1);
+        const int slot = sp & (depth - 1);
         const int2 v = lds[slot * kBlock];
-        if (sp >= kLdsStack) lds[slot * kBlock] = glob[sp - kLdsStack];
+        if (sp >= depth) lds[slot * kBlock] = glob[sp - depth];
         return v;
     }
 };

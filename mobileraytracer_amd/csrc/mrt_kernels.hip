@@ -19,6 +19,8 @@
 #include "mrt_kernels.hpp"
 #include "mrt_trace_ww.hpp"
 
+#include <algorithm>
+
 namespace mrt {
 
 // ---------------------------------------------------------------------------------------
@@ -101,16 +103,29 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
 }
 
 // ---------------------------------------------------------------------------------------
+// Trace-kernel variants (identical results; tools/perf_sweep.py A/Bs them):
+//   0 per-wave 64-ray batches, if-if walk (BVH2)        1 while-while + per-lane refill (BVH2)
+//   2 as 1 on the 4-wide BVH                            3 as 1, refill only when >= 16 lanes idle
+//   4 as 1, refill when >= 32 lanes idle                5 as 3 with an 8-entry LDS stack
+//   6 as 3 on the 4-wide BVH
+template <int kVariant>
+struct TraceCfg {
+    static constexpr int kWide = (kVariant == 2 || kVariant == 6) ? 4 : 2;
+    static constexpr int kRefill = kVariant == 3 || kVariant == 5 || kVariant == 6 ? 16 : (kVariant == 4 ? 32 : 1);
+    static constexpr int kStack = kVariant == 5 ? 8 : kLdsStack;
+};
+
 template <bool kCount, int kVariant>
 __global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* counters, int level, int2* gstack,
                                                   int gdepth, unsigned long long* stats) {
-    __shared__ int2 ldsStack[kLdsStack * kBlock];
-    TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0};
+    using C = TraceCfg<kVariant>;
+    __shared__ int2 ldsStack[C::kStack * kBlock];
+    TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
+              C::kStack};
     const int count = min(counters[kCntRays + level], lv.cap);
     int* fetch = counters + kCntFetchTrace + level;
     TravCount cnt{0u, 0u};
-    if (kVariant == 1) traceWhileWhile<false, kCount, 2>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
-    if (kVariant == 2) traceWhileWhile<false, kCount, 4>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
+    if (kVariant > 0) traceWhileWhile<false, kCount, C::kWide, C::kRefill>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -140,13 +155,14 @@ __global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* count
 template <bool kCount, int kVariant>
 __global__ __launch_bounds__(kBlock) void k_shadow(DScene s, Level lv, int* counters, int level, int2* gstack,
                                                    int gdepth, unsigned long long* stats) {
-    __shared__ int2 ldsStack[kLdsStack * kBlock];
-    TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0};
+    using C = TraceCfg<kVariant>;
+    __shared__ int2 ldsStack[C::kStack * kBlock];
+    TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
+              C::kStack};
     const int count = min(counters[kCntShadows + level], lv.shadowCap);
     int* fetch = counters + kCntFetchShadow + level;
     TravCount cnt{0u, 0u};
-    if (kVariant == 1) traceWhileWhile<true, kCount, 2>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
-    if (kVariant == 2) traceWhileWhile<true, kCount, 4>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
+    if (kVariant > 0) traceWhileWhile<true, kCount, C::kWide, C::kRefill>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -495,25 +511,23 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
     hipLaunchKernelGGL(k_raygen, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, a, lv, counters);
 }
 
+#define MRT_LAUNCH_ONE(KERNEL, V)                                                                           \
+    case V:                                                                                                  \
+        if (countStats)                                                                                      \
+            hipLaunchKernelGGL((KERNEL<true, V>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        else                                                                                                 \
+            hipLaunchKernelGGL((KERNEL<false, V>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        break;
 #define MRT_LAUNCH_TRACE(KERNEL)                                                                              \
-    do {                                                                                                     \
-        if (s.variant == 2) {                                                                                \
-            if (countStats)                                                                                  \
-                hipLaunchKernelGGL((KERNEL<true, 2>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-            else                                                                                             \
-                hipLaunchKernelGGL((KERNEL<false, 2>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-        } else if (s.variant == 1) {                                                                         \
-            if (countStats)                                                                                  \
-                hipLaunchKernelGGL((KERNEL<true, 1>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-            else                                                                                             \
-                hipLaunchKernelGGL((KERNEL<false, 1>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-        } else {                                                                                             \
-            if (countStats)                                                                                  \
-                hipLaunchKernelGGL((KERNEL<true, 0>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-            else                                                                                             \
-                hipLaunchKernelGGL((KERNEL<false, 0>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-        }                                                                                                    \
-    } while (0)
+    switch (s.variant) {                                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, 0)                                                                            \
+        MRT_LAUNCH_ONE(KERNEL, 1)                                                                            \
+        MRT_LAUNCH_ONE(KERNEL, 2)                                                                            \
+        MRT_LAUNCH_ONE(KERNEL, 3)                                                                            \
+        MRT_LAUNCH_ONE(KERNEL, 4)                                                                            \
+        MRT_LAUNCH_ONE(KERNEL, 5)                                                                            \
+        default: MRT_LAUNCH_ONE(KERNEL, 6)                                                                   \
+    }
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
@@ -564,8 +578,12 @@ void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStre
 
 int traceOccupancyBlocksPerCU() {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 1>, kBlock, 0) != hipSuccess) n = 4;
-    return n > 0 ? n : 1;
+    // persistent grids: size for the variant with the highest residency; surplus blocks of a
+    // lower-residency variant start as others retire and find the work cursor exhausted
+    int best = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 1>, kBlock, 0) == hipSuccess) best = std::max(best, n);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 5>, kBlock, 0) == hipSuccess) best = std::max(best, n);
+    return best;
 }
 
 }  // namespace mrt

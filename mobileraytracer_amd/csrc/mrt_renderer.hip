@@ -352,7 +352,7 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     }
     r->counters = r->queueMem.alloc<int>(kNumCounters);
     r->stats = r->queueMem.alloc<unsigned long long>(kNumStats);
-    r->gdepth = std::max(1, r->stackNeed - kLdsStack);
+    r->gdepth = std::max(1, r->stackNeed - kLdsStackMin);
     r->gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceGrid) * kBlock * static_cast<size_t>(r->gdepth));
     r->dBitmap = r->queueMem.alloc<int32_t>(static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height));
     MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * static_cast<size_t>(r->cfg.width) * r->cfg.height, r->stream));
@@ -609,7 +609,7 @@ int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
 }
 
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
-    if (key == 1 && value >= 0 && value <= 2) {
+    if (key == 1 && value >= 0 && value <= 6) {
         r->ds.variant = value;
         return 0;
     }

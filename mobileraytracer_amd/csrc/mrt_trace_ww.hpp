@@ -99,7 +99,7 @@ __device__ __forceinline__ int innerStep4(const GNode4* node, v3 o, v3 inv, floa
     return r0;
 }
 
-template <bool kAny, bool kCount, int kWide>
+template <bool kAny, bool kCount, int kWide, int kRefill>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                                 TStack& st, TravCount* cnt) {
@@ -133,8 +133,13 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             rayIdx = -1;
         }
         // ---- refill lanes without a ray (one atomic per wave) ----
-        const bool need = rayIdx < 0 && !exhausted;
-        const uint64_t needMask = __ballot(need);
+        bool need = rayIdx < 0 && !exhausted;
+        uint64_t needMask = __ballot(need);
+        // refill only once enough lanes are idle (fewer, larger fetches), or when none is busy
+        if (kRefill > 1 && __popcll(needMask) < kRefill && __ballot(rayIdx >= 0) != 0) {
+            need = false;
+            needMask = 0;
+        }
         if (needMask != 0) {
             const int n = __popcll(needMask);
             const int leader = __ffsll(static_cast<unsigned long long>(needMask)) - 1;

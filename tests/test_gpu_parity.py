@@ -200,6 +200,25 @@ def test_chunked_passes_and_cull_are_invariant():
     assert np.array_equal(a, b) and ra == rb
 
 
+def test_trace_kernel_variants_are_identical():
+    """Every trace-kernel organisation (per-wave batches / while-while + refill / 4-wide BVH)
+    returns the same hits, images and ray counts."""
+    import mobileraytracer_amd as m
+    for cfg in (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+                make_cfg(128, 128, shader=2, scene="water", spp=2), make_cfg(64, 64, shader=1)):
+        outs = []
+        with m.Renderer(cfg) as r:
+            for v in (0, 1, 2):
+                r.set_tuning(1, v)
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"], r.primary_hits()))
+        for bm, rays, shadows, hits in outs[1:]:
+            assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
+            assert all(np.array_equal(a, b) for a, b in zip(hits, outs[0][3]))
+
+
 def _render_shards(cfg_kw, world):
     """Render every shard separately into a device-packed buffer, gather, unpack on 'rank 0'."""
     import torch

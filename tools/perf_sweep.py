@@ -13,11 +13,11 @@ def main():
     r = m.Renderer(cfg)
     d = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
-    variants = [int(v) for v in os.environ.get("VARIANTS", "1,2").split(",")]
+    variants = [int(v) for v in os.environ.get("VARIANTS", "1,3,4,5,6,2").split(",")]
     imgs = {}
     res = {v: [] for v in variants}
     r.set_profiling(timing=True)
-    for rnd in range(4):
+    for rnd in range(3):
         for v in variants:
             r.set_tuning(1, v)
             r.render_frame_device(d.data_ptr(), 0, sh)
