@@ -119,9 +119,12 @@ MRT_HD uint32_t pathKey(uint32_t pixelIndex, uint32_t globalSample) {
     return hash32(pixelIndex * 0x9E3779B9u ^ hash32(globalSample + 0x632BE5ABu));
 }
 // treeCode: 1 for the camera ray's vertex; child = code * 4 + slot (slot 1 diffuse,
-// 2 specular, 3 transmission).  purpose: one of the kP* constants below.
+// 2 specular, 3 transmission).  purpose: one of the kP* constants below.  The draws of one
+// vertex are CONSECUTIVE table entries from a hashed start, as the reference's sampler
+// cursors hand out consecutive entries (Sampler.hpp:58-63, Shader.cpp:189-194); on the GPU
+// this keeps a vertex's draws in one or two cache lines per table.
 MRT_HD uint32_t sampleIndex(uint32_t key, uint32_t treeCode, uint32_t purpose) {
-    return hash32(key ^ hash32(treeCode * 1024u + purpose)) & kArrayMask;
+    return (hash32(key ^ hash32(treeCode * 0x9E3779B9u + 0x7F4A7C15u)) + purpose) & kArrayMask;
 }
 // purposes
 constexpr uint32_t kPJitterU = 0;   // pixel sampler, r1   (Renderer.cpp:137)

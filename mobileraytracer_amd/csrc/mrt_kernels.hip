@@ -107,25 +107,33 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
 //   0 per-wave 64-ray batches, if-if walk (BVH2)        1 while-while + per-lane refill (BVH2)
 //   2 as 1 on the 4-wide BVH                            3 as 1, refill only when >= 16 lanes idle
 //   4 as 1, refill when >= 32 lanes idle                5 as 3 with an 8-entry LDS stack
-//   6 as 3 on the 4-wide BVH
+//   6 as 3 on the 4-wide BVH                            7 as 4 with 8 per-XCD-group work cursors
+//   8 as 7 with an 8-entry LDS stack                    9 as 1, refill when >= 48 lanes idle
+//  10 as 8 compiled for 8 waves per SIMD
 template <int kVariant>
 struct TraceCfg {
     static constexpr int kWide = (kVariant == 2 || kVariant == 6) ? 4 : 2;
-    static constexpr int kRefill = kVariant == 3 || kVariant == 5 || kVariant == 6 ? 16 : (kVariant == 4 ? 32 : 1);
-    static constexpr int kStack = kVariant == 5 ? 8 : kLdsStack;
+    static constexpr int kRefill = (kVariant == 3 || kVariant == 5 || kVariant == 6) ? 16
+                                   : (kVariant == 4 || kVariant == 7 || kVariant == 8 || kVariant == 10) ? 32
+                                   : (kVariant == 9 ? 48 : 1);
+    static constexpr int kStack = (kVariant == 5 || kVariant == 8 || kVariant == 10) ? 8 : kLdsStack;
+    static constexpr int kShards = (kVariant == 7 || kVariant == 8 || kVariant == 10) ? kFetchShards : 1;
+    static constexpr int kMinWaves = kVariant == 10 ? 8 : 1;
 };
 
 template <bool kCount, int kVariant>
-__global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* counters, int level, int2* gstack,
+__global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_trace(DScene s, Level lv, int* counters, int level, int2* gstack,
                                                   int gdepth, unsigned long long* stats) {
     using C = TraceCfg<kVariant>;
     __shared__ int2 ldsStack[C::kStack * kBlock];
     TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
               C::kStack};
     const int count = min(counters[kCntRays + level], lv.cap);
-    int* fetch = counters + kCntFetchTrace + level;
+    int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kFetchShards * kFetchStride
+                                : counters + kCntFetchTrace + level;
     TravCount cnt{0u, 0u};
-    if (kVariant > 0) traceWhileWhile<false, kCount, C::kWide, C::kRefill>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
+    if (kVariant > 0)
+        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -153,16 +161,19 @@ __global__ __launch_bounds__(kBlock) void k_trace(DScene s, Level lv, int* count
 }
 
 template <bool kCount, int kVariant>
-__global__ __launch_bounds__(kBlock) void k_shadow(DScene s, Level lv, int* counters, int level, int2* gstack,
+__global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_shadow(DScene s, Level lv, int* counters, int level, int2* gstack,
                                                    int gdepth, unsigned long long* stats) {
     using C = TraceCfg<kVariant>;
     __shared__ int2 ldsStack[C::kStack * kBlock];
     TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
               C::kStack};
     const int count = min(counters[kCntShadows + level], lv.shadowCap);
-    int* fetch = counters + kCntFetchShadow + level;
+    int* fetch = C::kShards > 1
+                     ? counters + kCntFetchShards + (kMaxLevels + level) * kFetchShards * kFetchStride
+                     : counters + kCntFetchShadow + level;
     TravCount cnt{0u, 0u};
-    if (kVariant > 0) traceWhileWhile<true, kCount, C::kWide, C::kRefill>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
+    if (kVariant > 0)
+        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -526,7 +537,11 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
         MRT_LAUNCH_ONE(KERNEL, 3)                                                                            \
         MRT_LAUNCH_ONE(KERNEL, 4)                                                                            \
         MRT_LAUNCH_ONE(KERNEL, 5)                                                                            \
-        default: MRT_LAUNCH_ONE(KERNEL, 6)                                                                   \
+        MRT_LAUNCH_ONE(KERNEL, 6)                                                                            \
+        MRT_LAUNCH_ONE(KERNEL, 7)                                                                            \
+        MRT_LAUNCH_ONE(KERNEL, 8)                                                                            \
+        MRT_LAUNCH_ONE(KERNEL, 9)                                                                            \
+        default: MRT_LAUNCH_ONE(KERNEL, 10)                                                                  \
     }
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
@@ -583,6 +598,7 @@ int traceOccupancyBlocksPerCU() {
     int best = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 1>, kBlock, 0) == hipSuccess) best = std::max(best, n);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 5>, kBlock, 0) == hipSuccess) best = std::max(best, n);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 10>, kBlock, 0) == hipSuccess) best = std::max(best, n);
     return best;
 }
 

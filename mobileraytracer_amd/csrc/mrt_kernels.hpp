@@ -16,7 +16,8 @@ constexpr int kCntShadows = kMaxLevels;
 constexpr int kCntFetchTrace = 2 * kMaxLevels;
 constexpr int kCntFetchShadow = 3 * kMaxLevels;
 constexpr int kCntOverflow = 4 * kMaxLevels;
-constexpr int kNumCounters = 4 * kMaxLevels + 4;  // 16-byte multiple
+constexpr int kCntFetchShards = 4 * kMaxLevels + 32;  // 2 kinds x kMaxLevels x 8 cursors x 32 ints
+constexpr int kNumCounters = kCntFetchShards + 2 * kMaxLevels * 8 * 32;
 
 // 64-bit statistics accumulated on the device across a frame
 constexpr int kStatRays = 0;        // rays of every level (camera + diffuse + specular + transmission)

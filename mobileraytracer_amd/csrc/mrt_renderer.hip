@@ -609,7 +609,7 @@ int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
 }
 
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
-    if (key == 1 && value >= 0 && value <= 6) {
+    if (key == 1 && value >= 0 && value <= 10) {
         r->ds.variant = value;
         return 0;
     }

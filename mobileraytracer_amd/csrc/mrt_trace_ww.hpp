@@ -99,7 +99,10 @@ __device__ __forceinline__ int innerStep4(const GNode4* node, v3 o, v3 inv, floa
     return r0;
 }
 
-template <bool kAny, bool kCount, int kWide, int kRefill>
+constexpr int kFetchShards = 8;   // work cursors per level for the sharded variants
+constexpr int kFetchStride = 32;  // ints between cursors (one 128-byte line each)
+
+template <bool kAny, bool kCount, int kWide, int kRefill, int kShards>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                                 TStack& st, TravCount* cnt) {
@@ -112,6 +115,8 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
     Best b{kRayLengthMax, 0.0F, 0.0F, kNoPrim};
     int ref = kRefDone;
     int leaf = 0;  // < 0: a postponed leaf
+    int seg = static_cast<int>(blockIdx.x % kShards);  // wave-uniform cursor state
+    int segsLeft = kShards;
     while (true) {
         // ---- lanes whose triangle walk is over: lights (closest only), write the result ----
         if (rayIdx >= 0 && ref == kRefDone && leaf >= 0) {
@@ -141,16 +146,43 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             needMask = 0;
         }
         if (needMask != 0) {
-            const int n = __popcll(needMask);
-            const int leader = __ffsll(static_cast<unsigned long long>(needMask)) - 1;
-            int base = 0;
-            if (lane == leader) base = atomicAdd(fetch, n);
-            base = __shfl(base, leader, 64);
+            int got = -1;
+            if (kShards == 1) {
+                const int n = __popcll(needMask);
+                const int leader = __ffsll(static_cast<unsigned long long>(needMask)) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(fetch, n);
+                base = __shfl(base, leader, 64);
+                got = base + __popcll(needMask & lanesBelow);
+                if (got >= count) got = -1;
+            } else {
+                // per-XCD-group cursors over contiguous ray ranges; an empty range is left
+                // for the next one (speed only: any placement gives the same results)
+                uint64_t pending = needMask;
+                while (pending != 0 && segsLeft > 0) {
+                    const int n = __popcll(pending);
+                    const int leader = __ffsll(static_cast<unsigned long long>(pending)) - 1;
+                    int base = 0;
+                    if (lane == leader) base = atomicAdd(fetch + seg * kFetchStride, n);
+                    base = __shfl(base, leader, 64);
+                    const int segStart = static_cast<int>((static_cast<long long>(count) * seg) / kShards);
+                    const int segEnd = static_cast<int>((static_cast<long long>(count) * (seg + 1)) / kShards);
+                    const bool mine = ((pending >> lane) & 1ull) != 0;
+                    if (mine) {
+                        const int idx = segStart + base + __popcll(pending & lanesBelow);
+                        if (idx < segEnd) got = idx;
+                    }
+                    pending = __ballot(mine && got < 0);
+                    if (pending != 0) {
+                        seg = (seg + 1) % kShards;
+                        --segsLeft;
+                    }
+                }
+            }
             if (need) {
-                rayIdx = base + __popcll(needMask & lanesBelow);
-                if (rayIdx >= count) {
+                rayIdx = got;
+                if (rayIdx < 0) {
                     exhausted = true;
-                    rayIdx = -1;
                 } else {
                     const float4 o4 = rOs[rayIdx];
                     const float4 d4 = rDs[rayIdx];

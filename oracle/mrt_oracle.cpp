@@ -113,7 +113,7 @@ uint32_t pathKey(uint32_t pixelIndex, uint32_t globalSample) {
     return hash32(pixelIndex * 0x9E3779B9u ^ hash32(globalSample + 0x632BE5ABu));
 }
 uint32_t sampleIndex(uint32_t key, uint32_t treeCode, uint32_t purpose) {
-    return hash32(key ^ hash32(treeCode * 1024u + purpose)) & ArrayMask;
+    return (hash32(key ^ hash32(treeCode * 0x9E3779B9u + 0x7F4A7C15u)) + purpose) & ArrayMask;
 }
 enum Purpose : uint32_t { P_JITTER_U = 0, P_JITTER_V = 1, P_RUSSIAN = 2, P_HEMI1 = 3, P_HEMI2 = 4, P_LIGHT = 8 };
 

@@ -13,7 +13,7 @@ def main():
     r = m.Renderer(cfg)
     d = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
-    variants = [int(v) for v in os.environ.get("VARIANTS", "1,3,4,5,6,2").split(",")]
+    variants = [int(v) for v in os.environ.get("VARIANTS", "4,7,8,9,10,1").split(",")]
     imgs = {}
     res = {v: [] for v in variants}
     r.set_profiling(timing=True)
