@@ -85,6 +85,7 @@ typedef struct mrt_frame_stats {
     double frameMs;         /* profiling: whole frame on the render stream */
     int64_t traceLaunches;
     int64_t shadowLaunches;
+    double shadeMs;         /* profiling: summed duration of the shading launches */
 } mrt_frame_stats;
 
 const char *mrt_last_error(void);
@@ -105,9 +106,11 @@ int mrt_get_scene_info(const mrt_renderer *r, mrt_scene_info *info);
 int mrt_set_profiling(mrt_renderer *r, int32_t flags);
 int mrt_get_frame_stats(const mrt_renderer *r, mrt_frame_stats *stats);
 /* tuning knobs for A/B measurement (results are identical for every value):
- * key 1 = trace kernel organisation (0 per-wave batches, 1 while-while + per-lane refill),
+ * key 1 = trace kernel organisation, 0..15 (mrt_kernels.hip kTraceCfg: 0 per-wave batches,
+ *         others while-while walks with refill threshold / LDS stack / work-cursor options),
  * key 2 = near-first traversal with conservative t-culling (1) or the reference visit set (0) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
+int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /
  * 4 light; index in the scene's input order (-1 on miss); t = hit distance */
 int mrt_primary_hits(mrt_renderer *r, int32_t *kind, int32_t *index, float *t);

@@ -116,6 +116,11 @@ class Renderer:
         """A/B knobs (identical results): 1 = trace kernel variant, 2 = t-culling."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 
+    def get_tuning(self, key: int) -> int:
+        v = ctypes.c_int32(0)
+        _native.check(self._lib.mrt_get_tuning(self._h, key, ctypes.byref(v)))
+        return v.value
+
     def frame_stats(self) -> dict:
         s = _native.MrtFrameStats()
         _native.check(self._lib.mrt_get_frame_stats(self._h, ctypes.byref(s)))

@@ -31,8 +31,8 @@ struct DScene {
     const GNode* sphereNodes;
     const float4* lights;      // 4 per light: A or position (w = kind bits), AB, AC, Le
     const float4* mats;        // 4 per material: Le (w = ior), Kd, Ks, Kt
-    const float* shaderTable;  // 2^20 shuffled Halton values (Shader.cpp:23)
-    const float* samplerTable; // 2^20 shuffled Halton values (StaticHaltonSeq.cpp)
+    const float2* tables;  // 2^20 x {shader (Shader.cpp:23), sampler (StaticHaltonSeq.cpp)}
+                           // shuffled Halton values
     GRoot triRoot, triRoot4, planeRoot, sphereRoot;
     int32_t nLights;
     int32_t nMats;

@@ -20,6 +20,7 @@
 #include "mrt_trace_ww.hpp"
 
 #include <algorithm>
+#include <utility>
 
 namespace mrt {
 
@@ -50,6 +51,41 @@ __device__ __forceinline__ int waveAlloc(int* counter, int n) {
     return base + excl;
 }
 
+// Allocates nLo / nHi slots per thread from a pair of adjacent int counters {lo, hi} with
+// ONE 64-bit atomic per block (same-address atomics serialise at the memory side: per-wave
+// allocation made them the shading kernel's limiter).  Every thread of the block must call
+// it; lds holds 2 x (waves + 1) entries, alternated by the caller's parity.
+__device__ __forceinline__ void blockAllocPair(unsigned long long* pair, int nLo, int nHi, int* baseLo, int* baseHi,
+                                               unsigned long long* lds, int parity) {
+    constexpr int kWaves = kBlock / 64;
+    const int lane = laneId();
+    const int wave = static_cast<int>(threadIdx.x >> 6);
+    const unsigned long long v =
+        (static_cast<unsigned long long>(static_cast<unsigned>(nHi)) << 32) | static_cast<unsigned>(nLo);
+    unsigned long long x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    unsigned long long* buf = lds + parity * (kWaves + 1);
+    if (lane == 63) buf[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long sum = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            const unsigned long long t = buf[w];
+            buf[w] = sum;
+            sum += t;
+        }
+        buf[kWaves] = sum != 0 ? atomicAdd(pair, sum) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long e = buf[kWaves] + buf[wave] + (x - v);
+    *baseLo = static_cast<int>(static_cast<unsigned>(e & 0xFFFFFFFFull));
+    *baseHi = static_cast<int>(static_cast<unsigned>(e >> 32));
+}
+
 // ---------------------------------------------------------------------------------------
 // pixel mapping: path p -> (pixel slot, sample); slot -> (x, y) through the unit table
 __device__ __forceinline__ void slotToXY(const PixelMap& m, int slot, int* x, int* y) {
@@ -67,7 +103,7 @@ __device__ __forceinline__ void slotToXY(const PixelMap& m, int slot, int* x, in
 
 __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* counters) {
     const int p = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
-    if (p == 0) counters[kCntRays + 1] = a.nPaths;
+    if (p == 0) counters[cntRays(1)] = a.nPaths;
     if (p >= a.nPaths) return;
     const int slot = a.slotBase + p / a.spp;
     const int s = p % a.spp;
@@ -84,8 +120,8 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
     const float v = static_cast<float>(y) * invH;
     float r1 = 0.5F, r2 = 0.5F;  // Constant(0.5) when spp <= 1 (C_wrapper.cpp:144-148)
     if (a.sppTotal > 1) {
-        r1 = a.samplerTable[sampleIndex(key, 0u, kPJitterU)];
-        r2 = a.samplerTable[sampleIndex(key, 0u, kPJitterV)];
+        r1 = a.tables[sampleIndex(key, 0u, kPJitterU)].y;
+        r2 = a.tables[sampleIndex(key, 0u, kPJitterV)].y;
     }
     const float devU = (r1 - 0.5F) * 2.0F * pixW;
     const float devV = (r2 - 0.5F) * 2.0F * pixH;
@@ -103,22 +139,41 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
 }
 
 // ---------------------------------------------------------------------------------------
-// Trace-kernel variants (identical results; tools/perf_sweep.py A/Bs them):
-//   0 per-wave 64-ray batches, if-if walk (BVH2)        1 while-while + per-lane refill (BVH2)
-//   2 as 1 on the 4-wide BVH                            3 as 1, refill only when >= 16 lanes idle
-//   4 as 1, refill when >= 32 lanes idle                5 as 3 with an 8-entry LDS stack
-//   6 as 3 on the 4-wide BVH                            7 as 4 with 8 per-XCD-group work cursors
-//   8 as 7 with an 8-entry LDS stack                    9 as 1, refill when >= 48 lanes idle
-//  10 as 8 compiled for 8 waves per SIMD
+// Trace-kernel variants (identical results; tools/perf_sweep.py A/Bs them).  Columns:
+// BVH width, refill threshold (idle lanes before a wave fetches new rays; 1 = per lane),
+// LDS stack entries, work cursors (8 = one per XCD group of workgroups), min waves per SIMD.
+//   0 per-wave 64-ray batches, if-if walk (BVH2); the rest are while-while walks.
+struct TraceCfgRow {
+    int wide, refill, stack, shards, minWaves;  // shards <= kMaxFetchShards
+};
+constexpr TraceCfgRow kTraceCfg[] = {
+    {2, 1, kLdsStack, 1, 1},             // 0
+    {2, 1, kLdsStack, 1, 1},             // 1
+    {4, 1, kLdsStack, 1, 1},             // 2
+    {2, 16, kLdsStack, 1, 1},            // 3
+    {2, 32, kLdsStack, 1, 1},            // 4
+    {2, 16, 8, 1, 1},                    // 5
+    {4, 16, kLdsStack, 1, 1},            // 6
+    {2, 32, kLdsStack, 8, 1},            // 7
+    {2, 32, 8, 8, 1},                    // 8
+    {2, 48, kLdsStack, 1, 1},            // 9
+    {2, 32, 8, 16, 1},                   // 10
+    {2, 32, 8, 32, 1},                   // 11
+    {2, 32, 4, 8, 1},                    // 12
+    {2, 16, 8, 8, 1},                    // 13
+    {2, 16, 8, 32, 1},                   // 14
+    {2, 8, 8, 32, 1},                    // 15
+};
+constexpr int kNumTraceVariants = sizeof(kTraceCfg) / sizeof(kTraceCfg[0]);
+static_assert(kNumTraceVariants == kTraceVariants, "mrt_kernels.hpp kTraceVariants");
+
 template <int kVariant>
 struct TraceCfg {
-    static constexpr int kWide = (kVariant == 2 || kVariant == 6) ? 4 : 2;
-    static constexpr int kRefill = (kVariant == 3 || kVariant == 5 || kVariant == 6) ? 16
-                                   : (kVariant == 4 || kVariant == 7 || kVariant == 8 || kVariant == 10) ? 32
-                                   : (kVariant == 9 ? 48 : 1);
-    static constexpr int kStack = (kVariant == 5 || kVariant == 8 || kVariant == 10) ? 8 : kLdsStack;
-    static constexpr int kShards = (kVariant == 7 || kVariant == 8 || kVariant == 10) ? kFetchShards : 1;
-    static constexpr int kMinWaves = kVariant == 10 ? 8 : 1;
+    static constexpr int kWide = kTraceCfg[kVariant].wide;
+    static constexpr int kRefill = kTraceCfg[kVariant].refill;
+    static constexpr int kStack = kTraceCfg[kVariant].stack;
+    static constexpr int kShards = kTraceCfg[kVariant].shards;
+    static constexpr int kMinWaves = kTraceCfg[kVariant].minWaves;
 };
 
 template <bool kCount, int kVariant>
@@ -128,8 +183,8 @@ __global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_trace
     __shared__ int2 ldsStack[C::kStack * kBlock];
     TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
               C::kStack};
-    const int count = min(counters[kCntRays + level], lv.cap);
-    int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kFetchShards * kFetchStride
+    const int count = min(counters[cntRays(level)], lv.cap);
+    int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride
                                 : counters + kCntFetchTrace + level;
     TravCount cnt{0u, 0u};
     if (kVariant > 0)
@@ -167,9 +222,9 @@ __global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_shado
     __shared__ int2 ldsStack[C::kStack * kBlock];
     TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
               C::kStack};
-    const int count = min(counters[kCntShadows + level], lv.shadowCap);
+    const int count = min(counters[cntShadows(level)], lv.shadowCap);
     int* fetch = C::kShards > 1
-                     ? counters + kCntFetchShards + (kMaxLevels + level) * kFetchShards * kFetchStride
+                     ? counters + kCntFetchShards + (kMaxLevels + level) * kMaxFetchShards * kFetchStride
                      : counters + kCntFetchShadow + level;
     TravCount cnt{0u, 0u};
     if (kVariant > 0)
@@ -278,10 +333,13 @@ __device__ __forceinline__ bool lightSample(const DScene& s, const HitGeom& g, f
 }
 
 template <int kShader>
-__global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
-    const int count = min(counters[kCntRays + level], lv.cap);
-    int* nextCount = counters + kCntRays + level + 1;
-    int* shadowCount = counters + kCntShadows + level;
+__global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
+    const int count = min(counters[cntRays(level)], lv.cap);
+    // {rays of level+1, shadow rays of level}: one 64-bit allocation per block and iteration
+    auto* pair = reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1));
+    static_assert(cntShadows(1) == cntRays(2) + 1, "pair layout");
+    __shared__ unsigned long long allocLds[2 * (kBlock / 64 + 1)];
+    int parity = 0;
     for (int base = static_cast<int>(blockIdx.x * blockDim.x); base < count;
          base += static_cast<int>(gridDim.x * blockDim.x)) {
         const int i = base + static_cast<int>(threadIdx.x);
@@ -308,12 +366,12 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
             tc = lv.tree[i];
             d = xyz(d4);
             // issue every table gather of this vertex at once: their latencies overlap
-            const float pick0 = s.shaderTable[sampleIndex(key, tc, purposeLightPick(0))];
-            const float lr0 = s.samplerTable[sampleIndex(key, tc, purposeLightR(0))];
-            const float lq0 = s.samplerTable[sampleIndex(key, tc, purposeLightS(0))];
-            const float rr = s.samplerTable[sampleIndex(key, tc, kPRussian)];
-            hemi1 = s.shaderTable[sampleIndex(key, tc, kPHemi1)];
-            hemi2 = s.shaderTable[sampleIndex(key, tc, kPHemi2)];
+            const float pick0 = s.tables[sampleIndex(key, tc, purposeLightPick(0))].x;
+            const float lr0 = s.tables[sampleIndex(key, tc, purposeLightR(0))].y;
+            const float lq0 = s.tables[sampleIndex(key, tc, purposeLightS(0))].y;
+            const float rr = s.tables[sampleIndex(key, tc, kPRussian)].y;
+            hemi1 = s.tables[sampleIndex(key, tc, kPHemi1)].x;
+            hemi2 = s.tables[sampleIndex(key, tc, kPHemi2)].x;
             const uint32_t code = fbits(h.w);
             const uint32_t kind = primKind(code);
             // Shader.cpp:122: shade only if hit; Whitted.cpp:14-17 / PathTracer.cpp:25-28: depth cap
@@ -343,9 +401,9 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
                         for (int k = 1; k < a.samplesLight; ++k) {
                             v3 ld, lc;
                             float dist;
-                            if (lightSample(s, g, s.shaderTable[sampleIndex(key, tc, purposeLightPick(k))],
-                                            s.samplerTable[sampleIndex(key, tc, purposeLightR(k))],
-                                            s.samplerTable[sampleIndex(key, tc, purposeLightS(k))], &ld, &dist, &lc))
+                            if (lightSample(s, g, s.tables[sampleIndex(key, tc, purposeLightPick(k))].x,
+                                            s.tables[sampleIndex(key, tc, purposeLightR(k))].y,
+                                            s.tables[sampleIndex(key, tc, purposeLightS(k))].y, &ld, &dist, &lc))
                                 ++nShadow;
                         }
                     }
@@ -358,8 +416,9 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
                 }
             }
         }
-        const int shadowBase = waveAlloc(shadowCount, nShadow);
-        const int childBase = waveAlloc(nextCount, nChild);
+        int childBase, shadowBase;
+        blockAllocPair(pair, nChild, nShadow, &childBase, &shadowBase, allocLds, parity);
+        parity ^= 1;
         if (!active) continue;
         if (terminal) {
             lv.res[i] = leaf;
@@ -374,9 +433,9 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
                 float dist = dist0;
                 if (k == 0) {
                     if (!ok0) continue;
-                } else if (!lightSample(s, g, s.shaderTable[sampleIndex(key, tc, purposeLightPick(k))],
-                                        s.samplerTable[sampleIndex(key, tc, purposeLightR(k))],
-                                        s.samplerTable[sampleIndex(key, tc, purposeLightS(k))], &ld, &dist, &lc)) {
+                } else if (!lightSample(s, g, s.tables[sampleIndex(key, tc, purposeLightPick(k))].x,
+                                        s.tables[sampleIndex(key, tc, purposeLightR(k))].y,
+                                        s.tables[sampleIndex(key, tc, purposeLightS(k))].y, &ld, &dist, &lc)) {
                     continue;
                 }
                 const int j = shadowBase + written;
@@ -415,7 +474,7 @@ __global__ __launch_bounds__(256) void k_shade(DScene s, Level lv, Level nx, int
 // ---------------------------------------------------------------------------------------
 template <int kShader>
 __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
-    const int count = min(counters[kCntRays + level], lv.cap);
+    const int count = min(counters[cntRays(level)], lv.cap);
     for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
          i += static_cast<int>(gridDim.x * blockDim.x)) {
         const int4 va = lv.vtxA[i];
@@ -506,12 +565,12 @@ __global__ __launch_bounds__(256) void k_dump_hits(Level lv, int n, int32_t* kin
 __global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats) {
     unsigned long long rays = 0, shadows = 0;
     for (int l = 1; l <= maxLevel; ++l) {
-        rays += static_cast<unsigned long long>(counters[kCntRays + l]);
-        shadows += static_cast<unsigned long long>(counters[kCntShadows + l]);
+        rays += static_cast<unsigned long long>(counters[cntRays(l)]);
+        shadows += static_cast<unsigned long long>(counters[cntShadows(l)]);
     }
     stats[kStatRays] += rays;
     stats[kStatShadowRays] += shadows;
-    stats[kStatPrimary] += static_cast<unsigned long long>(counters[kCntRays + 1]);
+    stats[kStatPrimary] += static_cast<unsigned long long>(counters[cntRays(1)]);
     if (counters[kCntOverflow] != 0) stats[kStatOverflow] = 1ull;
 }
 
@@ -522,44 +581,68 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
     hipLaunchKernelGGL(k_raygen, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, a, lv, counters);
 }
 
-#define MRT_LAUNCH_ONE(KERNEL, V)                                                                           \
-    case V:                                                                                                  \
+// Persistent grid: the variant's own occupancy x CUs (capped by the grid the spill stacks
+// were sized for).
+template <typename K>
+int persistentGrid(K kernel, int variant, int kind, int maxGrid) {
+    static int occ[2][kTraceVariants] = {};
+    static int cus = 0;
+    if (cus == 0) {
+        hipDeviceProp_t prop;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return maxGrid;
+        cus = prop.multiProcessorCount;
+    }
+    int& o = occ[kind][variant];
+    if (o == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, kBlock, 0) != hipSuccess) o = 0;
+    return o > 0 ? std::min(maxGrid, o * cus) : maxGrid;
+}
+
+#define MRT_LAUNCH_ONE(KERNEL, KIND, V)                                                                     \
+    case V: {                                                                                                \
+        const int g = persistentGrid(KERNEL<false, V>, V, KIND, grid);                                      \
         if (countStats)                                                                                      \
-            hipLaunchKernelGGL((KERNEL<true, V>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+            hipLaunchKernelGGL((KERNEL<true, V>), dim3(g), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
         else                                                                                                 \
-            hipLaunchKernelGGL((KERNEL<false, V>), dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-        break;
-#define MRT_LAUNCH_TRACE(KERNEL)                                                                              \
+            hipLaunchKernelGGL((KERNEL<false, V>), dim3(g), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        break;                                                                                               \
+    }
+#define MRT_LAUNCH_TRACE(KERNEL, KIND)                                                                        \
     switch (s.variant) {                                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, 0)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 1)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 2)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 3)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 4)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 5)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 6)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 7)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 8)                                                                            \
-        MRT_LAUNCH_ONE(KERNEL, 9)                                                                            \
-        default: MRT_LAUNCH_ONE(KERNEL, 10)                                                                  \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 0)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 1)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 2)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 3)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 4)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 5)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 6)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 7)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 8)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 9)                                                                      \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 10)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 11)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 12)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 13)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 14)                                                                     \
+        default: MRT_LAUNCH_ONE(KERNEL, KIND, 15)                                                            \
     }
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
-    MRT_LAUNCH_TRACE(k_trace);
+    MRT_LAUNCH_TRACE(k_trace, 0);
 }
 
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
-    MRT_LAUNCH_TRACE(k_shadow);
+    MRT_LAUNCH_TRACE(k_shadow, 1);
 }
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st) {
     if (shader == kShaderWhitted) {
-        hipLaunchKernelGGL(k_shade<kShaderWhitted>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+        hipLaunchKernelGGL(k_shade<kShaderWhitted>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a);
     } else {
-        hipLaunchKernelGGL(k_shade<kShaderPathTracer>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+        hipLaunchKernelGGL(k_shade<kShaderPathTracer>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a);
     }
 }
 
@@ -591,15 +674,19 @@ void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStre
     hipLaunchKernelGGL(k_tally, dim3(1), dim3(1), 0, st, counters, maxLevel, stats);
 }
 
-int traceOccupancyBlocksPerCU() {
-    int n = 0;
-    // persistent grids: size for the variant with the highest residency; surplus blocks of a
-    // lower-residency variant start as others retire and find the work cursor exhausted
+template <int... V>
+int maxOccupancy(std::integer_sequence<int, V...>) {
     int best = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 1>, kBlock, 0) == hipSuccess) best = std::max(best, n);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 5>, kBlock, 0) == hipSuccess) best = std::max(best, n);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace<false, 10>, kBlock, 0) == hipSuccess) best = std::max(best, n);
+    for (const auto k : {reinterpret_cast<const void*>(k_trace<false, V>)...}) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, 0) == hipSuccess) best = std::max(best, n);
+    }
     return best;
+}
+
+int traceOccupancyBlocksPerCU() {
+    // the spill stacks are sized for the variant with the highest residency
+    return maxOccupancy(std::make_integer_sequence<int, kTraceVariants>{});
 }
 
 }  // namespace mrt

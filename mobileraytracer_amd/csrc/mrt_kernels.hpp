@@ -7,17 +7,22 @@ namespace mrt {
 
 constexpr int kShaderWhitted = 1;     // C_wrapper.cpp:155-160
 constexpr int kShaderPathTracer = 2;  // C_wrapper.cpp:162-172
-constexpr int kMaxLevels = 16;        // max ray depth + 2
+constexpr int kMaxLevels = 16;           // max ray depth + 2
+constexpr int kTraceVariants = 16;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
+constexpr int kDefaultTraceVariant = 8;
 
-// device counters (ints): [kCntRays + L] rays of level L, [kCntShadows + L] shadow rays of
-// level L, work-fetch cursors of the persistent trace kernels, overflow flag
-constexpr int kCntRays = 0;
-constexpr int kCntShadows = kMaxLevels;
-constexpr int kCntFetchTrace = 2 * kMaxLevels;
-constexpr int kCntFetchShadow = 3 * kMaxLevels;
-constexpr int kCntOverflow = 4 * kMaxLevels;
-constexpr int kCntFetchShards = 4 * kMaxLevels + 32;  // 2 kinds x kMaxLevels x 8 cursors x 32 ints
-constexpr int kNumCounters = kCntFetchShards + 2 * kMaxLevels * 8 * 32;
+// Device counters (ints).  Pair l = {rays of level l+1, shadow rays of level l} sits on two
+// adjacent ints so k_shade allocates both with one 64-bit atomic per block.
+constexpr int kCntPairs = 0;                          // 2 * (kMaxLevels + 1) ints
+constexpr int kCntFetchTrace = 64;                    // kMaxLevels single work cursors
+constexpr int kCntFetchShadow = kCntFetchTrace + kMaxLevels;
+constexpr int kCntOverflow = kCntFetchShadow + kMaxLevels;
+constexpr int kMaxFetchShards = 32;                   // sharded work cursors per level
+constexpr int kFetchStride = 32;                      // ints between cursors (a 128-byte line each)
+constexpr int kCntFetchShards = 128;                  // 2 kinds x kMaxLevels x kMaxFetchShards lines
+constexpr int kNumCounters = kCntFetchShards + 2 * kMaxLevels * kMaxFetchShards * kFetchStride;
+MRT_HD constexpr int cntRays(int level) { return kCntPairs + 2 * (level - 1); }
+MRT_HD constexpr int cntShadows(int level) { return kCntPairs + 2 * level + 1; }
 
 // 64-bit statistics accumulated on the device across a frame
 constexpr int kStatRays = 0;        // rays of every level (camera + diffuse + specular + transmission)
@@ -58,7 +63,7 @@ struct PixelMap {
 struct RaygenArgs {
     GCamera cam;
     PixelMap map;
-    const float* samplerTable;
+    const float2* tables;  // .y: the sampler table
     int width, height;
     int slotBase;    // first pixel slot of this chunk
     int nPaths;      // slots in chunk * spp

@@ -294,13 +294,19 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.nMats = static_cast<int32_t>(sc.materials.size());
     d.cull = r->cfg.cull;
     const char* tv = std::getenv("MRT_TRACE_VARIANT");
-    d.variant = tv != nullptr ? std::atoi(tv) : 1;
+    d.variant = tv != nullptr ? std::atoi(tv) : kDefaultTraceVariant;
 
-    std::vector<float> table;
-    fillHaltonTable(&table, kSeedShaderTable);
-    d.shaderTable = r->sceneMem.upload(table, st);
-    fillHaltonTable(&table, kSeedSamplerTable);
-    d.samplerTable = r->sceneMem.upload(table, st);
+    // the two sample tables interleaved: one vertex's draws (consecutive indices, both
+    // tables) share one or two cache lines
+    std::vector<float> shaderT, samplerT, both;
+    fillHaltonTable(&shaderT, kSeedShaderTable);
+    fillHaltonTable(&samplerT, kSeedSamplerTable);
+    both.resize(2 * shaderT.size());
+    for (size_t k = 0; k < shaderT.size(); ++k) {
+        both[2 * k] = shaderT[k];
+        both[2 * k + 1] = samplerT[k];
+    }
+    d.tables = reinterpret_cast<const float2*>(r->sceneMem.upload(both, st));
     MRT_HIP(hipStreamSynchronize(st));
 }
 
@@ -385,7 +391,7 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         RaygenArgs ra{};
         ra.cam = r->cam;
         ra.map = map;
-        ra.samplerTable = r->ds.samplerTable;
+        ra.tables = r->ds.tables;
         ra.width = r->cfg.width;
         ra.height = r->cfg.height;
         ra.slotBase = slot0;
@@ -450,10 +456,12 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
         fs.frameMs = std::chrono::duration<double, std::milli>(t1 - t0).count();
         if (r->profileFlags & 1) {
             for (size_t e = 0; e + 3 < evCount; e += 4) {
-                float a = 0.0F, b = 0.0F;
+                float a = 0.0F, b = 0.0F, c = 0.0F;
                 MRT_HIP(hipEventElapsedTime(&a, r->evPool[e], r->evPool[e + 1]));
+                MRT_HIP(hipEventElapsedTime(&c, r->evPool[e + 1], r->evPool[e + 2]));
                 MRT_HIP(hipEventElapsedTime(&b, r->evPool[e + 2], r->evPool[e + 3]));
                 fs.traceMs += a;
+                fs.shadeMs += c;
                 fs.shadowMs += b;
                 fs.traceLaunches += 1;
                 fs.shadowLaunches += 1;
@@ -609,7 +617,7 @@ int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
 }
 
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
-    if (key == 1 && value >= 0 && value <= 10) {
+    if (key == 1 && value >= 0 && value < mrt::kTraceVariants) {
         r->ds.variant = value;
         return 0;
     }
@@ -618,6 +626,19 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         return 0;
     }
     gLastError = "unknown tuning key/value";
+    return -1;
+}
+
+int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
+    if (key == 1) {
+        *value = r->ds.variant;
+        return 0;
+    }
+    if (key == 2) {
+        *value = r->ds.cull;
+        return 0;
+    }
+    gLastError = "unknown tuning key";
     return -1;
 }
 
@@ -654,7 +675,7 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
                 RaygenArgs ra{};
                 ra.cam = r->cam;
                 ra.map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
-                ra.samplerTable = r->ds.samplerTable;
+                ra.tables = r->ds.tables;
                 ra.width = r->cfg.width;
                 ra.height = r->cfg.height;
                 ra.slotBase = slot0;

@@ -12,6 +12,7 @@
 #pragma once
 
 #include "mrt_device.hpp"
+#include "mrt_kernels.hpp"
 
 namespace mrt {
 
@@ -99,8 +100,6 @@ __device__ __forceinline__ int innerStep4(const GNode4* node, v3 o, v3 inv, floa
     return r0;
 }
 
-constexpr int kFetchShards = 8;   // work cursors per level for the sharded variants
-constexpr int kFetchStride = 32;  // ints between cursors (one 128-byte line each)
 
 template <bool kAny, bool kCount, int kWide, int kRefill, int kShards>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,

@@ -24,19 +24,19 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             n = 5
-            tr = shw = 0.0
+            tr = shw = shd = 0.0
             for _ in range(n):
                 r.render_frame_device(d.data_ptr(), 0, sh)
                 st = r.frame_stats()
-                tr += st["traceMs"]; shw += st["shadowMs"]
+                tr += st["traceMs"]; shw += st["shadowMs"]; shd += st["shadeMs"]
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / n
             rays = st["rays"] + st["shadowRays"]
-            res[v].append((dt * 1e3, tr / n, shw / n, rays / dt / 1e6))
+            res[v].append((dt * 1e3, tr / n, shw / n, rays / dt / 1e6, shd / n))
             imgs[v] = d.cpu().numpy().copy()
     for v in variants:
         a = np.array(res[v])
-        print(f"variant {v}: frame {np.median(a[:,0]):.2f} ms  trace {np.median(a[:,1]):.2f}  shadow {np.median(a[:,2]):.2f}  Mrays/s {np.median(a[:,3]):.0f}", flush=True)
+        print(f"variant {v}: frame {np.median(a[:,0]):.2f} ms  trace {np.median(a[:,1]):.2f}  shadow {np.median(a[:,2]):.2f}  shade {np.median(a[:,4]):.2f}  Mrays/s {np.median(a[:,3]):.0f}", flush=True)
     base = imgs[variants[0]]
     for v in variants[1:]:
         print(f"variant {v} identical image: {np.array_equal(base, imgs[v])}")
