@@ -69,13 +69,14 @@ __device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx,
 // Short traversal stack: the top `depth` (power of two) entries live in LDS (conflict-free
 // layout [slot][thread]), deeper entries spill to a per-thread global area.
 struct TStack {
-    int2* lds;   // &ldsBase[threadIdx.x]; slot s at lds[s * kBlock]
-    int2* glob;  // per-thread overflow area
+    int2* lds;    // &ldsBase[threadIdx.x]; slot s at lds[s * kBlock]
+    int2* gbase;  // overflow areas (kernel-uniform base) ...
+    int gofs;     // ... and this thread's offset into them (32-bit: one VGPR)
     int sp;
     int depth;
     __device__ __forceinline__ void push(int ref, float t) {
         const int slot = sp & (depth - 1);
-        if (sp >= depth) glob[sp - depth] = lds[slot * kBlock];
+        if (sp >= depth) gbase[gofs + sp - depth] = lds[slot * kBlock];
         lds[slot * kBlock] = make_int2(ref, __float_as_int(t));
         ++sp;
     }
@@ -83,7 +84,7 @@ struct TStack {
         --sp;
         const int slot = sp & (depth - 1);
         const int2 v = lds[slot * kBlock];
-        if (sp >= depth) lds[slot * kBlock] = glob[sp - depth];
+        if (sp >= depth) lds[slot * kBlock] = gbase[gofs + sp - depth];
         return v;
     }
 };
@@ -114,9 +115,10 @@ __device__ __forceinline__ bool triTest(float4 a4, float4 ab4, float4 ac4, v3 o,
 }
 
 // lexicographic (t, kind, index) acceptance; `same` = candidate kind equals best kind
-__device__ __forceinline__ bool better(float t, uint32_t code, const Best& b) {
-    return !(t >= b.t) || (t == b.t && primKind(b.code) == primKind(code) && primIndex(code) < primIndex(b.code));
+__device__ __forceinline__ bool betterThan(float t, uint32_t code, float bt, uint32_t bcode) {
+    return !(t >= bt) || (t == bt && primKind(bcode) == primKind(code) && primIndex(code) < primIndex(bcode));
 }
+__device__ __forceinline__ bool better(float t, uint32_t code, const Best& b) { return betterThan(t, code, b.t, b.code); }
 
 template <bool kAny>
 __device__ __forceinline__ bool leafTriangles(const DScene& s, int first, int count, v3 o, v3 d, uint32_t src,

@@ -157,7 +157,7 @@ constexpr TraceCfgRow kTraceCfg[] = {
     {2, 32, kLdsStack, 8, 1},            // 7
     {2, 32, 8, 8, 1},                    // 8
     {2, 48, kLdsStack, 1, 1},            // 9
-    {2, 32, 8, 16, 1},                   // 10
+    {2, 32, 8, 8, 8},                    // 10
     {2, 32, 8, 32, 1},                   // 11
     {2, 32, 4, 8, 1},                    // 12
     {2, 16, 8, 8, 1},                    // 13
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_trace
                                                   int gdepth, unsigned long long* stats) {
     using C = TraceCfg<kVariant>;
     __shared__ int2 ldsStack[C::kStack * kBlock];
-    TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
               C::kStack};
     const int count = min(counters[cntRays(level)], lv.cap);
     int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_shado
                                                    int gdepth, unsigned long long* stats) {
     using C = TraceCfg<kVariant>;
     __shared__ int2 ldsStack[C::kStack * kBlock];
-    TStack st{ldsStack + threadIdx.x, gstack + static_cast<size_t>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
               C::kStack};
     const int count = min(counters[cntShadows(level)], lv.shadowCap);
     int* fetch = C::kShards > 1

@@ -18,6 +18,12 @@ namespace mrt {
 
 constexpr int kRefDone = 0x7FFFFFFF;  // sentinel: no node (never a valid inner index)
 
+// number of set bits of a wave mask below this lane
+__device__ __forceinline__ int lanesBelowIn(uint64_t m) {
+    return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+}
+
 __device__ __forceinline__ int popCulled(TStack& st, float lim, bool cull) {
     while (st.sp > 0) {
         const int2 e = st.pop();
@@ -32,7 +38,7 @@ __device__ __forceinline__ int innerStep2(const GNode* node, v3 o, v3 inv, float
                                           TravCount* cnt, bool count) {
     const float4* np = reinterpret_cast<const float4*>(node);
     const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-    const int4 n3 = reinterpret_cast<const int4*>(np)[3];
+    const int2 n3 = reinterpret_cast<const int2*>(np)[6];  // child refs (the rest is padding)
     if (count) cnt->nodes += 2;
     float tl, tr;
     bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
@@ -106,12 +112,14 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                                 TStack& st, TravCount* cnt) {
     const int lane = static_cast<int>(threadIdx.x & 63u);
-    const uint64_t lanesBelow = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int rayIdx = -1;
     bool exhausted = false;
     v3 o{0, 0, 0}, d{0, 0, 0}, inv{0, 0, 0};
     uint32_t src = 0;
-    Best b{kRayLengthMax, 0.0F, 0.0F, kNoPrim};
+    // closest hit so far: t and primitive code only; u, v are recomputed for the winner at
+    // the end (same inputs -> same bits), which keeps two registers out of the walk
+    float bt = kRayLengthMax;
+    uint32_t bcode = kNoPrim;
     int ref = kRefDone;
     int leaf = 0;  // < 0: a postponed leaf
     int seg = static_cast<int>(blockIdx.x % kShards);  // wave-uniform cursor state
@@ -130,9 +138,18 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     if (!triTest(a4, l[1], l[2], o, d, &t, &u, &v)) continue;
                     if (t < kEpsilon) continue;
                     const uint32_t code = encodePrim(kLight, static_cast<uint32_t>(j));
-                    if (better(t, code, b)) b = Best{t, u, v, code};
+                    if (betterThan(t, code, bt, bcode)) {
+                        bt = t;
+                        bcode = code;
+                    }
                 }
-                out[rayIdx] = make_float4(b.t, b.u, b.v, bitsf(b.code));
+                float u = 0.0F, v = 0.0F, t;  // planes / spheres: 0, 0
+                const uint32_t kind = primKind(bcode);
+                if (kind == kTriangle || kind == kLight) {
+                    const float4* g = kind == kTriangle ? s.triGeom + 3 * primIndex(bcode) : s.lights + 4 * primIndex(bcode);
+                    (void)triTest(g[0], g[1], g[2], o, d, &t, &u, &v);
+                }
+                out[rayIdx] = make_float4(bt, u, v, bitsf(bcode));
             }
             rayIdx = -1;
         }
@@ -152,7 +169,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 int base = 0;
                 if (lane == leader) base = atomicAdd(fetch, n);
                 base = __shfl(base, leader, 64);
-                got = base + __popcll(needMask & lanesBelow);
+                got = base + lanesBelowIn(needMask);
                 if (got >= count) got = -1;
             } else {
                 // per-XCD-group cursors over contiguous ray ranges; an empty range is left
@@ -168,7 +185,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     const int segEnd = static_cast<int>((static_cast<long long>(count) * (seg + 1)) / kShards);
                     const bool mine = ((pending >> lane) & 1ull) != 0;
                     if (mine) {
-                        const int idx = segStart + base + __popcll(pending & lanesBelow);
+                        const int idx = segStart + base + lanesBelowIn(pending);
                         if (idx < segEnd) got = idx;
                     }
                     pending = __ballot(mine && got < 0);
@@ -188,6 +205,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     o = xyz(o4);
                     d = xyz(d4);
                     inv = v3{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
+                    Best b;
                     if (kAny) {
                         src = fbits(o4.w);
                         b = Best{d4.w, 0.0F, 0.0F, kNoPrim};
@@ -203,6 +221,8 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                         traverse<kPlane, false>(s, s.planeNodes, s.planeRoot, o, d, inv, src, &b, st, cnt);
                         traverse<kSphere, false>(s, s.sphereNodes, s.sphereRoot, o, d, inv, src, &b, st, cnt);
                     }
+                    bt = b.t;
+                    bcode = b.code;
                     if (rayIdx >= 0) {
                         float te;
                         const GRoot& r = kWide == 4 ? s.triRoot4 : s.triRoot;
@@ -224,7 +244,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         }
         // ---- inner nodes until every active lane holds a postponed leaf ----
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
-            const float curLim = b.t + b.t * kCullMargin;
+            const float curLim = bt + bt * kCullMargin;
             if (kWide == 4) {
                 ref = innerStep4(s.triNodes4 + ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
             } else {
@@ -250,12 +270,13 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 if (!triTest(g[0], g[1], g[2], o, d, &t, &u, &v)) continue;
                 if (t < kEpsilon) continue;
                 if (kAny) {
-                    if (!(t >= b.t)) {
+                    if (!(t >= bt)) {
                         hit = true;
                         break;
                     }
-                } else if (better(t, code, b)) {
-                    b = Best{t, u, v, code};
+                } else if (betterThan(t, code, bt, bcode)) {
+                    bt = t;
+                    bcode = code;
                 }
             }
             if (kAny && hit) {
@@ -269,7 +290,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             leaf = 0;
             if (ref < 0) {  // the next node is a leaf too: test it now
                 leaf = ref;
-                ref = popCulled(st, b.t + b.t * kCullMargin, s.cull != 0);
+                ref = popCulled(st, bt + bt * kCullMargin, s.cull != 0);
             }
         }
     }
