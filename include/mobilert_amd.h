@@ -86,6 +86,10 @@ typedef struct mrt_frame_stats {
     int64_t traceLaunches;
     int64_t shadowLaunches;
     double shadeMs;         /* profiling: summed duration of the shading launches */
+    uint64_t levelRays[16];       /* rays of depth 1..16 (1 = camera rays) */
+    uint64_t levelShadowRays[16]; /* shadow rays built at depth 1..16 */
+    double levelTraceMs[16];      /* profiling: closest-hit trace time per depth */
+    double levelShadowMs[16];     /* profiling: any-hit trace time per depth */
 } mrt_frame_stats;
 
 const char *mrt_last_error(void);

@@ -124,7 +124,12 @@ class Renderer:
     def frame_stats(self) -> dict:
         s = _native.MrtFrameStats()
         _native.check(self._lib.mrt_get_frame_stats(self._h, ctypes.byref(s)))
-        return {f: getattr(s, f) for f, _ in s._fields_}
+        out = {f: getattr(s, f) for f, _ in s._fields_}
+        out["levelRays"] = list(s.levelRays)
+        out["levelShadowRays"] = list(s.levelShadowRays)
+        out["levelTraceMs"] = list(s.levelTraceMs)
+        out["levelShadowMs"] = list(s.levelShadowMs)
+        return out
 
     def primary_hits(self):
         """(kind, index, t) per pixel, index in the scene's input order (config C2)."""

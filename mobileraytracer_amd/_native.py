@@ -47,6 +47,8 @@ class MrtFrameStats(ctypes.Structure):
         ("traceMs", ctypes.c_double), ("shadowMs", ctypes.c_double), ("frameMs", ctypes.c_double),
         ("traceLaunches", ctypes.c_int64), ("shadowLaunches", ctypes.c_int64),
         ("shadeMs", ctypes.c_double),
+        ("levelRays", ctypes.c_uint64 * 16), ("levelShadowRays", ctypes.c_uint64 * 16),
+        ("levelTraceMs", ctypes.c_double * 16), ("levelShadowMs", ctypes.c_double * 16),
     ]
 
 

@@ -567,6 +567,8 @@ __global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats) 
     for (int l = 1; l <= maxLevel; ++l) {
         rays += static_cast<unsigned long long>(counters[cntRays(l)]);
         shadows += static_cast<unsigned long long>(counters[cntShadows(l)]);
+        stats[kStatLevelRays + l - 1] += static_cast<unsigned long long>(counters[cntRays(l)]);
+        stats[kStatLevelShadows + l - 1] += static_cast<unsigned long long>(counters[cntShadows(l)]);
     }
     stats[kStatRays] += rays;
     stats[kStatShadowRays] += shadows;

@@ -33,7 +33,9 @@ constexpr int kStatTris = 4;        // closest-hit kernel: triangle tests (count
 constexpr int kStatOverflow = 5;
 constexpr int kStatNodesShadow = 6; // any-hit kernel: child node records fetched (counting pass only)
 constexpr int kStatTrisShadow = 7;  // any-hit kernel: triangle tests (counting pass only)
-constexpr int kNumStats = 8;
+constexpr int kStatLevelRays = 8;                     // + level - 1: rays of each level
+constexpr int kStatLevelShadows = 8 + kMaxLevels;     // + level - 1: shadow rays of each level
+constexpr int kNumStats = 8 + 2 * kMaxLevels;
 
 // One level of the wavefront (SoA queues).
 struct Level {

@@ -109,11 +109,15 @@ struct mrt_renderer {
     int chunkSlots = 0;
     int* counters = nullptr;
     unsigned long long* stats = nullptr;
-    int2* gstack = nullptr;
+    int2* gstack = nullptr;        // spill stacks of the closest-hit kernel ...
+    int2* gstackShadow = nullptr;  // ... and of the any-hit kernel (the two can run together)
     int gdepth = 0;
     int traceGrid = 0, workGrid = 0;
     int32_t* dBitmap = nullptr;  // for the host-bitmap entry point
     hipStream_t stream = nullptr;
+    hipStream_t shadowStream = nullptr;  // any-hit launches, overlapped with the next level
+    std::vector<hipEvent_t> syncPool;    // ordering events between the two streams
+    int overlap = 1;                     // tuning key 3: shadow rays on their own stream
 
     // state (Renderer.hpp:30-40)
     std::atomic<bool> stopFlag{false};
@@ -125,7 +129,9 @@ struct mrt_renderer {
 
     ~mrt_renderer() {
         for (hipEvent_t e : evPool) (void)hipEventDestroy(e);
+        for (hipEvent_t e : syncPool) (void)hipEventDestroy(e);
         if (stream != nullptr) (void)hipStreamDestroy(stream);
+        if (shadowStream != nullptr) (void)hipStreamDestroy(shadowStream);
     }
 };
 
@@ -330,8 +336,14 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
         tree[k] = r->queueMem.alloc<uint32_t>(capN);
         hit[k] = r->queueMem.alloc<float4>(capN);
     }
-    float4* sO = r->queueMem.alloc<float4>(capN * spl);
-    float4* sD = r->queueMem.alloc<float4>(capN * spl);
+    // shadow rays: ping-pong too, so k_shade of level L+1 can run while the any-hit kernel
+    // of level L still reads its rays
+    float4* sO[2];
+    float4* sD[2];
+    for (int k = 0; k < 2; ++k) {
+        sO[k] = r->queueMem.alloc<float4>(capN * spl);
+        sD[k] = r->queueMem.alloc<float4>(capN * spl);
+    }
     for (int l = 1; l <= nLevels + 1 && l < kMaxLevels; ++l) {
         Level& lv = r->levels[l];
         const size_t cap = (l == 1) ? n1 : capN;
@@ -342,8 +354,8 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
         lv.rD = rD[l & 1];
         lv.tree = tree[l & 1];
         lv.hit = hit[l & 1];
-        lv.sO = sO;
-        lv.sD = sD;
+        lv.sO = sO[l & 1];
+        lv.sD = sD[l & 1];
         if (real) {
             lv.vtxA = r->queueMem.alloc<int4>(cap);
             lv.vtxB = r->queueMem.alloc<int4>(cap);
@@ -360,8 +372,18 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     r->stats = r->queueMem.alloc<unsigned long long>(kNumStats);
     r->gdepth = std::max(1, r->stackNeed - kLdsStackMin);
     r->gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceGrid) * kBlock * static_cast<size_t>(r->gdepth));
+    r->gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceGrid) * kBlock * static_cast<size_t>(r->gdepth));
     r->dBitmap = r->queueMem.alloc<int32_t>(static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height));
     MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * static_cast<size_t>(r->cfg.width) * r->cfg.height, r->stream));
+}
+
+hipEvent_t syncEvent(mrt_renderer* r, size_t i) {
+    while (r->syncPool.size() <= i) {
+        hipEvent_t e;
+        MRT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        r->syncPool.push_back(e);
+    }
+    return r->syncPool[i];
 }
 
 hipEvent_t poolEvent(mrt_renderer* r, size_t i) {
@@ -400,15 +422,42 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.sppTotal = r->cfg.samplesPixel;
         ra.sampleBase = sampleBase;
         launchRaygen(ra, r->levels[1], r->counters, st);
+        // Any-hit (shadow) rays of level L run on a second stream, overlapped with the
+        // closest-hit trace and shading of level L+1: the persistent kernels' drain phases fill
+        // each other.  Orders: shade(L) -> shadow(L); shadow(L) -> shade(L+2) (the shadow ray
+        // buffers alternate by level); every shadow(L) -> resolve.
+        hipStream_t sb = r->overlap ? r->shadowStream : st;
+        size_t sync = 0;
+        hipEvent_t shadowDone[kMaxLevels] = {};
+        if (sb != st) {
+            const hipEvent_t start = syncEvent(r, sync++);
+            MRT_HIP(hipEventRecord(start, st));
+            MRT_HIP(hipStreamWaitEvent(sb, start, 0));
+        }
         for (int l = 1; l <= nLevels; ++l) {
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
             launchTrace(r->ds, r->levels[l], r->counters, l, r->gstack, r->gdepth, r->stats, counting, r->traceGrid, st);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
+            if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             launchShade(shader, r->ds, r->levels[l], r->levels[l + 1], r->counters, l, sa, r->workGrid, st);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
-            launchShadow(r->ds, r->levels[l], r->counters, l, r->gstack, r->gdepth, r->stats, counting, r->traceGrid, st);
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
+            if (sb != st) {
+                const hipEvent_t shaded = syncEvent(r, sync++);
+                MRT_HIP(hipEventRecord(shaded, st));
+                MRT_HIP(hipStreamWaitEvent(sb, shaded, 0));
+            }
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), sb));
+            if (l < nLevels) {  // the last level (depth > RayDepthMax) shades nothing: no shadow rays
+                launchShadow(r->ds, r->levels[l], r->counters, l, r->gstackShadow, r->gdepth, r->stats, counting,
+                             r->traceGrid, sb);
+            }
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), sb));
+            if (sb != st) {
+                shadowDone[l] = syncEvent(r, sync++);
+                MRT_HIP(hipEventRecord(shadowDone[l], sb));
+            }
         }
+        if (sb != st) MRT_HIP(hipStreamWaitEvent(st, shadowDone[nLevels], 0));
         for (int l = nLevels; l >= 1; --l) {
             launchResolve(shader, r->ds, r->levels[l], r->levels[l + 1], r->counters, l, sa, r->workGrid, st);
         }
@@ -453,16 +502,23 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
         fs.triTests = hs[kStatTris];
         fs.shadowNodeRecords = hs[kStatNodesShadow];
         fs.shadowTriTests = hs[kStatTrisShadow];
+        for (int l = 0; l < kMaxLevels; ++l) {
+            fs.levelRays[l] = hs[kStatLevelRays + l];
+            fs.levelShadowRays[l] = hs[kStatLevelShadows + l];
+        }
         fs.frameMs = std::chrono::duration<double, std::milli>(t1 - t0).count();
         if (r->profileFlags & 1) {
-            for (size_t e = 0; e + 3 < evCount; e += 4) {
+            for (size_t e = 0; e + 4 < evCount; e += 5) {
                 float a = 0.0F, b = 0.0F, c = 0.0F;
                 MRT_HIP(hipEventElapsedTime(&a, r->evPool[e], r->evPool[e + 1]));
                 MRT_HIP(hipEventElapsedTime(&c, r->evPool[e + 1], r->evPool[e + 2]));
-                MRT_HIP(hipEventElapsedTime(&b, r->evPool[e + 2], r->evPool[e + 3]));
+                MRT_HIP(hipEventElapsedTime(&b, r->evPool[e + 3], r->evPool[e + 4]));
                 fs.traceMs += a;
                 fs.shadeMs += c;
                 fs.shadowMs += b;
+                const size_t lvl = (e / 5) % static_cast<size_t>(r->maxDepth + 1);
+                fs.levelTraceMs[lvl] += a;
+                fs.levelShadowMs[lvl] += b;
                 fs.traceLaunches += 1;
                 fs.shadowLaunches += 1;
             }
@@ -497,6 +553,7 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
     if (cfg->device >= 0) MRT_HIP(hipSetDevice(cfg->device));
     MRT_HIP(hipGetDevice(&r->device));
     MRT_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+    MRT_HIP(hipStreamCreateWithFlags(&r->shadowStream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     MRT_HIP(hipGetDeviceProperties(&prop, r->device));
     r->traceGrid = prop.multiProcessorCount * traceOccupancyBlocksPerCU();
@@ -625,6 +682,10 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.cull = value;
         return 0;
     }
+    if (key == 3 && (value == 0 || value == 1)) {
+        r->overlap = value;
+        return 0;
+    }
     gLastError = "unknown tuning key/value";
     return -1;
 }
@@ -636,6 +697,10 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
     }
     if (key == 2) {
         *value = r->ds.cull;
+        return 0;
+    }
+    if (key == 3) {
+        *value = r->overlap;
         return 0;
     }
     gLastError = "unknown tuning key";

@@ -208,7 +208,7 @@ def test_trace_kernel_variants_are_identical():
                 make_cfg(128, 128, shader=2, scene="water", spp=2), make_cfg(64, 64, shader=1)):
         outs = []
         with m.Renderer(cfg) as r:
-            for v in range(11):
+            for v in range(16):  # every kTraceCfg row
                 r.set_tuning(1, v)
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
                 r.render_frame(bm)
@@ -217,6 +217,23 @@ def test_trace_kernel_variants_are_identical():
         for bm, rays, shadows, hits in outs[1:]:
             assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
             assert all(np.array_equal(a, b) for a, b in zip(hits, outs[0][3]))
+
+
+def test_shadow_stream_overlap_is_invariant():
+    """Any-hit launches on their own stream (overlapping the next level) change nothing."""
+    import mobileraytracer_amd as m
+    for cfg in (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+                make_cfg(64, 64, shader=1)):
+        outs = []
+        with m.Renderer(cfg) as r:
+            for ov in (0, 1, 0, 1):
+                r.set_tuning(3, ov)
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"]))
+        for bm, rays, shadows in outs[1:]:
+            assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
 
 
 def _render_shards(cfg_kw, world):

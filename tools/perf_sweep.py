@@ -13,13 +13,16 @@ def main():
     r = m.Renderer(cfg)
     d = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
-    variants = [int(v) for v in os.environ.get("VARIANTS", "4,7,8,9,10,1").split(",")]
+    # "V" or "V:O": trace variant V, shadow-stream overlap O (default 1)
+    variants = os.environ.get("VARIANTS", "8,8:0,13,14").split(",")
     imgs = {}
     res = {v: [] for v in variants}
     r.set_profiling(timing=True)
     for rnd in range(3):
         for v in variants:
-            r.set_tuning(1, v)
+            vv, _, ov = v.partition(":")
+            r.set_tuning(1, int(vv))
+            r.set_tuning(3, int(ov or 1))
             r.render_frame_device(d.data_ptr(), 0, sh)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
