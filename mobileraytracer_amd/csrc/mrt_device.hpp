@@ -37,7 +37,8 @@ struct DScene {
     int32_t nLights;
     int32_t nMats;
     int32_t cull;              // 1: near-first + conservative t-culling, 0: reference visit set
-    int32_t variant;           // trace kernels: 0 per-wave batches, 1 while-while + refill, 2 the same on BVH4
+    int32_t variant;           // trace kernel organisation (mrt_kernels.hip kTraceCfg)
+    int32_t triTop;            // triNodes[0, triTop) are the breadth-first top of the tree
 };
 
 __device__ __forceinline__ float4 ld4(const float4* p) { return *p; }
@@ -69,22 +70,23 @@ __device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx,
 // Short traversal stack: the top `depth` (power of two) entries live in LDS (conflict-free
 // layout [slot][thread]), deeper entries spill to a per-thread global area.
 struct TStack {
-    int2* lds;    // &ldsBase[threadIdx.x]; slot s at lds[s * kBlock]
+    int2* lds;    // &ldsBase[threadIdx.x]; slot s at lds[s * stride]
     int2* gbase;  // overflow areas (kernel-uniform base) ...
     int gofs;     // ... and this thread's offset into them (32-bit: one VGPR)
     int sp;
     int depth;
+    int stride;   // threads per workgroup
     __device__ __forceinline__ void push(int ref, float t) {
         const int slot = sp & (depth - 1);
-        if (sp >= depth) gbase[gofs + sp - depth] = lds[slot * kBlock];
-        lds[slot * kBlock] = make_int2(ref, __float_as_int(t));
+        if (sp >= depth) gbase[gofs + sp - depth] = lds[slot * stride];
+        lds[slot * stride] = make_int2(ref, __float_as_int(t));
         ++sp;
     }
     __device__ __forceinline__ int2 pop() {
         --sp;
         const int slot = sp & (depth - 1);
-        const int2 v = lds[slot * kBlock];
-        if (sp >= depth) lds[slot * kBlock] = gbase[gofs + sp - depth];
+        const int2 v = lds[slot * stride];
+        if (sp >= depth) lds[slot * stride] = gbase[gofs + sp - depth];
         return v;
     }
 };

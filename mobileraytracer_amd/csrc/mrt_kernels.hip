@@ -145,24 +145,26 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
 //   0 per-wave 64-ray batches, if-if walk (BVH2); the rest are while-while walks.
 struct TraceCfgRow {
     int wide, refill, stack, shards, minWaves;  // shards <= kMaxFetchShards
+    int top;                                    // BVH2 top nodes staged in LDS (<= kTopNodesMax)
+    int threads = kBlock;                       // per workgroup (the LDS top is shared by them)
 };
 constexpr TraceCfgRow kTraceCfg[] = {
-    {2, 1, kLdsStack, 1, 1},             // 0
-    {2, 1, kLdsStack, 1, 1},             // 1
-    {4, 1, kLdsStack, 1, 1},             // 2
-    {2, 16, kLdsStack, 1, 1},            // 3
-    {2, 32, kLdsStack, 1, 1},            // 4
-    {2, 16, 8, 1, 1},                    // 5
-    {4, 16, kLdsStack, 1, 1},            // 6
-    {2, 32, kLdsStack, 8, 1},            // 7
-    {2, 32, 8, 8, 1},                    // 8
-    {2, 48, kLdsStack, 1, 1},            // 9
-    {2, 32, 8, 8, 8},                    // 10
-    {2, 32, 8, 32, 1},                   // 11
-    {2, 32, 4, 8, 1},                    // 12
-    {2, 16, 8, 8, 1},                    // 13
-    {2, 16, 8, 32, 1},                   // 14
-    {2, 8, 8, 32, 1},                    // 15
+    {2, 1, kLdsStack, 1, 1, 0},   // 0  per-wave batches, if-if
+    {2, 1, kLdsStack, 1, 1, 0},   // 1  while-while, per-lane refill
+    {4, 1, kLdsStack, 1, 1, 0},   // 2  as 1, 4-wide BVH
+    {2, 16, kLdsStack, 1, 1, 0},  // 3
+    {2, 32, kLdsStack, 1, 1, 0},  // 4
+    {2, 16, 8, 1, 1, 0},          // 5
+    {4, 16, kLdsStack, 1, 1, 0},  // 6
+    {2, 32, kLdsStack, 8, 1, 0},  // 7
+    {2, 32, 8, 8, 1, 0},          // 8  default
+    {2, 48, kLdsStack, 1, 1, 0},  // 9
+    {2, 32, 8, 8, 8, 0},          // 10 as 8, compiled for 8 waves per SIMD
+    {2, 32, 8, 32, 1, 0},         // 11 as 8, 32 cursors
+    {2, 32, 8, 8, 1, 64},         // 12 as 8, top 64 nodes in LDS
+    {2, 32, 8, 8, 1, 128},        // 13 as 8, top 128 nodes in LDS
+    {2, 32, 8, 8, 1, 128, 512},   // 14 as 13, 512-thread workgroups
+    {2, 32, 8, 8, 1, 256, 512},   // 15 as 14, top 256 nodes
 };
 constexpr int kNumTraceVariants = sizeof(kTraceCfg) / sizeof(kTraceCfg[0]);
 static_assert(kNumTraceVariants == kTraceVariants, "mrt_kernels.hpp kTraceVariants");
@@ -174,21 +176,39 @@ struct TraceCfg {
     static constexpr int kStack = kTraceCfg[kVariant].stack;
     static constexpr int kShards = kTraceCfg[kVariant].shards;
     static constexpr int kMinWaves = kTraceCfg[kVariant].minWaves;
+    static constexpr int kTop = kTraceCfg[kVariant].wide == 2 ? kTraceCfg[kVariant].top : 0;
+    static constexpr int kThreads = kTraceCfg[kVariant].threads;
+    static_assert(kTop <= kTopNodesMax, "top nodes");
+    static_assert(kThreads % 64 == 0 && kThreads <= 1024, "workgroup size");
 };
 
+// Copies the BVH2 top into LDS (all threads; ends with a barrier).
+template <int kTop, int kThreads>
+__device__ __forceinline__ void stageTop(const DScene& s, GNode* ldsTop) {
+    if (kTop == 0) return;
+    const int n = min(kTop, s.triTop) * static_cast<int>(sizeof(GNode) / sizeof(float4));
+    const float4* src = reinterpret_cast<const float4*>(s.triNodes);
+    float4* dst = reinterpret_cast<float4*>(ldsTop);
+    for (int i = static_cast<int>(threadIdx.x); i < n; i += kThreads) dst[i] = src[i];
+    __syncthreads();
+}
+
 template <bool kCount, int kVariant>
-__global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_trace(DScene s, Level lv, int* counters, int level, int2* gstack,
+__global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::kMinWaves) void k_trace(DScene s, Level lv, int* counters, int level, int2* gstack,
                                                   int gdepth, unsigned long long* stats) {
     using C = TraceCfg<kVariant>;
-    __shared__ int2 ldsStack[C::kStack * kBlock];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
-              C::kStack};
+    __shared__ int2 ldsStack[C::kStack * C::kThreads];
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * C::kThreads + threadIdx.x) * gdepth, 0,
+              C::kStack, C::kThreads};
     const int count = min(counters[cntRays(level)], lv.cap);
     int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride
                                 : counters + kCntFetchTrace + level;
     TravCount cnt{0u, 0u};
+    __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
+    stageTop<C::kTop, C::kThreads>(s, ldsTop);
     if (kVariant > 0)
-        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt);
+        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop>(s, lv.rO, lv.rD, lv.hit, count, fetch,
+                                                                                   st, &cnt, ldsTop);
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -216,19 +236,22 @@ __global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_trace
 }
 
 template <bool kCount, int kVariant>
-__global__ __launch_bounds__(kBlock, TraceCfg<kVariant>::kMinWaves) void k_shadow(DScene s, Level lv, int* counters, int level, int2* gstack,
+__global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::kMinWaves) void k_shadow(DScene s, Level lv, int* counters, int level, int2* gstack,
                                                    int gdepth, unsigned long long* stats) {
     using C = TraceCfg<kVariant>;
-    __shared__ int2 ldsStack[C::kStack * kBlock];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kBlock + threadIdx.x) * gdepth, 0,
-              C::kStack};
+    __shared__ int2 ldsStack[C::kStack * C::kThreads];
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * C::kThreads + threadIdx.x) * gdepth, 0,
+              C::kStack, C::kThreads};
     const int count = min(counters[cntShadows(level)], lv.shadowCap);
     int* fetch = C::kShards > 1
                      ? counters + kCntFetchShards + (kMaxLevels + level) * kMaxFetchShards * kFetchStride
                      : counters + kCntFetchShadow + level;
     TravCount cnt{0u, 0u};
+    __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
+    stageTop<C::kTop, C::kThreads>(s, ldsTop);
     if (kVariant > 0)
-        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt);
+        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop>(s, lv.sO, lv.sD, lv.sC, count, fetch,
+                                                                                  st, &cnt, ldsTop);
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -583,30 +606,32 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
     hipLaunchKernelGGL(k_raygen, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, a, lv, counters);
 }
 
-// Persistent grid: the variant's own occupancy x CUs (capped by the grid the spill stacks
-// were sized for).
+// Persistent grid: the variant's own occupancy x CUs workgroups, capped by the thread count
+// the spill stacks were sized for.
 template <typename K>
-int persistentGrid(K kernel, int variant, int kind, int maxGrid) {
+int persistentGrid(K kernel, int variant, int kind, int threads, int maxThreads) {
     static int occ[2][kTraceVariants] = {};
     static int cus = 0;
+    const int cap = std::max(1, maxThreads / threads);
     if (cus == 0) {
         hipDeviceProp_t prop;
         int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return maxGrid;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return cap;
         cus = prop.multiProcessorCount;
     }
     int& o = occ[kind][variant];
-    if (o == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, kBlock, 0) != hipSuccess) o = 0;
-    return o > 0 ? std::min(maxGrid, o * cus) : maxGrid;
+    if (o == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, threads, 0) != hipSuccess) o = 0;
+    return o > 0 ? std::min(cap, o * cus) : cap;
 }
 
 #define MRT_LAUNCH_ONE(KERNEL, KIND, V)                                                                     \
     case V: {                                                                                                \
-        const int g = persistentGrid(KERNEL<false, V>, V, KIND, grid);                                      \
+        constexpr int kT = TraceCfg<V>::kThreads;                                                            \
+        const int g = persistentGrid(KERNEL<false, V>, V, KIND, kT, maxThreads);                            \
         if (countStats)                                                                                      \
-            hipLaunchKernelGGL((KERNEL<true, V>), dim3(g), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+            hipLaunchKernelGGL((KERNEL<true, V>), dim3(g), dim3(kT), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
         else                                                                                                 \
-            hipLaunchKernelGGL((KERNEL<false, V>), dim3(g), dim3(kBlock), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+            hipLaunchKernelGGL((KERNEL<false, V>), dim3(g), dim3(kT), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
         break;                                                                                               \
     }
 #define MRT_LAUNCH_TRACE(KERNEL, KIND)                                                                        \
@@ -630,12 +655,12 @@ int persistentGrid(K kernel, int variant, int kind, int maxGrid) {
     }
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
-                 unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
+                 unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
     MRT_LAUNCH_TRACE(k_trace, 0);
 }
 
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
-                  unsigned long long* stats, bool countStats, int grid, hipStream_t st) {
+                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
     MRT_LAUNCH_TRACE(k_shadow, 1);
 }
 
@@ -677,18 +702,21 @@ void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStre
 }
 
 template <int... V>
-int maxOccupancy(std::integer_sequence<int, V...>) {
-    int best = 1;
-    for (const auto k : {reinterpret_cast<const void*>(k_trace<false, V>)...}) {
+int maxResidentThreads(std::integer_sequence<int, V...>) {
+    int best = kBlock;
+    const void* kernels[] = {reinterpret_cast<const void*>(k_trace<false, V>)...};
+    const int threads[] = {TraceCfg<V>::kThreads...};
+    for (size_t i = 0; i < sizeof...(V); ++i) {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, 0) == hipSuccess) best = std::max(best, n);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernels[i], threads[i], 0) == hipSuccess)
+            best = std::max(best, n * threads[i]);
     }
     return best;
 }
 
-int traceOccupancyBlocksPerCU() {
-    // the spill stacks are sized for the variant with the highest residency
-    return maxOccupancy(std::make_integer_sequence<int, kTraceVariants>{});
+int traceResidentThreadsPerCU() {
+    // the spill stacks are sized for the variant with the most resident threads
+    return maxResidentThreads(std::make_integer_sequence<int, kTraceVariants>{});
 }
 
 }  // namespace mrt

@@ -9,7 +9,8 @@ constexpr int kShaderWhitted = 1;     // C_wrapper.cpp:155-160
 constexpr int kShaderPathTracer = 2;  // C_wrapper.cpp:162-172
 constexpr int kMaxLevels = 16;           // max ray depth + 2
 constexpr int kTraceVariants = 16;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
-constexpr int kDefaultTraceVariant = 8;
+constexpr int kDefaultTraceVariant = 13;
+constexpr int kTopNodesMax = 256;        // BVH2 nodes numbered breadth-first (LDS-staged by some variants)
 
 // Device counters (ints).  Pair l = {rays of level l+1, shadow rays of level l} sits on two
 // adjacent ints so k_shade allocates both with one 64-bit atomic per block.
@@ -92,9 +93,9 @@ struct AccumArgs {
 
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
-                 unsigned long long* stats, bool countStats, int grid, hipStream_t st);
+                 unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
-                  unsigned long long* stats, bool countStats, int grid, hipStream_t st);
+                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st);
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
@@ -103,6 +104,6 @@ void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, in
 void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st);
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);
 void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st);
-int traceOccupancyBlocksPerCU();
+int traceResidentThreadsPerCU();  // max over trace variants of resident threads per CU
 
 }  // namespace mrt

@@ -112,7 +112,7 @@ struct mrt_renderer {
     int2* gstack = nullptr;        // spill stacks of the closest-hit kernel ...
     int2* gstackShadow = nullptr;  // ... and of the any-hit kernel (the two can run together)
     int gdepth = 0;
-    int traceGrid = 0, workGrid = 0;
+    int traceThreads = 0, workGrid = 0;  // traceThreads: resident trace threads, whole device
     int32_t* dBitmap = nullptr;  // for the host-bitmap entry point
     hipStream_t stream = nullptr;
     hipStream_t shadowStream = nullptr;  // any-hit launches, overlapped with the next level
@@ -219,7 +219,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
 
     std::vector<GNode> g;
     DScene& d = r->ds;
-    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot);
+    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop);
     d.triNodes = r->sceneMem.upload(g, st);
     {
         std::vector<GNode4> g4;
@@ -371,8 +371,8 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     r->counters = r->queueMem.alloc<int>(kNumCounters);
     r->stats = r->queueMem.alloc<unsigned long long>(kNumStats);
     r->gdepth = std::max(1, r->stackNeed - kLdsStackMin);
-    r->gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceGrid) * kBlock * static_cast<size_t>(r->gdepth));
-    r->gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceGrid) * kBlock * static_cast<size_t>(r->gdepth));
+    r->gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
+    r->gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
     r->dBitmap = r->queueMem.alloc<int32_t>(static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height));
     MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * static_cast<size_t>(r->cfg.width) * r->cfg.height, r->stream));
 }
@@ -436,7 +436,7 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         }
         for (int l = 1; l <= nLevels; ++l) {
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
-            launchTrace(r->ds, r->levels[l], r->counters, l, r->gstack, r->gdepth, r->stats, counting, r->traceGrid, st);
+            launchTrace(r->ds, r->levels[l], r->counters, l, r->gstack, r->gdepth, r->stats, counting, r->traceThreads, st);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             launchShade(shader, r->ds, r->levels[l], r->levels[l + 1], r->counters, l, sa, r->workGrid, st);
@@ -449,7 +449,7 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), sb));
             if (l < nLevels) {  // the last level (depth > RayDepthMax) shades nothing: no shadow rays
                 launchShadow(r->ds, r->levels[l], r->counters, l, r->gstackShadow, r->gdepth, r->stats, counting,
-                             r->traceGrid, sb);
+                             r->traceThreads, sb);
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), sb));
             if (sb != st) {
@@ -556,7 +556,7 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
     MRT_HIP(hipStreamCreateWithFlags(&r->shadowStream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     MRT_HIP(hipGetDeviceProperties(&prop, r->device));
-    r->traceGrid = prop.multiProcessorCount * traceOccupancyBlocksPerCU();
+    r->traceThreads = prop.multiProcessorCount * traceResidentThreadsPerCU();
     r->workGrid = prop.multiProcessorCount * 8;
 
     // scene (C_wrapper.cpp:68-141)
@@ -749,7 +749,7 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
                 ra.sppTotal = r->cfg.samplesPixel;
                 ra.sampleBase = 0;
                 launchRaygen(ra, r->levels[1], r->counters, st);
-                launchTrace(r->ds, r->levels[1], r->counters, 1, r->gstack, r->gdepth, r->stats, false, r->traceGrid, st);
+                launchTrace(r->ds, r->levels[1], r->counters, 1, r->gstack, r->gdepth, r->stats, false, r->traceThreads, st);
                 launchDumpHits(r->levels[1], n, dk, di, dt, st);
                 MRT_HIP(hipMemcpyAsync(hk.data(), dk, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
                 MRT_HIP(hipMemcpyAsync(hi.data(), di, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));

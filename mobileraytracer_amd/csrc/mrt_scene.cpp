@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <random>
 #include <sstream>
@@ -690,13 +691,15 @@ template std::vector<HBVHNode> buildBVH<HTriangle>(std::vector<HTriangle>*, std:
 template std::vector<HBVHNode> buildBVH<HPlane>(std::vector<HPlane>*, std::vector<int32_t>*);
 template std::vector<HBVHNode> buildBVH<HSphere>(std::vector<HSphere>*, std::vector<int32_t>*);
 
-static int32_t encodeRef(const std::vector<HBVHNode>& nodes, int32_t j) {
-    const HBVHNode& c = nodes[static_cast<size_t>(j)];
-    return c.numPrimitives > 0 ? leafRef(c.indexOffset, c.numPrimitives) : j;
-}
-
-void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root) {
-    out->assign(nodes.size(), GNode{});
+// Device BVH2: one GNode per inner node, holding both children's boxes.  Inner nodes are
+// renumbered: the first topCount in breadth-first order (the levels every ray crosses; the
+// trace kernels can stage them in LDS), the rest in depth-first pre-order, left child first,
+// so a parent and its left child usually share a 128-byte line.  Node numbering does not
+// affect results (boxes, child order and leaves are the reference's).
+void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
+                 int topCount, int* topPlaced) {
+    out->clear();
+    if (topPlaced != nullptr) *topPlaced = 0;
     const HBVHNode& r = nodes[0];
     root->bmin[0] = r.box.mn.x;
     root->bmin[1] = r.box.mn.y;
@@ -705,11 +708,48 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
     root->bmax[1] = r.box.mx.y;
     root->bmax[2] = r.box.mx.z;
     root->count = static_cast<int32_t>(numPrims);
-    root->ref = numPrims == 0 ? 0 : encodeRef(nodes, 0);
-    for (size_t i = 0; i < nodes.size(); ++i) {
-        const HBVHNode& nd = nodes[i];
-        if (numPrims == 0 || nd.numPrimitives > 0) continue;
-        const int32_t l = nd.indexOffset;
+    if (numPrims == 0) {
+        root->ref = 0;
+        return;
+    }
+    if (r.numPrimitives > 0) {
+        root->ref = leafRef(r.indexOffset, r.numPrimitives);
+        return;
+    }
+    auto inner = [&](int32_t i) { return nodes[static_cast<size_t>(i)].numPrimitives == 0; };
+    std::vector<int32_t> newIdx(nodes.size(), -1);
+    std::vector<int32_t> order;
+    std::deque<int32_t> bfs{0};
+    while (!bfs.empty() && static_cast<int>(order.size()) < topCount) {
+        const int32_t i = bfs.front();
+        bfs.pop_front();
+        newIdx[static_cast<size_t>(i)] = static_cast<int32_t>(order.size());
+        order.push_back(i);
+        const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
+        if (inner(l)) bfs.push_back(l);
+        if (inner(l + 1)) bfs.push_back(l + 1);
+    }
+    if (topPlaced != nullptr) *topPlaced = static_cast<int>(order.size());
+    std::vector<int32_t> dfs{0};
+    while (!dfs.empty()) {
+        const int32_t i = dfs.back();
+        dfs.pop_back();
+        if (newIdx[static_cast<size_t>(i)] < 0) {
+            newIdx[static_cast<size_t>(i)] = static_cast<int32_t>(order.size());
+            order.push_back(i);
+        }
+        const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
+        if (inner(l + 1)) dfs.push_back(l + 1);
+        if (inner(l)) dfs.push_back(l);
+    }
+    auto ref = [&](int32_t j) {
+        const HBVHNode& c = nodes[static_cast<size_t>(j)];
+        return c.numPrimitives > 0 ? leafRef(c.indexOffset, c.numPrimitives) : newIdx[static_cast<size_t>(j)];
+    };
+    root->ref = 0;
+    out->resize(order.size());
+    for (size_t k = 0; k < order.size(); ++k) {
+        const int32_t l = nodes[static_cast<size_t>(order[k])].indexOffset;
         const HBVHNode& L = nodes[static_cast<size_t>(l)];
         const HBVHNode& R = nodes[static_cast<size_t>(l + 1)];
         GNode g{};
@@ -725,9 +765,9 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
         g.rmaxx = R.box.mx.x;
         g.rmaxy = R.box.mx.y;
         g.rmaxz = R.box.mx.z;
-        g.refL = encodeRef(nodes, l);
-        g.refR = encodeRef(nodes, l + 1);
-        (*out)[i] = g;
+        g.refL = ref(l);
+        g.refR = ref(l + 1);
+        (*out)[k] = g;
     }
 }
 

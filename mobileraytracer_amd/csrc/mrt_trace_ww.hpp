@@ -34,11 +34,25 @@ __device__ __forceinline__ int popCulled(TStack& st, float lim, bool cull) {
 
 // kAny = false: closest hit -> writes lv.hit;  kAny = true: shadow any-hit -> writes lv.sC.w
 // One BVH2 inner-node visit: returns the next node (near child, or a popped entry).
-__device__ __forceinline__ int innerStep2(const GNode* node, v3 o, v3 inv, float lim, bool cull, TStack& st,
-                                          TravCount* cnt, bool count) {
-    const float4* np = reinterpret_cast<const float4*>(node);
-    const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-    const int2 n3 = reinterpret_cast<const int2*>(np)[6];  // child refs (the rest is padding)
+// top: nodes [0, top) are read from the LDS copy ldsTop (the breadth-first top of the tree)
+template <int kTop>
+__device__ __forceinline__ int innerStep2(const GNode* nodes, const GNode* ldsTop, int top, int ref, v3 o, v3 inv,
+                                          float lim, bool cull, TStack& st, TravCount* cnt, bool count) {
+    float4 n0, n1, n2;
+    int2 n3;
+    if (kTop > 0 && ref < top) {
+        const float4* np = reinterpret_cast<const float4*>(ldsTop + ref);
+        n0 = np[0];
+        n1 = np[1];
+        n2 = np[2];
+        n3 = reinterpret_cast<const int2*>(np)[6];
+    } else {
+        const float4* np = reinterpret_cast<const float4*>(nodes + ref);
+        n0 = np[0];
+        n1 = np[1];
+        n2 = np[2];
+        n3 = reinterpret_cast<const int2*>(np)[6];  // child refs (the rest is padding)
+    }
     if (count) cnt->nodes += 2;
     float tl, tr;
     bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
@@ -107,10 +121,11 @@ __device__ __forceinline__ int innerStep4(const GNode4* node, v3 o, v3 inv, floa
 }
 
 
-template <bool kAny, bool kCount, int kWide, int kRefill, int kShards>
+template <bool kAny, bool kCount, int kWide, int kRefill, int kShards, int kTop>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                TStack& st, TravCount* cnt) {
+                                                TStack& st, TravCount* cnt, const GNode* ldsTop) {
+    const int top = kTop > 0 ? min(kTop, s.triTop) : 0;
     const int lane = static_cast<int>(threadIdx.x & 63u);
     int rayIdx = -1;
     bool exhausted = false;
@@ -248,7 +263,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             if (kWide == 4) {
                 ref = innerStep4(s.triNodes4 + ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
             } else {
-                ref = innerStep2(s.triNodes + ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
+                ref = innerStep2<kTop>(s.triNodes, ldsTop, top, ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
             }
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
