@@ -67,6 +67,27 @@ __device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx,
     return tMax >= e;
 }
 
+// The same predicate for rays whose 1/d components are all finite.  Then no operand can be
+// NaN ((box - o) * finite is finite or +-inf), so IEEE min/max (v_min3 / v_max3) return the
+// ternaries' values, up to the sign of a zero, which no comparison made with tEntry can see.
+__device__ __forceinline__ bool slabFinite(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, v3 o,
+                                           v3 inv, float* tEntry) {
+    const float t1x = (mnx - o.x) * inv.x;
+    const float t2x = (mxx - o.x) * inv.x;
+    const float t1y = (mny - o.y) * inv.y;
+    const float t2y = (mxy - o.y) * inv.y;
+    const float t1z = (mnz - o.z) * inv.z;
+    const float t2z = (mxz - o.z) * inv.z;
+    const float e = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fmaxf(fminf(t1z, t2z), 0.0F));
+    const float tMax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+    *tEntry = e;
+    return tMax >= e;
+}
+
+__device__ __forceinline__ bool finiteInv(v3 inv) {
+    return __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+}
+
 // Short traversal stack: the top `depth` (power of two) entries live in LDS (conflict-free
 // layout [slot][thread]), deeper entries spill to a per-thread global area.
 struct TStack {

@@ -147,6 +147,7 @@ struct TraceCfgRow {
     int wide, refill, stack, shards, minWaves;  // shards <= kMaxFetchShards
     int top;                                    // BVH2 top nodes staged in LDS (<= kTopNodesMax)
     int threads = kBlock;                       // per workgroup (the LDS top is shared by them)
+    int fastSlab = 0;                           // IEEE min/max slab test when every 1/d is finite
 };
 constexpr TraceCfgRow kTraceCfg[] = {
     {2, 1, kLdsStack, 1, 1, 0},   // 0  per-wave batches, if-if
@@ -163,8 +164,8 @@ constexpr TraceCfgRow kTraceCfg[] = {
     {2, 32, 8, 32, 1, 0},         // 11 as 8, 32 cursors
     {2, 32, 8, 8, 1, 64},         // 12 as 8, top 64 nodes in LDS
     {2, 32, 8, 8, 1, 128},        // 13 as 8, top 128 nodes in LDS
-    {2, 32, 8, 8, 1, 128, 512},   // 14 as 13, 512-thread workgroups
-    {2, 32, 8, 8, 1, 256, 512},   // 15 as 14, top 256 nodes
+    {2, 32, 8, 8, 1, 128, 256, 1},  // 14 as 13, IEEE min/max slab test for finite 1/d
+    {2, 32, 8, 8, 1, 256, 512},     // 15 as 13, top 256 nodes, 512-thread workgroups
 };
 constexpr int kNumTraceVariants = sizeof(kTraceCfg) / sizeof(kTraceCfg[0]);
 static_assert(kNumTraceVariants == kTraceVariants, "mrt_kernels.hpp kTraceVariants");
@@ -178,6 +179,7 @@ struct TraceCfg {
     static constexpr int kMinWaves = kTraceCfg[kVariant].minWaves;
     static constexpr int kTop = kTraceCfg[kVariant].wide == 2 ? kTraceCfg[kVariant].top : 0;
     static constexpr int kThreads = kTraceCfg[kVariant].threads;
+    static constexpr bool kFastSlab = kTraceCfg[kVariant].fastSlab != 0;
     static_assert(kTop <= kTopNodesMax, "top nodes");
     static_assert(kThreads % 64 == 0 && kThreads <= 1024, "workgroup size");
 };
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
     __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
     stageTop<C::kTop, C::kThreads>(s, ldsTop);
     if (kVariant > 0)
-        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop>(s, lv.rO, lv.rD, lv.hit, count, fetch,
+        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab>(s, lv.rO, lv.rD, lv.hit, count, fetch,
                                                                                    st, &cnt, ldsTop);
     while (kVariant == 0) {
         int base = 0;
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
     __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
     stageTop<C::kTop, C::kThreads>(s, ldsTop);
     if (kVariant > 0)
-        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop>(s, lv.sO, lv.sD, lv.sC, count, fetch,
+        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab>(s, lv.sO, lv.sD, lv.sC, count, fetch,
                                                                                   st, &cnt, ldsTop);
     while (kVariant == 0) {
         int base = 0;

@@ -9,7 +9,7 @@ constexpr int kShaderWhitted = 1;     // C_wrapper.cpp:155-160
 constexpr int kShaderPathTracer = 2;  // C_wrapper.cpp:162-172
 constexpr int kMaxLevels = 16;           // max ray depth + 2
 constexpr int kTraceVariants = 16;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
-constexpr int kDefaultTraceVariant = 13;
+constexpr int kDefaultTraceVariant = 14;
 constexpr int kTopNodesMax = 256;        // BVH2 nodes numbered breadth-first (LDS-staged by some variants)
 
 // Device counters (ints).  Pair l = {rays of level l+1, shadow rays of level l} sits on two

@@ -35,9 +35,10 @@ __device__ __forceinline__ int popCulled(TStack& st, float lim, bool cull) {
 // kAny = false: closest hit -> writes lv.hit;  kAny = true: shadow any-hit -> writes lv.sC.w
 // One BVH2 inner-node visit: returns the next node (near child, or a popped entry).
 // top: nodes [0, top) are read from the LDS copy ldsTop (the breadth-first top of the tree)
+// finite: wave-uniform, every active lane's 1/d is finite (slabFinite applies)
 template <int kTop>
 __device__ __forceinline__ int innerStep2(const GNode* nodes, const GNode* ldsTop, int top, int ref, v3 o, v3 inv,
-                                          float lim, bool cull, TStack& st, TravCount* cnt, bool count) {
+                                          float lim, bool cull, TStack& st, TravCount* cnt, bool count, bool finite) {
     float4 n0, n1, n2;
     int2 n3;
     if (kTop > 0 && ref < top) {
@@ -55,8 +56,14 @@ __device__ __forceinline__ int innerStep2(const GNode* nodes, const GNode* ldsTo
     }
     if (count) cnt->nodes += 2;
     float tl, tr;
-    bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
-    bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+    bool hl, hr;
+    if (finite) {
+        hl = slabFinite(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
+        hr = slabFinite(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+    } else {
+        hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
+        hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+    }
     if (cull) {
         hl = hl && !(tl > lim);
         hr = hr && !(tr > lim);
@@ -121,7 +128,7 @@ __device__ __forceinline__ int innerStep4(const GNode4* node, v3 o, v3 inv, floa
 }
 
 
-template <bool kAny, bool kCount, int kWide, int kRefill, int kShards, int kTop>
+template <bool kAny, bool kCount, int kWide, int kRefill, int kShards, int kTop, bool kFastSlab>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                                 TStack& st, TravCount* cnt, const GNode* ldsTop) {
@@ -263,7 +270,9 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             if (kWide == 4) {
                 ref = innerStep4(s.triNodes4 + ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
             } else {
-                ref = innerStep2<kTop>(s.triNodes, ldsTop, top, ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
+                const bool finite = kFastSlab && __ballot(!finiteInv(inv)) == 0;
+                ref = innerStep2<kTop>(s.triNodes, ldsTop, top, ref, o, inv, curLim, s.cull != 0, st, cnt, kCount,
+                                       finite);
             }
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
