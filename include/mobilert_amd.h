@@ -57,6 +57,9 @@ typedef struct mrt_config {
     int32_t device;       /* HIP device ordinal, -1 = current device */
     int32_t cull;         /* 1 (default): near-first traversal + conservative t-culling */
     int32_t maxPathsPerPass; /* <= 0 -> automatic chunk size */
+    int32_t progressive;  /* 1: one pass per sample; bitmap and mrt_get_sample() updated after
+                           * each (Renderer.cpp:53-88).  0: all samples in flight at once.
+                           * The final bitmap is the same. */
 } mrt_config;
 
 typedef struct mrt_scene_info {

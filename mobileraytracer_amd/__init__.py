@@ -51,12 +51,13 @@ class Config:
     device: int = -1
     cull: int = 1
     maxPathsPerPass: int = 0
+    progressive: int = 0
 
     def to_c(self):
         c = _native.MrtConfig()
         for f in ("width", "height", "threads", "shader", "sceneIndex", "samplesPixel", "samplesLight",
                   "repeats", "accelerator", "maxDepth", "rankIndex", "rankCount", "device", "cull",
-                  "maxPathsPerPass"):
+                  "maxPathsPerPass", "progressive"):
             setattr(c, f, int(getattr(self, f)))
         c.printStdOut = int(bool(self.printStdOut))
         self._keep = [s.encode() for s in (self.objFilePath, self.mtlFilePath, self.camFilePath)]
@@ -113,7 +114,8 @@ class Renderer:
         _native.check(self._lib.mrt_set_profiling(self._h, int(timing) | (2 * int(counting))))
 
     def set_tuning(self, key: int, value: int) -> None:
-        """A/B knobs (identical results): 1 = trace kernel variant, 2 = t-culling."""
+        """A/B knobs (identical results): 1 = trace kernel variant (0..15), 2 = t-culling,
+        3 = shadow rays on their own stream."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 
     def get_tuning(self, key: int) -> int:
@@ -165,7 +167,8 @@ def ray_trace(config: Config, async_: bool = False):
         if config.bitmap is None:
             config.bitmap = np.zeros(config.width * config.height, np.int32)
         t0 = time.perf_counter()
-        r = Renderer(config)
+        # progressive, as C_wrapper's render loop: the caller may read config.bitmap meanwhile
+        r = Renderer(dataclasses.replace(config, progressive=1))
         t1 = time.perf_counter()
         _active.append(r)
         try:

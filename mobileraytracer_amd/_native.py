@@ -30,6 +30,7 @@ class MrtConfig(ctypes.Structure):
         ("objFilePath", ctypes.c_char_p), ("mtlFilePath", ctypes.c_char_p), ("camFilePath", ctypes.c_char_p),
         ("maxDepth", ctypes.c_int32), ("rankIndex", ctypes.c_int32), ("rankCount", ctypes.c_int32),
         ("device", ctypes.c_int32), ("cull", ctypes.c_int32), ("maxPathsPerPass", ctypes.c_int32),
+        ("progressive", ctypes.c_int32),
     ]
 
 

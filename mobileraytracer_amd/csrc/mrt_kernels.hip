@@ -557,7 +557,8 @@ __global__ __launch_bounds__(256) void k_accumulate(AccumArgs a, const float4* r
     int x, y;
     slotToXY(a.map, slot, &x, &y);
     const int idx = y * a.width + x;
-    int32_t c = (a.sampleBase > 0 && bitmap != nullptr) ? bitmap[idx] : 0;
+    int32_t c = 0;  // the running average (progressive passes: sampleBase > 0)
+    if (a.sampleBase > 0) c = bitmap != nullptr ? bitmap[idx] : (packed != nullptr ? packed[slot] : 0);
     for (int s = 0; s < a.spp; ++s) {
         const float4 r = res[q * a.spp + s];
         c = incrementalAvg(v3{r.x, r.y, r.z}, c, a.sampleBase + s + 1);

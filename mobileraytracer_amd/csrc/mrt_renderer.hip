@@ -104,7 +104,7 @@ struct mrt_renderer {
     int nSlots = 0, maxSlots = 0;
 
     // queues
-    DeviceMem sceneMem, queueMem;
+    DeviceMem sceneMem, queueMem, frameMem;  // frameMem: bitmaps, kept when the queues are resized
     mrt::Level levels[mrt::kMaxLevels]{};
     int chunkSlots = 0;
     int* counters = nullptr;
@@ -114,6 +114,8 @@ struct mrt_renderer {
     int gdepth = 0;
     int traceThreads = 0, workGrid = 0;  // traceThreads: resident trace threads, whole device
     int32_t* dBitmap = nullptr;  // for the host-bitmap entry point
+    int32_t* dBackup = nullptr;  // progressive mode: the running average before the current pass
+    size_t backupN = 0;
     hipStream_t stream = nullptr;
     hipStream_t shadowStream = nullptr;  // any-hit launches, overlapped with the next level
     std::vector<hipEvent_t> syncPool;    // ordering events between the two streams
@@ -373,8 +375,6 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     r->gdepth = std::max(1, r->stackNeed - kLdsStackMin);
     r->gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
     r->gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
-    r->dBitmap = r->queueMem.alloc<int32_t>(static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height));
-    MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * static_cast<size_t>(r->cfg.width) * r->cfg.height, r->stream));
 }
 
 hipEvent_t syncEvent(mrt_renderer* r, size_t i) {
@@ -474,61 +474,129 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     return true;
 }
 
-// Renderer::renderFrame (Renderer.cpp:53-88): samples 0..spp-1, progressive average.
-void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st) {
+// One pass (samples [sampleBase, sampleBase + spp)) with its statistics added to *fs.
+// Returns false when the wavefront queues overflowed (the pass's output is then invalid).
+bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp,
+             mrt_frame_stats* fs) {
+    using namespace mrt;
+    MRT_HIP(hipMemsetAsync(r->stats, 0, sizeof(unsigned long long) * kNumStats, st));
+    size_t evCount = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    renderPass(r, dBitmap, dPacked, st, sampleBase, spp, &evCount);
+    unsigned long long hs[kNumStats];
+    MRT_HIP(hipMemcpyAsync(hs, r->stats, sizeof(hs), hipMemcpyDeviceToHost, st));
+    MRT_HIP(hipStreamSynchronize(st));
+    const auto t1 = std::chrono::steady_clock::now();
+    if (hs[kStatOverflow] != 0) return false;
+    fs->rays += hs[kStatRays];
+    fs->shadowRays += hs[kStatShadowRays];
+    fs->primaryRays += hs[kStatPrimary];
+    fs->nodeRecords += hs[kStatNodes];
+    fs->triTests += hs[kStatTris];
+    fs->shadowNodeRecords += hs[kStatNodesShadow];
+    fs->shadowTriTests += hs[kStatTrisShadow];
+    for (int l = 0; l < kMaxLevels; ++l) {
+        fs->levelRays[l] += hs[kStatLevelRays + l];
+        fs->levelShadowRays[l] += hs[kStatLevelShadows + l];
+    }
+    fs->frameMs += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (r->profileFlags & 1) {
+        for (size_t e = 0; e + 4 < evCount; e += 5) {
+            float ta = 0.0F, tb = 0.0F, tc = 0.0F;
+            MRT_HIP(hipEventElapsedTime(&ta, r->evPool[e], r->evPool[e + 1]));
+            MRT_HIP(hipEventElapsedTime(&tc, r->evPool[e + 1], r->evPool[e + 2]));
+            MRT_HIP(hipEventElapsedTime(&tb, r->evPool[e + 3], r->evPool[e + 4]));
+            fs->traceMs += ta;
+            fs->shadeMs += tc;
+            fs->shadowMs += tb;
+            const size_t lvl = (e / 5) % static_cast<size_t>(r->maxDepth + 1);
+            fs->levelTraceMs[lvl] += ta;
+            fs->levelShadowMs[lvl] += tb;
+            fs->traceLaunches += 1;
+            fs->shadowLaunches += 1;
+        }
+    }
+    return true;
+}
+
+// Renderer::renderFrame (Renderer.cpp:53-88): samples 0..spp-1 averaged with incrementalAvg.
+// Default: every sample of the frame in flight at once (one wavefront pass per chunk).
+// cfg.progressive: one pass per sample, the bitmap (and hostBitmap, if given) updated and
+// getSample() advanced after each, stopRender() honoured between samples - the reference's
+// progressive contract for the Qt / Android front ends.  Both give the same final bitmap.
+void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st,
+                       int32_t* hostBitmap = nullptr) {
     using namespace mrt;
     r->sample.store(0);
     if (r->stopFlag.load()) return;  // stopRender zeroes samplesPixel_ (Renderer.cpp:97)
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        MRT_HIP(hipMemsetAsync(r->stats, 0, sizeof(unsigned long long) * kNumStats, st));
-        size_t evCount = 0;
-        const auto t0 = std::chrono::steady_clock::now();
-        renderPass(r, dBitmap, dPacked, st, 0, std::max(1, r->cfg.samplesPixel), &evCount);
-        unsigned long long hs[kNumStats];
-        MRT_HIP(hipMemcpyAsync(hs, r->stats, sizeof(hs), hipMemcpyDeviceToHost, st));
-        MRT_HIP(hipStreamSynchronize(st));
-        const auto t1 = std::chrono::steady_clock::now();
-        if (hs[kStatOverflow] != 0) {
-            // wavefront queues overflowed: halve the chunk (more passes, same results) and redo
-            const int slots = std::max(1, r->chunkSlots / 2);
-            allocQueues(r, slots, 2);
-            continue;
+    const int spp = std::max(1, r->cfg.samplesPixel);
+    const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
+    mrt_frame_stats fs{};
+    if (r->cfg.progressive == 0) {
+        bool done = false;
+        for (int attempt = 0; attempt < 4 && !done; ++attempt) {
+            fs = mrt_frame_stats{};
+            done = runPass(r, dBitmap, dPacked, st, 0, spp, &fs);
+            if (!done) allocQueues(r, std::max(1, r->chunkSlots / 2), 2);  // same results, more passes
         }
-        mrt_frame_stats fs{};
-        fs.rays = hs[kStatRays];
-        fs.shadowRays = hs[kStatShadowRays];
-        fs.primaryRays = hs[kStatPrimary];
-        fs.nodeRecords = hs[kStatNodes];
-        fs.triTests = hs[kStatTris];
-        fs.shadowNodeRecords = hs[kStatNodesShadow];
-        fs.shadowTriTests = hs[kStatTrisShadow];
-        for (int l = 0; l < kMaxLevels; ++l) {
-            fs.levelRays[l] = hs[kStatLevelRays + l];
-            fs.levelShadowRays[l] = hs[kStatLevelShadows + l];
+        if (!done) throw std::runtime_error("wavefront queue overflow persists after shrinking the chunk");
+        if (hostBitmap != nullptr && dBitmap != nullptr) {
+            MRT_HIP(hipMemcpyAsync(hostBitmap, dBitmap, npx * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            MRT_HIP(hipStreamSynchronize(st));
         }
-        fs.frameMs = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        if (r->profileFlags & 1) {
-            for (size_t e = 0; e + 4 < evCount; e += 5) {
-                float a = 0.0F, b = 0.0F, c = 0.0F;
-                MRT_HIP(hipEventElapsedTime(&a, r->evPool[e], r->evPool[e + 1]));
-                MRT_HIP(hipEventElapsedTime(&c, r->evPool[e + 1], r->evPool[e + 2]));
-                MRT_HIP(hipEventElapsedTime(&b, r->evPool[e + 3], r->evPool[e + 4]));
-                fs.traceMs += a;
-                fs.shadeMs += c;
-                fs.shadowMs += b;
-                const size_t lvl = (e / 5) % static_cast<size_t>(r->maxDepth + 1);
-                fs.levelTraceMs[lvl] += a;
-                fs.levelShadowMs[lvl] += b;
-                fs.traceLaunches += 1;
-                fs.shadowLaunches += 1;
-            }
-        }
-        r->last = fs;
-        r->totalRays.fetch_add(fs.rays + fs.shadowRays);
         if (!r->stopFlag.load()) r->sample.store(r->cfg.samplesPixel);
-        return;
+    } else {
+        // the running average is read by the next pass: keep a copy to redo an overflowed pass
+        int32_t* acc = dBitmap != nullptr ? dBitmap : dPacked;
+        const size_t accN = dBitmap != nullptr ? npx : static_cast<size_t>(r->nSlots);
+        if (r->dBackup == nullptr || r->backupN < accN) {
+            r->dBackup = r->frameMem.alloc<int32_t>(accN);
+            r->backupN = accN;
+        }
+        for (int smp = 0; smp < spp && !r->stopFlag.load(); ++smp) {
+            bool done = false;
+            for (int attempt = 0; attempt < 4 && !done; ++attempt) {
+                if (acc != nullptr) MRT_HIP(hipMemcpyAsync(r->dBackup, acc, accN * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+                mrt_frame_stats pass{};
+                done = runPass(r, dBitmap, dPacked, st, smp, 1, &pass);
+                if (done) {
+                    const mrt_frame_stats prev = fs;
+                    fs = pass;
+                    fs.rays += prev.rays;
+                    fs.shadowRays += prev.shadowRays;
+                    fs.primaryRays += prev.primaryRays;
+                    fs.nodeRecords += prev.nodeRecords;
+                    fs.triTests += prev.triTests;
+                    fs.shadowNodeRecords += prev.shadowNodeRecords;
+                    fs.shadowTriTests += prev.shadowTriTests;
+                    fs.traceMs += prev.traceMs;
+                    fs.shadowMs += prev.shadowMs;
+                    fs.shadeMs += prev.shadeMs;
+                    fs.frameMs += prev.frameMs;
+                    fs.traceLaunches += prev.traceLaunches;
+                    fs.shadowLaunches += prev.shadowLaunches;
+                    for (int l = 0; l < kMaxLevels; ++l) {
+                        fs.levelRays[l] += prev.levelRays[l];
+                        fs.levelShadowRays[l] += prev.levelShadowRays[l];
+                        fs.levelTraceMs[l] += prev.levelTraceMs[l];
+                        fs.levelShadowMs[l] += prev.levelShadowMs[l];
+                    }
+                } else {
+                    if (acc != nullptr)
+                        MRT_HIP(hipMemcpyAsync(acc, r->dBackup, accN * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+                    allocQueues(r, std::max(1, r->chunkSlots / 2), 2);
+                }
+            }
+            if (!done) throw std::runtime_error("wavefront queue overflow persists after shrinking the chunk");
+            if (hostBitmap != nullptr && dBitmap != nullptr) {
+                MRT_HIP(hipMemcpyAsync(hostBitmap, dBitmap, npx * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+                MRT_HIP(hipStreamSynchronize(st));
+            }
+            r->sample.store(smp + 1);  // Renderer.cpp:82-86
+        }
     }
-    throw std::runtime_error("wavefront queue overflow persists after shrinking the chunk");
+    r->last = fs;
+    r->totalRays.fetch_add(fs.rays + fs.shadowRays);
 }
 
 mrt_renderer* createRenderer(const mrt_config* cfg) {
@@ -578,6 +646,9 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
     size_t maxPaths = cfg->maxPathsPerPass > 0 ? static_cast<size_t>(cfg->maxPathsPerPass) : (size_t{1} << 24);
     size_t slots = std::max<size_t>(1, std::min<size_t>(static_cast<size_t>(r->nSlots), maxPaths / spp));
     allocQueues(r.get(), static_cast<int>(slots), 2);
+    const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
+    r->dBitmap = r->frameMem.alloc<int32_t>(npx);
+    MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * npx, r->stream));
     MRT_HIP(hipStreamSynchronize(r->stream));
     return r.release();
 }
@@ -617,9 +688,7 @@ int mrt_render_frame(mrt_renderer* r, int32_t* bitmap) {
     return guarded([&] {
         const size_t n = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
         MRT_HIP(hipMemcpyAsync(r->dBitmap, bitmap, n * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
-        renderFrameDevice(r, r->dBitmap, nullptr, r->stream);
-        MRT_HIP(hipMemcpyAsync(bitmap, r->dBitmap, n * sizeof(int32_t), hipMemcpyDeviceToHost, r->stream));
-        MRT_HIP(hipStreamSynchronize(r->stream));
+        renderFrameDevice(r, r->dBitmap, nullptr, r->stream, bitmap);
     });
 }
 
@@ -664,7 +733,7 @@ int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
     info->triangleBvhDepth = r->triDepth;
     info->pixelSlots = r->nSlots;
     info->pixelSlotsMax = r->maxSlots;
-    info->deviceBytes = static_cast<int64_t>(r->sceneMem.total + r->queueMem.total);
+    info->deviceBytes = static_cast<int64_t>(r->sceneMem.total + r->queueMem.total + r->frameMem.total);
     return 0;
 }
 
@@ -809,6 +878,7 @@ void workThread(::MobileRT::Config& config) {
         c.device = dev != nullptr ? std::atoi(dev) : -1;
         c.rankCount = 1;
         c.cull = 1;
+        c.progressive = 1;  // the UI polls config.bitmap while the frame renders
         const auto tc0 = std::chrono::steady_clock::now();
         mrt_renderer* r = createRenderer(&c);
         const auto tc1 = std::chrono::steady_clock::now();
@@ -821,9 +891,7 @@ void workThread(::MobileRT::Config& config) {
         do {  // C_wrapper.cpp:227-233
             const size_t n = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
             MRT_HIP(hipMemcpyAsync(r->dBitmap, config.bitmap.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
-            renderFrameDevice(r, r->dBitmap, nullptr, r->stream);
-            MRT_HIP(hipMemcpyAsync(config.bitmap.data(), r->dBitmap, n * sizeof(int32_t), hipMemcpyDeviceToHost, r->stream));
-            MRT_HIP(hipStreamSynchronize(r->stream));
+            renderFrameDevice(r, r->dBitmap, nullptr, r->stream, config.bitmap.data());
             repeats--;
         } while (repeats > 0);
         const auto t1 = std::chrono::steady_clock::now();

@@ -308,6 +308,42 @@ def test_stop_render_and_counters():
         del before
 
 
+def test_progressive_mode_same_bitmap_live_samples_and_stop():
+    """cfg.progressive: one pass per sample (Renderer.cpp:53-88). Same final bitmap and ray
+    count as all samples in flight; getSample() advances while the frame renders; stopRender()
+    ends the frame between samples."""
+    import dataclasses, threading, time
+    import mobileraytracer_amd as m
+    for cfg in (make_cfg(64, 64, shader=2, spp=4), make_cfg(160, 96, shader=2, scene="conference", spp=3, max_depth=5),
+                make_cfg(64, 64, shader=1, spp=3)):
+        a, ra, _ = gpu_render(cfg)
+        b, rb, _ = gpu_render(dataclasses.replace(cfg, progressive=1))
+        assert np.array_equal(a, b) and ra == rb
+    cfg = make_cfg(1920, 1080, shader=2, scene="conference", spp=8, max_depth=5, progressive=1)
+    with m.Renderer(cfg) as r:
+        bm = np.zeros(cfg.width * cfg.height, np.int32)
+        th = threading.Thread(target=r.render_frame, args=(bm,))
+        th.start()
+        seen = set()
+        while th.is_alive():
+            seen.add(r.get_sample())
+            time.sleep(0.0005)
+        th.join()
+        assert r.get_sample() == 8 and len(seen - {0, 8}) >= 2
+    cfg = make_cfg(1920, 1080, shader=2, scene="conference", spp=256, max_depth=5, progressive=1)
+    with m.Renderer(cfg) as r:
+        bm = np.zeros(cfg.width * cfg.height, np.int32)
+        th = threading.Thread(target=r.render_frame, args=(bm,))
+        th.start()
+        t0 = time.time()
+        while r.get_sample() < 2 and time.time() - t0 < 60:
+            time.sleep(0.0005)
+        r.stop_render()
+        th.join()
+        assert 2 <= r.get_sample() < 256
+        assert len(np.unique(bm)) > 1  # the samples done so far reached the host bitmap
+
+
 def test_ray_trace_entry_point(capsys):
     import mobileraytracer_amd as m
     cfg = make_cfg(96, 96, shader=1, scene="conference", printStdOut=True)
