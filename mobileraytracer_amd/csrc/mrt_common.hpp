@@ -189,8 +189,8 @@ struct GRoot {
 // Camera parameters (Camera.cpp:14-19, Perspective.cpp:8-14)
 struct GCamera {
     v3 position, direction, right, up;
-    float hFov, vFov;  // radians
-    int32_t kind;      // 0 perspective
+    float hFov, vFov;  // perspective: radians; orthographic: half sizes (Orthographic.cpp:11-12)
+    int32_t kind;      // 0 perspective, 1 orthographic
     int32_t pad;
 };
 

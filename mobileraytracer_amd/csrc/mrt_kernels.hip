@@ -125,15 +125,25 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
     }
     const float devU = (r1 - 0.5F) * 2.0F * pixW;
     const float devV = (r2 - 0.5F) * 2.0F * pixH;
-    // Perspective.cpp:16-28
     const GCamera& c = a.cam;
-    const float rf = fastArcTan(c.hFov * (u - 0.5F)) + devU;
-    const v3 right = c.right * rf;
-    const float uf = fastArcTan(c.vFov * (0.5F - v)) + devV;
-    const v3 up = c.up * uf;
-    const v3 dest = ((c.position + c.direction) + right) + up;
-    const v3 dir = normalize(dest - c.position);
-    lv.rO[p] = make_float4(c.position.x, c.position.y, c.position.z, bitsf(key));
+    v3 origin, dir;
+    if (c.kind == 1) {  // Orthographic.cpp:15-24 (hFov / vFov hold the half sizes)
+        const float rf = (u - 0.5F) * c.hFov;
+        const v3 right = c.right * rf + c.right * devU;
+        const float uf = (0.5F - v) * c.vFov;
+        const v3 up = c.up * uf + c.up * devV;
+        origin = (c.position + right) + up;
+        dir = c.direction;
+    } else {  // Perspective.cpp:16-28
+        const float rf = fastArcTan(c.hFov * (u - 0.5F)) + devU;
+        const v3 right = c.right * rf;
+        const float uf = fastArcTan(c.vFov * (0.5F - v)) + devV;
+        const v3 up = c.up * uf;
+        const v3 dest = ((c.position + c.direction) + right) + up;
+        origin = c.position;
+        dir = normalize(dest - c.position);
+    }
+    lv.rO[p] = make_float4(origin.x, origin.y, origin.z, bitsf(key));
     lv.rD[p] = make_float4(dir.x, dir.y, dir.z, bitsf(kNoPrim));
     lv.tree[p] = 1u;
 }
@@ -496,6 +506,74 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
     }
 }
 
+// Single-level shaders: the camera ray's shade() spawns no rays, so the result is final here.
+//   DepthMap (DepthMap.cpp:13-18), DiffuseMaterial (DiffuseMaterial.cpp:12-28),
+//   NoShadows (NoShadows.cpp:13-44: direct light without shadow rays + ambient).
+template <int kShader>
+__global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int* counters, int level, ShadeArgs a) {
+    const int count = min(counters[cntRays(level)], lv.cap);
+    for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
+         i += static_cast<int>(gridDim.x * blockDim.x)) {
+        const float4 o4 = lv.rO[i];
+        const float4 d4 = lv.rD[i];
+        const float4 h = lv.hit[i];
+        const uint32_t code = fbits(h.w);
+        const uint32_t kind = primKind(code);
+        v3 rgb{0.0F, 0.0F, 0.0F};
+        float hitLight = 0.0F;
+        if (kind != kMiss) {  // Shader.cpp:122: shade only on a hit
+            v3 Le, Kd{0, 0, 0}, Ks{0, 0, 0}, Kt{0, 0, 0};
+            if (kind == kLight) {
+                Le = xyz(s.lights[4 * primIndex(code) + 3]);  // Light::radiance_
+            } else {
+                const float4* m = s.mats + 4 * hitMaterial(s, code);
+                Le = xyz(m[0]);
+                Kd = xyz(m[1]);
+                Ks = xyz(m[2]);
+                Kt = xyz(m[3]);
+            }
+            if (kShader == kShaderDepthMap) {
+                const v3 mp{a.maxPoint[0], a.maxPoint[1], a.maxPoint[2]};
+                const float maxDist = length(mp - xyz(o4)) * 1.1F;
+                const float depth = stdmax((maxDist - h.x) / maxDist, 0.0F);
+                rgb = v3{depth, depth, depth};
+            } else if (kShader == kShaderDiffuse) {
+                if (hasPositive(Kd)) {
+                    rgb = Kd;
+                } else if (hasPositive(Ks)) {
+                    rgb = Ks;
+                } else if (hasPositive(Kt)) {
+                    rgb = Kt;
+                } else if (hasPositive(Le)) {
+                    rgb = Le;
+                }
+            } else if (hasPositive(Le)) {  // NoShadows
+                rgb = Le;
+                hitLight = 1.0F;
+            } else {
+                if (hasPositive(Kd) && s.nLights > 0) {
+                    const uint32_t key = fbits(o4.w);
+                    const uint32_t tc = lv.tree[i];
+                    const HitGeom g = hitGeometry(s, xyz(o4), xyz(d4), h);
+                    for (int k = 0; k < a.samplesLight; ++k) {
+                        v3 ld, lc;
+                        float dist;
+                        if (lightSample(s, g, s.tables[sampleIndex(key, tc, purposeLightPick(k))].x,
+                                        s.tables[sampleIndex(key, tc, purposeLightR(k))].y,
+                                        s.tables[sampleIndex(key, tc, purposeLightS(k))].y, &ld, &dist, &lc))
+                            rgb = rgb + lc;  // Le * cosNl
+                    }
+                    rgb = rgb * Kd;
+                    rgb = rgb / static_cast<float>(a.samplesLight);
+                }
+                rgb = rgb + Kd * 0.1F;
+            }
+        }
+        lv.res[i] = make_float4(rgb.x, rgb.y, rgb.z, hitLight);
+        lv.vtxA[i] = make_int4(-1, 0, 0, 0);
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 template <int kShader>
 __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
@@ -669,20 +747,32 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st) {
-    if (shader == kShaderWhitted) {
-        hipLaunchKernelGGL(k_shade<kShaderWhitted>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a);
-    } else {
-        hipLaunchKernelGGL(k_shade<kShaderPathTracer>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a);
+    switch (shader) {
+        case kShaderWhitted:
+            hipLaunchKernelGGL(k_shade<kShaderWhitted>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a);
+            break;
+        case kShaderPathTracer:
+            hipLaunchKernelGGL(k_shade<kShaderPathTracer>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a);
+            break;
+        case kShaderDepthMap:
+            hipLaunchKernelGGL(k_shade_simple<kShaderDepthMap>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, a);
+            break;
+        case kShaderDiffuse:
+            hipLaunchKernelGGL(k_shade_simple<kShaderDiffuse>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, a);
+            break;
+        default:
+            hipLaunchKernelGGL(k_shade_simple<kShaderNoShadows>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, a);
+            break;
     }
 }
 
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                    const ShadeArgs& a, int grid, hipStream_t st) {
-    if (shader == kShaderWhitted) {
-        hipLaunchKernelGGL(k_resolve<kShaderWhitted>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
-    } else {
+    if (shader == kShaderPathTracer) {
         hipLaunchKernelGGL(k_resolve<kShaderPathTracer>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
-    }
+    } else if (shader == kShaderWhitted) {
+        hipLaunchKernelGGL(k_resolve<kShaderWhitted>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+    }  // single-level shaders: k_shade_simple wrote the final results
 }
 
 void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, int32_t* packed, hipStream_t st) {

@@ -7,6 +7,9 @@ namespace mrt {
 
 constexpr int kShaderWhitted = 1;     // C_wrapper.cpp:155-160
 constexpr int kShaderPathTracer = 2;  // C_wrapper.cpp:162-172
+constexpr int kShaderDepthMap = 3;    // C_wrapper.cpp:175-179
+constexpr int kShaderDiffuse = 4;     // C_wrapper.cpp:181-186 (DiffuseMaterial)
+constexpr int kShaderNoShadows = 5;   // C_wrapper.cpp:188-193 (the switch's default: 0, 5, ...)
 constexpr int kMaxLevels = 16;           // max ray depth + 2
 constexpr int kTraceVariants = 16;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
 constexpr int kDefaultTraceVariant = 14;
@@ -79,6 +82,7 @@ struct RaygenArgs {
 struct ShadeArgs {
     int maxDepth;      // RayDepthMax
     int samplesLight;  // Config::samplesLight
+    float maxPoint[3]; // DepthMap::maxPoint_ (C_wrapper.cpp:79-131 maxDist)
 };
 
 struct AccumArgs {

@@ -86,6 +86,9 @@ struct mrt_renderer {
     mrt_config cfg{};
     std::string objPath, mtlPath, camPath;
     int maxDepth = mrt::kRayDepthMaxDefault;
+    int shader = mrt::kShaderWhitted;  // kShader* after the reference's switch (C_wrapper.cpp:153-193)
+    int nLevels = 1;                   // wavefront levels: maxDepth + 1, or 1 for single-level shaders
+    mrt::v3 maxPoint{1.0F, 1.0F, 1.0F};  // DepthMap
     int rankIndex = 0, rankCount = 1;
     int device = 0;
 
@@ -326,7 +329,7 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     r->chunkSlots = chunkSlots;
     const size_t n1 = static_cast<size_t>(chunkSlots) * static_cast<size_t>(spp);
     const size_t capN = n1 * static_cast<size_t>(growth);
-    const int nLevels = r->maxDepth + 1;
+    const int nLevels = r->nLevels;
     // ping-pong ray / hit buffers (dead after k_shade of their level)
     float4* rO[2];
     float4* rD[2];
@@ -400,11 +403,11 @@ hipEvent_t poolEvent(mrt_renderer* r, size_t i) {
 bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp,
                 size_t* evCount) {
     using namespace mrt;
-    const int shader = r->cfg.shader == kShaderWhitted ? kShaderWhitted : kShaderPathTracer;
+    const int shader = r->shader;
     const bool timing = (r->profileFlags & 1) != 0;
     const bool counting = (r->profileFlags & 2) != 0;
-    ShadeArgs sa{r->maxDepth, std::max(1, r->cfg.samplesLight)};
-    const int nLevels = r->maxDepth + 1;
+    ShadeArgs sa{r->maxDepth, std::max(1, r->cfg.samplesLight), {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z}};
+    const int nLevels = r->nLevels;
     const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
     for (int slot0 = 0; slot0 < r->nSlots; slot0 += r->chunkSlots) {
         if (r->stopFlag.load()) return true;
@@ -509,7 +512,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
             fs->traceMs += ta;
             fs->shadeMs += tc;
             fs->shadowMs += tb;
-            const size_t lvl = (e / 5) % static_cast<size_t>(r->maxDepth + 1);
+            const size_t lvl = (e / 5) % static_cast<size_t>(r->nLevels);
             fs->levelTraceMs[lvl] += ta;
             fs->levelShadowMs[lvl] += tb;
             fs->traceLaunches += 1;
@@ -614,8 +617,9 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
     r->rankCount = cfg->rankCount > 0 ? cfg->rankCount : 1;
     r->rankIndex = cfg->rankIndex;
     if (r->rankIndex < 0 || r->rankIndex >= r->rankCount) throw std::runtime_error("rankIndex out of range");
-    if (cfg->shader != kShaderWhitted && cfg->shader != kShaderPathTracer)
-        throw std::runtime_error("the GPU path implements shader 1 (Whitted) and 2 (PathTracer)");
+    // C_wrapper.cpp:153-193: 1 Whitted, 2 PathTracer, 3 DepthMap, 4 DiffuseMaterial, else NoShadows
+    r->shader = (cfg->shader >= kShaderWhitted && cfg->shader <= kShaderDiffuse) ? cfg->shader : kShaderNoShadows;
+    r->nLevels = (r->shader == kShaderWhitted || r->shader == kShaderPathTracer) ? r->maxDepth + 1 : 1;
     if (cfg->width < 16 || cfg->height < 16) throw std::runtime_error("width/height must be >= 16");
     if (cfg->samplesPixel < 1 || cfg->samplesLight < 1) throw std::runtime_error("samplesPixel/samplesLight must be >= 1");
     if (cfg->device >= 0) MRT_HIP(hipSetDevice(cfg->device));
@@ -630,11 +634,11 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
     // scene (C_wrapper.cpp:68-141)
     const float ratio = static_cast<float>(cfg->width) / static_cast<float>(cfg->height);
     HScene sc;
-    if (cfg->sceneIndex == 0) {
-        sc = cornellBoxScene();
-        r->cam = cornellBoxCamera(ratio);
-    } else if (cfg->sceneIndex >= 1 && cfg->sceneIndex <= 3) {
-        throw std::runtime_error("built-in scenes 1-3 are outside this path's scope (SURVEY.md section 2)");
+    r->maxPoint = v3{1.0F, 1.0F, 1.0F};
+    if (cfg->sceneIndex >= 0 && cfg->sceneIndex <= 3) {
+        sc = builtinScene(cfg->sceneIndex);
+        r->cam = builtinCamera(cfg->sceneIndex, ratio);
+        r->maxPoint = builtinMaxPoint(cfg->sceneIndex);
     } else {
         std::string err;
         if (!loadObjScene(r->objPath, r->mtlPath, &sc, &err)) throw std::runtime_error(err);

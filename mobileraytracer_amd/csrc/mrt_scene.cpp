@@ -110,45 +110,131 @@ bool aabbIntersect(const HAABB& b, v3 o, v3 d) {
 }
 
 // ---- built-in Cornell box (Scenes.cpp:19-150) -----------------------------------------
-HScene cornellBoxScene() {
-    HScene s;
-    const HMaterial lightMat = material(v3{0, 0, 0}, v3{0, 0, 0}, v3{0, 0, 0}, 1.0F, v3{0.9F, 0.9F, 0.9F});
-    const HMaterial mirrorMat = material(v3{0, 0, 0}, v3{0.9F, 0.9F, 0.9F}, v3{0, 0, 0}, 1.0F);
-    const HMaterial lightGrayMat = material(v3{0.7F, 0.7F, 0.7F});
-    const HMaterial redMat = material(v3{0.9F, 0.0F, 0.0F});
-    const HMaterial yellowMat = material(v3{0.9F, 0.9F, 0.0F});
-    const HMaterial greenMat = material(v3{0.0F, 0.9F, 0.0F});
-    const HMaterial blueMat = material(v3{0.0F, 0.0F, 0.9F});
-    const HMaterial lightBlueMat = material(v3{0.0F, 0.9F, 0.9F});
+namespace {
+// Scenes.cpp:19-58 materials
+const HMaterial kLightMat = material(v3{0, 0, 0}, v3{0, 0, 0}, v3{0, 0, 0}, 1.0F, v3{0.9F, 0.9F, 0.9F});
+const HMaterial kMirrorMat = material(v3{0, 0, 0}, v3{0.9F, 0.9F, 0.9F}, v3{0, 0, 0}, 1.0F);
+const HMaterial kTransmissionMat = material(v3{0, 0, 0}, v3{0, 0, 0}, v3{0.9F, 0.9F, 0.9F}, 1.9F);
+const HMaterial kLightGrayMat = material(v3{0.7F, 0.7F, 0.7F});
+const HMaterial kRedMat = material(v3{0.9F, 0.0F, 0.0F});
+const HMaterial kYellowMat = material(v3{0.9F, 0.9F, 0.0F});
+const HMaterial kGreenMat = material(v3{0.0F, 0.9F, 0.0F});
+const HMaterial kBlueMat = material(v3{0.0F, 0.0F, 0.9F});
+const HMaterial kSandMat = material(v3{0.914F, 0.723F, 0.531F});
+const HMaterial kLightBlueMat = material(v3{0.0F, 0.9F, 0.9F});
 
-    HLight light;
-    light.kind = kPointLight;
-    light.radiance = lightMat;
-    light.position = v3{0.0F, 0.99F, 0.0F};
-    s.lights.push_back(light);
+void addTriangle(HScene* s, v3 a, v3 b, v3 c, const HMaterial& m) {
+    HTriangle tri = makeTriangle(a, b, c);
+    tri.mat = static_cast<int32_t>(s->materials.size());
+    s->triangles.push_back(tri);
+    s->materials.push_back(m);
+}
 
-    HTriangle tri = makeTriangle(v3{0.5F, -0.5F, 0.99F}, v3{0.5F, 0.5F, 1.001F}, v3{-0.5F, -0.5F, 0.99F});
-    tri.mat = static_cast<int32_t>(s.materials.size());
-    s.triangles.push_back(tri);
-    s.materials.push_back(yellowMat);
+void addSphere(HScene* s, v3 c, float r, const HMaterial& m) {
+    s->spheres.push_back(makeSphere(c, r, static_cast<int32_t>(s->materials.size())));
+    s->materials.push_back(m);
+}
 
-    s.spheres.push_back(makeSphere(v3{0.45F, -0.65F, 0.4F}, 0.35F, static_cast<int32_t>(s.materials.size())));
-    s.materials.push_back(mirrorMat);
-    s.spheres.push_back(makeSphere(v3{-0.45F, -0.1F, 0.0F}, 0.35F, static_cast<int32_t>(s.materials.size())));
-    s.materials.push_back(greenMat);
+void addPlane(HScene* s, v3 p, v3 n, const HMaterial& m) {
+    s->planes.push_back(makePlane(p, n, static_cast<int32_t>(s->materials.size())));
+    s->materials.push_back(m);
+}
 
+void cornellBoxWalls(HScene* s) {  // Scenes.cpp:63-107
     const v3 back{0, 0, 1}, front{0, 0, -1}, bottom{0, -1, 0}, top{0, 1, 0};
-    auto addPlane = [&s](v3 p, v3 n, const HMaterial& m) {
-        s.planes.push_back(makePlane(p, n, static_cast<int32_t>(s.materials.size())));
-        s.materials.push_back(m);
-    };
-    addPlane(back, front, lightGrayMat);
-    addPlane(v3{0.0F, 0.0F, -3.5F}, v3{0.0F, 0.0F, 1.0F}, lightBlueMat);
-    addPlane(bottom, top, lightGrayMat);
-    addPlane(top, bottom, lightGrayMat);
-    addPlane(v3{-1.0F, 0.0F, 0.0F}, v3{1.0F, 0.0F, 0.0F}, redMat);
-    addPlane(v3{1.0F, 0.0F, 0.0F}, v3{-1.0F, 0.0F, 0.0F}, blueMat);
+    addPlane(s, back, front, kLightGrayMat);
+    addPlane(s, v3{0.0F, 0.0F, -3.5F}, v3{0.0F, 0.0F, 1.0F}, kLightBlueMat);
+    addPlane(s, bottom, top, kLightGrayMat);
+    addPlane(s, top, bottom, kLightGrayMat);
+    addPlane(s, v3{-1.0F, 0.0F, 0.0F}, v3{1.0F, 0.0F, 0.0F}, kRedMat);
+    addPlane(s, v3{1.0F, 0.0F, 0.0F}, v3{-1.0F, 0.0F, 0.0F}, kBlueMat);
+}
+
+HLight pointLight(v3 p) {
+    HLight l;
+    l.kind = kPointLight;
+    l.radiance = kLightMat;
+    l.position = p;
+    return l;
+}
+}  // namespace
+
+HScene cornellBoxScene() {  // Scenes.cpp:109-137
+    HScene s;
+    s.lights.push_back(pointLight(v3{0.0F, 0.99F, 0.0F}));
+    addTriangle(&s, v3{0.5F, -0.5F, 0.99F}, v3{0.5F, 0.5F, 1.001F}, v3{-0.5F, -0.5F, 0.99F}, kYellowMat);
+    addSphere(&s, v3{0.45F, -0.65F, 0.4F}, 0.35F, kMirrorMat);
+    addSphere(&s, v3{-0.45F, -0.1F, 0.0F}, 0.35F, kGreenMat);
+    cornellBoxWalls(&s);
     return s;
+}
+
+HScene builtinScene(int index) {
+    HScene s;
+    switch (index) {
+        case 0:
+            return cornellBoxScene();
+        case 1:  // spheres_Scene (Scenes.cpp:227-249): no lights
+            addSphere(&s, v3{4.0F, 4.0F, 4.0F}, 4.0F, kRedMat);
+            addTriangle(&s, v3{0.0F, 10.0F, 10.0F}, v3{0.0F, 0.0F, 10.0F}, v3{10.0F, 0.0F, 10.0F}, kSandMat);
+            return s;
+        case 2: {  // cornellBox2_Scene (Scenes.cpp:152-224): two area lights, transmission
+            const v3 quad[2][3] = {{v3{-0.25F, 0.99F, -0.25F}, v3{0.25F, 0.99F, -0.25F}, v3{0.25F, 0.99F, 0.25F}},
+                                   {v3{0.25F, 0.99F, 0.25F}, v3{-0.25F, 0.99F, 0.25F}, v3{-0.25F, 0.99F, -0.25F}}};
+            for (const auto& q : quad) {
+                HLight l;
+                l.kind = kAreaLight;
+                l.radiance = kLightMat;
+                l.position = v3{0, 0, 0};
+                l.tri = makeTriangle(q[0], q[1], q[2]);
+                l.tri.mat = -1;
+                s.lights.push_back(l);
+            }
+            addTriangle(&s, v3{0.5F, -0.5F, 0.99F}, v3{0.5F, 0.5F, 1.001F}, v3{-0.5F, -0.5F, 0.99F}, kYellowMat);
+            addTriangle(&s, v3{-0.5F, 0.5F, 0.99F}, v3{-0.5F, -0.5F, 0.99F}, v3{0.5F, 0.5F, 0.99F}, kGreenMat);
+            addSphere(&s, v3{0.45F, -0.65F, 0.4F}, 0.35F, kMirrorMat);
+            addSphere(&s, v3{-0.4F, -0.3F, 0.0F}, 0.35F, kTransmissionMat);
+            cornellBoxWalls(&s);
+            return s;
+        }
+        default:  // 3: spheres2_Scene (Scenes.cpp:264-289)
+            s.lights.push_back(pointLight(v3{0.0F, 15.0F, 4.0F}));
+            addSphere(&s, v3{-1.0F, 1.0F, 6.0F}, 1.0F, kRedMat);
+            addSphere(&s, v3{-0.5F, 2.0F, 5.0F}, 0.3F, kBlueMat);
+            addSphere(&s, v3{0.0F, 2.0F, 7.0F}, 1.0F, kMirrorMat);
+            addSphere(&s, v3{0.5F, 0.5F, 5.0F}, 0.2F, kYellowMat);
+            addSphere(&s, v3{1.0F, 0.5F, 4.5F}, 0.5F, kGreenMat);
+            addPlane(&s, v3{0.0F, 0.0F, 0.0F}, v3{0.0F, 1.0F, 0.0F}, kSandMat);
+            return s;
+    }
+}
+
+GCamera builtinCamera(int index, float ratio) {
+    switch (index) {
+        case 1:  // spheres_Cam (Scenes.cpp:251-262)
+            return makeOrthographic(v3{0.0F, 1.0F, -10.0F}, v3{0.0F, 1.0F, 7.0F}, v3{0.0F, 1.0F, 0.0F}, 10.0F * ratio,
+                                    10.0F);
+        case 3:  // spheres2_Cam (Scenes.cpp:291-302)
+            return makePerspective(v3{0.0F, 0.5F, 1.0F}, v3{0.0F, 0.0F, 7.0F}, v3{0.0F, 1.0F, 0.0F}, 60.0F * ratio, 60.0F);
+        default:  // 0, 2: cornellBox_Cam
+            return cornellBoxCamera(ratio);
+    }
+}
+
+v3 builtinMaxPoint(int index) {  // C_wrapper.cpp:79-131 maxDist (DepthMap)
+    return (index == 1 || index == 3) ? v3{8.0F, 8.0F, 8.0F} : v3{1.0F, 1.0F, 1.0F};
+}
+
+GCamera makeOrthographic(v3 position, v3 lookAt, v3 up, float sizeH, float sizeV) {  // Orthographic.cpp:7-13
+    GCamera c{};
+    c.position = position;
+    c.direction = normalize(lookAt - position);  // Camera.cpp:14-19
+    c.right = cross(up, c.direction);
+    c.up = cross(c.direction, c.right);
+    c.hFov = sizeH / 2.0F;  // half sizes
+    c.vFov = sizeV / 2.0F;
+    c.kind = 1;
+    return c;
 }
 
 GCamera makePerspective(v3 position, v3 lookAt, v3 up, float hFovDeg, float vFovDeg) {

@@ -80,6 +80,10 @@ struct HBVHNode {
 
 // ---- scenes / loaders ------------------------------------------------------------------
 HScene cornellBoxScene();                                     // Scenes.cpp:63-137 (scene 0)
+HScene builtinScene(int index);                               // C_wrapper.cpp:76-99: scenes 0-3
+GCamera builtinCamera(int index, float ratio);                // their cameras (Scenes.cpp)
+v3 builtinMaxPoint(int index);                                // DepthMap maxDist (C_wrapper.cpp:79-131)
+GCamera makeOrthographic(v3 position, v3 lookAt, v3 up, float sizeH, float sizeV);
 GCamera cornellBoxCamera(float ratio);                        // Scenes.cpp:139-150
 GCamera makePerspective(v3 position, v3 lookAt, v3 up, float hFovDeg, float vFovDeg);
 // CameraFactory.cpp + PerspectiveLoader.cpp:18-64 (position.x negated, hFov = fov.u * ratio)

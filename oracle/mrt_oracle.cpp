@@ -538,9 +538,22 @@ struct Light {
 };
 
 // ---- camera -------------------------------------------------------------------------------
-struct Camera {  // Camera.cpp:14-19, Perspective.cpp
+struct Camera {  // Camera.cpp:14-19, Perspective.cpp, Orthographic.cpp
     Vec3 position, direction, right, up;
     float hFov = 0, vFov = 0;
+    bool ortho = false;
+    float sizeH = 0, sizeV = 0;  // Orthographic: half sizes (Orthographic.cpp:8-13)
+    static Camera orthographic(const Vec3& pos, const Vec3& lookAt, const Vec3& upv, float sH, float sV) {
+        Camera c;
+        c.position = pos;
+        c.direction = normalize(lookAt - pos);
+        c.right = cross(upv, c.direction);
+        c.up = cross(c.direction, c.right);
+        c.ortho = true;
+        c.sizeH = sH / 2.0F;
+        c.sizeV = sV / 2.0F;
+        return c;
+    }
     static float degToRad(float deg) { return (deg * kPi) / 180.0F; }
     static Camera perspective(const Vec3& pos, const Vec3& lookAt, const Vec3& upv, float hFovDeg, float vFovDeg) {
         Camera c;
@@ -557,6 +570,13 @@ struct Camera {  // Camera.cpp:14-19, Perspective.cpp
         return kQuarterPi * value - (value * (absValue - 1.0F)) * (0.2447F + (0.0663F * absValue));
     }
     Ray generateRay(float u, float v, float du, float dv, std::atomic<uint64_t>* counter) const {
+        if (ortho) {  // Orthographic.cpp:15-24
+            const float rightFactor = (u - 0.5F) * sizeH;
+            const Vec3 r = right * rightFactor + right * du;
+            const float upFactor = (0.5F - v) * sizeV;
+            const Vec3 uu = up * upFactor + up * dv;
+            return Ray(direction, position + r + uu, 1, false, nullptr, counter);
+        }
         const float rightFactor = fastArcTan(hFov * (u - 0.5F)) + du;
         const Vec3 r = right * rightFactor;
         const float upFactor = fastArcTan(vFov * (0.5F - v)) + dv;
@@ -575,6 +595,8 @@ struct Scene {
     std::vector<Material> materials;
 };
 
+void cornellBoxWalls(Scene* s);
+
 void cornellBox(Scene* s, Camera* cam, float ratio) {  // Scenes.cpp:19-150
     const Material lightMat(Vec3(0.0F), Vec3(0.0F), Vec3(0.0F), 1.0F, Vec3(0.9F, 0.9F, 0.9F));
     const Material mirrorMat(Vec3(0.0F), Vec3(0.9F, 0.9F, 0.9F), Vec3(0.0F), 1.0F);
@@ -591,6 +613,11 @@ void cornellBox(Scene* s, Camera* cam, float ratio) {  // Scenes.cpp:19-150
     s->materials.push_back(mirrorMat);
     s->spheres.emplace_back(Vec3(-0.45F, -0.1F, 0.0F), 0.35F, static_cast<int32_t>(s->materials.size()));
     s->materials.emplace_back(Vec3(0.0F, 0.9F, 0.0F));
+    cornellBoxWalls(s);
+    *cam = Camera::perspective(Vec3(0.0F, 0.0F, -3.4F), Vec3(0.0F, 0.0F, 1.0F), Vec3(0.0F, 1.0F, 0.0F), 45.0F * ratio, 45.0F);
+}
+
+void cornellBoxWalls(Scene* s) {  // Scenes.cpp:63-107
     const Material gray(Vec3(0.7F, 0.7F, 0.7F));
     struct P { Vec3 p, n; Material m; };
     const P ps[] = {{Vec3(0, 0, 1), Vec3(0, 0, -1), gray},
@@ -603,7 +630,69 @@ void cornellBox(Scene* s, Camera* cam, float ratio) {  // Scenes.cpp:19-150
         s->planes.emplace_back(p.p, p.n, static_cast<int32_t>(s->materials.size()));
         s->materials.push_back(p.m);
     }
+}
+
+// Scenes.cpp:152-224 (scene 2: two area lights, transmission sphere)
+void cornellBox2(Scene* s, Camera* cam, float ratio) {
+    const Material lightMat(Vec3(0.0F), Vec3(0.0F), Vec3(0.0F), 1.0F, Vec3(0.9F, 0.9F, 0.9F));
+    const Material mirrorMat(Vec3(0.0F), Vec3(0.9F, 0.9F, 0.9F), Vec3(0.0F), 1.0F);
+    const Material transmissionMat(Vec3(0.0F), Vec3(0.0F), Vec3(0.9F, 0.9F, 0.9F), 1.9F);
+    const Vec3 quad[2][3] = {{Vec3(-0.25F, 0.99F, -0.25F), Vec3(0.25F, 0.99F, -0.25F), Vec3(0.25F, 0.99F, 0.25F)},
+                             {Vec3(0.25F, 0.99F, 0.25F), Vec3(-0.25F, 0.99F, 0.25F), Vec3(-0.25F, 0.99F, -0.25F)}};
+    for (const auto& q : quad) {
+        Light l;
+        l.area = true;
+        l.radiance = lightMat;
+        l.triangle = Triangle::build(q[0], q[1], q[2], nullptr, nullptr, nullptr, -1);
+        l.index = static_cast<int64_t>(s->lights.size());
+        s->lights.push_back(l);
+    }
+    s->triangles.push_back(Triangle::build(Vec3(0.5F, -0.5F, 0.99F), Vec3(0.5F, 0.5F, 1.001F), Vec3(-0.5F, -0.5F, 0.99F),
+                                           nullptr, nullptr, nullptr, static_cast<int32_t>(s->materials.size())));
+    s->materials.emplace_back(Vec3(0.9F, 0.9F, 0.0F));
+    s->triangles.push_back(Triangle::build(Vec3(-0.5F, 0.5F, 0.99F), Vec3(-0.5F, -0.5F, 0.99F), Vec3(0.5F, 0.5F, 0.99F),
+                                           nullptr, nullptr, nullptr, static_cast<int32_t>(s->materials.size())));
+    s->materials.emplace_back(Vec3(0.0F, 0.9F, 0.0F));
+    s->spheres.emplace_back(Vec3(0.45F, -0.65F, 0.4F), 0.35F, static_cast<int32_t>(s->materials.size()));
+    s->materials.push_back(mirrorMat);
+    s->spheres.emplace_back(Vec3(-0.4F, -0.3F, 0.0F), 0.35F, static_cast<int32_t>(s->materials.size()));
+    s->materials.push_back(transmissionMat);
+    cornellBoxWalls(s);
     *cam = Camera::perspective(Vec3(0.0F, 0.0F, -3.4F), Vec3(0.0F, 0.0F, 1.0F), Vec3(0.0F, 1.0F, 0.0F), 45.0F * ratio, 45.0F);
+}
+
+// Scenes.cpp:227-262 (scene 1: no lights, orthographic camera)
+void spheres(Scene* s, Camera* cam, float ratio) {
+    s->spheres.emplace_back(Vec3(4.0F, 4.0F, 4.0F), 4.0F, static_cast<int32_t>(s->materials.size()));
+    s->materials.emplace_back(Vec3(0.9F, 0.0F, 0.0F));
+    s->triangles.push_back(Triangle::build(Vec3(0.0F, 10.0F, 10.0F), Vec3(0.0F, 0.0F, 10.0F), Vec3(10.0F, 0.0F, 10.0F),
+                                           nullptr, nullptr, nullptr, static_cast<int32_t>(s->materials.size())));
+    s->materials.emplace_back(Vec3(0.914F, 0.723F, 0.531F));
+    *cam = Camera::orthographic(Vec3(0.0F, 1.0F, -10.0F), Vec3(0.0F, 1.0F, 7.0F), Vec3(0.0F, 1.0F, 0.0F), 10.0F * ratio,
+                                10.0F);
+}
+
+// Scenes.cpp:264-302 (scene 3: point light, five spheres, a floor plane)
+void spheres2(Scene* s, Camera* cam, float ratio) {
+    Light pl;
+    pl.radiance = Material(Vec3(0.0F), Vec3(0.0F), Vec3(0.0F), 1.0F, Vec3(0.9F, 0.9F, 0.9F));
+    pl.position = Vec3(0.0F, 15.0F, 4.0F);
+    pl.index = 0;
+    s->lights.push_back(pl);
+    const Material mirrorMat(Vec3(0.0F), Vec3(0.9F, 0.9F, 0.9F), Vec3(0.0F), 1.0F);
+    struct Sp { Vec3 c; float r; Material m; };
+    const Sp sp[] = {{Vec3(-1.0F, 1.0F, 6.0F), 1.0F, Material(Vec3(0.9F, 0.0F, 0.0F))},
+                     {Vec3(-0.5F, 2.0F, 5.0F), 0.3F, Material(Vec3(0.0F, 0.0F, 0.9F))},
+                     {Vec3(0.0F, 2.0F, 7.0F), 1.0F, mirrorMat},
+                     {Vec3(0.5F, 0.5F, 5.0F), 0.2F, Material(Vec3(0.9F, 0.9F, 0.0F))},
+                     {Vec3(1.0F, 0.5F, 4.5F), 0.5F, Material(Vec3(0.0F, 0.9F, 0.0F))}};
+    for (const Sp& q : sp) {
+        s->spheres.emplace_back(q.c, q.r, static_cast<int32_t>(s->materials.size()));
+        s->materials.push_back(q.m);
+    }
+    s->planes.emplace_back(Vec3(0.0F, 0.0F, 0.0F), Vec3(0.0F, 1.0F, 0.0F), static_cast<int32_t>(s->materials.size()));
+    s->materials.emplace_back(Vec3(0.914F, 0.723F, 0.531F));
+    *cam = Camera::perspective(Vec3(0.0F, 0.5F, 1.0F), Vec3(0.0F, 0.0F, 7.0F), Vec3(0.0F, 1.0F, 0.0F), 60.0F * ratio, 60.0F);
 }
 
 // tinyobjloader v1.0.7 number parser
@@ -891,6 +980,7 @@ struct Config {
 struct Engine {
     Config cfg{};
     Camera camera;
+    Vec3 maxPoint;  // DepthMap (C_wrapper.cpp:79-131)
     std::vector<Material> materials;
     std::vector<Light> lights;
     std::unique_ptr<BVH<Plane>> planes;
@@ -993,6 +1083,48 @@ struct Engine {
 
     bool shade(Vec3* rgb, const Intersection& it, Ctx ctx, uint32_t tc) {
         const int32_t rayDepth = it.ray.depth;
+        if (cfg.shader == 3) {  // DepthMap.cpp:13-18
+            const float maxDist = length(maxPoint - it.ray.origin) * 1.1F;
+            const float depth = std::max((maxDist - it.length) / maxDist, 0.0F);
+            *rgb = Vec3(depth, depth, depth);
+            return false;
+        }
+        if (cfg.shader == 4) {  // DiffuseMaterial.cpp:12-28
+            const Material& m = *it.material;
+            if (hasPositiveValue(m.Kd)) {
+                *rgb = m.Kd;
+            } else if (hasPositiveValue(m.Ks)) {
+                *rgb = m.Ks;
+            } else if (hasPositiveValue(m.Kt)) {
+                *rgb = m.Kt;
+            } else if (hasPositiveValue(m.Le)) {
+                *rgb = m.Le;
+            }
+            return false;
+        }
+        if (cfg.shader != 1 && cfg.shader != 2) {  // NoShadows.cpp:13-44 (C_wrapper.cpp:188-193 default)
+            const Vec3& lE = it.material->Le;
+            if (hasPositiveValue(lE)) {
+                *rgb = lE;
+                return true;
+            }
+            const Vec3& kD = it.material->Kd;
+            if (hasPositiveValue(kD)) {
+                if (!lights.empty()) {
+                    for (int32_t j = 0; j < cfg.samplesLight; ++j) {
+                        const Light& light = lights[lightIndex(ctx, tc, j)];
+                        const Vec3 lightPos = lightPosition(light, ctx, tc, j);
+                        const Vec3 toLight = normalize(lightPos - it.point);
+                        const float cosNl = dot(it.normal, toLight);
+                        if (cosNl > 0.0F) *rgb += light.radiance.Le * cosNl;
+                    }
+                    *rgb *= kD;
+                    *rgb /= static_cast<float>(cfg.samplesLight);
+                }
+            }
+            *rgb += kD * 0.1F;
+            return false;
+        }
         if (rayDepth > cfg.maxDepth) return false;
         const Vec3& lE = it.material->Le;
         if (hasPositiveValue(lE)) {
@@ -1139,8 +1271,18 @@ Engine* create(const Config& cfg) {
     e->cfg = cfg;
     const float ratio = static_cast<float>(cfg.width) / cfg.height;
     Scene s;
+    // C_wrapper.cpp:76-140; maxDist feeds DepthMap (shader 3)
+    e->maxPoint = Vec3(1.0F, 1.0F, 1.0F);
     if (cfg.sceneIndex == 0) {
         cornellBox(&s, &e->camera, ratio);
+    } else if (cfg.sceneIndex == 1) {
+        spheres(&s, &e->camera, ratio);
+        e->maxPoint = Vec3(8.0F, 8.0F, 8.0F);
+    } else if (cfg.sceneIndex == 2) {
+        cornellBox2(&s, &e->camera, ratio);
+    } else if (cfg.sceneIndex == 3) {
+        spheres2(&s, &e->camera, ratio);
+        e->maxPoint = Vec3(8.0F, 8.0F, 8.0F);
     } else {
         std::string err;
         if (!loadObj(cfg.obj, cfg.mtl, &s, &err)) return nullptr;

@@ -36,6 +36,18 @@ CASES = {
     "conference96_whitted": dict(width=96, height=96, shader=1, sceneIndex=-1, scene="conference"),
     "conference96_pt4": dict(width=96, height=96, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5,
                              scene="conference"),
+    # the other built-in scenes (C_wrapper.cpp:76-99) and shaders (C_wrapper.cpp:153-193)
+    "spheres128_whitted": dict(width=128, height=128, shader=1, sceneIndex=1),
+    "spheres128_depthmap": dict(width=128, height=128, shader=3, sceneIndex=1),
+    "cornell2_128_whitted": dict(width=128, height=128, shader=1, sceneIndex=2),
+    "cornell2_128_pt4": dict(width=128, height=128, shader=2, sceneIndex=2, samplesPixel=4),
+    "spheres2_128_whitted": dict(width=128, height=128, shader=1, sceneIndex=3),
+    "spheres2_128_noshadows": dict(width=128, height=128, shader=0, sceneIndex=3),
+    "cornell128_depthmap": dict(width=128, height=128, shader=3, sceneIndex=0),
+    "cornell128_diffuse": dict(width=128, height=128, shader=4, sceneIndex=0),
+    "cornell2_128_noshadows_spl2": dict(width=128, height=128, shader=5, sceneIndex=2, samplesLight=2, samplesPixel=2),
+    "conference96_noshadows": dict(width=96, height=96, shader=0, sceneIndex=-1, scene="conference"),
+    "conference96_diffuse": dict(width=96, height=96, shader=4, sceneIndex=-1, scene="conference"),
 }
 
 

@@ -26,8 +26,11 @@ def golden():
         return json.load(f)
 
 
-@pytest.mark.parametrize("name", ["cornell256_whitted", "cornell512_whitted", "cornell256_pt4", "water128_whitted",
-                                  "water128_pt4", "teapot128_whitted", "conference96_whitted", "conference96_pt4"])
+with open(os.path.join(GOLDEN, "golden.json")) as _f:
+    GOLDEN_CASES = sorted(k for k, v in json.load(_f).items() if isinstance(v, dict))
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
 def test_oracle_matches_golden(oracle_mod, golden, name):
     import importlib.util
     spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))

@@ -29,8 +29,9 @@ def scene_paths(name):
 
 def make_cfg(width, height, shader=1, scene=None, spp=1, spl=1, max_depth=6, **kw):
     import mobileraytracer_amd as m
+    scene_index = kw.pop("sceneIndex", 0 if scene is None else -1)
     cfg = m.Config(width=width, height=height, shader=shader, samplesPixel=spp, samplesLight=spl, maxDepth=max_depth,
-                   sceneIndex=0 if scene is None else -1, **kw)
+                   sceneIndex=scene_index, **kw)
     if scene is not None:
         cfg.objFilePath, cfg.mtlFilePath, cfg.camFilePath = scene_paths(scene)
     return cfg
@@ -85,6 +86,9 @@ def assert_within_tolerance(gpu, ref, mask=None):
     dict(width=96, height=96, scene="conference"),
     dict(width=30, height=30),                                   # the reference engine tests' size
     dict(width=100, height=60),                                  # non-multiple-of-16 tiling
+    dict(width=128, height=128, sceneIndex=1),                   # spheres_Scene, orthographic camera
+    dict(width=128, height=128, sceneIndex=2),                   # cornellBox2_Scene, area lights
+    dict(width=128, height=128, sceneIndex=3),                   # spheres2_Scene
 ])
 def test_primary_hits_bit_exact(oracle_mod, case):
     cfg = make_cfg(**case)
@@ -117,6 +121,42 @@ def test_whitted_bit_exact(oracle_mod, case):
     assert rays == ref_rays
 
 
+# ---- the other built-in scenes and shaders (C_wrapper.cpp:76-99, 153-193): bit-exact ----------------
+@pytest.mark.parametrize("case", [
+    dict(width=128, height=128, sceneIndex=1, shader=1),             # no lights: ambient only
+    dict(width=128, height=128, sceneIndex=1, shader=3),             # DepthMap, orthographic camera
+    dict(width=128, height=128, sceneIndex=2, shader=1),             # area lights, transmission sphere
+    dict(width=128, height=128, sceneIndex=3, shader=1),             # point light, plane + spheres
+    dict(width=128, height=128, sceneIndex=3, shader=0),             # NoShadows (the switch's default)
+    dict(width=128, height=128, sceneIndex=0, shader=3),             # DepthMap
+    dict(width=128, height=128, sceneIndex=0, shader=4),             # DiffuseMaterial
+    dict(width=128, height=128, sceneIndex=2, shader=5, spl=2, spp=2),  # NoShadows, area lights, jitter
+    dict(width=96, height=96, scene="conference", shader=0),
+    dict(width=96, height=96, scene="conference", shader=4),
+    dict(width=96, height=96, scene="conference", shader=3),
+    dict(width=100, height=60, sceneIndex=3, shader=2, spp=2),       # PathTracer: tolerance below
+])
+def test_other_scenes_and_shaders(oracle_mod, case):
+    cfg = make_cfg(**case)
+    bm, rays, _ = gpu_render(cfg)
+    ref, ref_rays = oracle_render(oracle_mod, cfg)
+    once = coverage(cfg.width, cfg.height) == 1
+    if cfg.shader == 2:
+        assert_within_tolerance(bm, ref, once & (ref != SENTINEL))
+        assert abs(rays - ref_rays) <= 0.002 * ref_rays, (rays, ref_rays)
+    else:
+        assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
+        assert rays == ref_rays
+    assert len(np.unique(bm)) > 1
+
+
+def test_unknown_shader_ids_are_noshadows():
+    """C_wrapper.cpp:188-193: every shader id other than 1-4 builds NoShadows."""
+    a, ra, _ = gpu_render(make_cfg(64, 64, shader=0, sceneIndex=3))
+    b, rb, _ = gpu_render(make_cfg(64, 64, shader=7, sceneIndex=3))
+    assert np.array_equal(a, b) and ra == rb
+
+
 def coverage(width, height):
     """How many reference tiles write each bitmap index.  With width % 16 != 0 the tile formula
     (Renderer.cpp:126-135) wraps x past the row end, so some pixels belong to two tiles and the
@@ -142,6 +182,7 @@ def test_c1_matches_committed_fixture():
     dict(width=128, height=128, spp=4, scene="water"),            # branching ray tree (Kd + Ks)
     dict(width=96, height=96, spp=4, max_depth=5, scene="conference"),
     dict(width=64, height=64, spp=2, spl=2, scene="water"),
+    dict(width=128, height=128, spp=4, sceneIndex=2),             # area lights + transmission sphere
 ])
 def test_pathtracer_within_tolerance(oracle_mod, case):
     cfg = make_cfg(shader=2, **case)
@@ -358,8 +399,6 @@ def test_invalid_config_raises():
     import mobileraytracer_amd as m
     with pytest.raises(RuntimeError):
         m.Renderer(make_cfg(8, 8))
-    with pytest.raises(RuntimeError):
-        m.Renderer(make_cfg(64, 64, shader=7))
     bad = make_cfg(64, 64, scene="water")
     bad.objFilePath = "/nonexistent.obj"
     with pytest.raises(RuntimeError):
