@@ -121,6 +121,12 @@ int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /
  * 4 light; index in the scene's input order (-1 on miss); t = hit distance */
 int mrt_primary_hits(mrt_renderer *r, int32_t *kind, int32_t *index, float *t);
+/* Host only (no GPU): the scene's triangle BVH as built for the device (BVH.hpp:161-283,
+ * built in parallel with the serial build's result).  Returns the node-array length N
+ * (slots; unreachable slots are zero) or -1.  With non-NULL outputs fills boxes[N*6]
+ * (min xyz, max xyz), offsets[N] / counts[N] (BVHNode::indexOffset / numPrimitives) and
+ * order[triangles] (input index of each triangle in BVH order). */
+int64_t mrt_triangle_bvh(const mrt_config *cfg, float *boxes, int32_t *offsets, int32_t *counts, int32_t *order);
 
 #ifdef __cplusplus
 }

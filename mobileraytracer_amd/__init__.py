@@ -157,6 +157,23 @@ class Renderer:
         self.close()
 
 
+def triangle_bvh(config: Config):
+    """Host-side triangle BVH of the configured scene (no GPU): boxes (N, 6), offsets, counts,
+    order - the layout of the reference's BVHNode array (BVH.hpp:56-60)."""
+    lib = _native.lib()
+    c = config.to_c()
+    n = lib.mrt_triangle_bvh(ctypes.byref(c), None, None, None, None)
+    if n < 0:
+        raise RuntimeError(lib.mrt_last_error().decode())
+    boxes = np.empty((n, 6), np.float32)
+    off, cnt = np.empty(n, np.int32), np.empty(n, np.int32)
+    order = np.full((n + 1) // 2, -1, np.int32)  # 2 * triangles - 1 slots (a lone root: 0 or 1 triangle)
+    n2 = lib.mrt_triangle_bvh(ctypes.byref(c), _ptr(boxes), _ptr(off), _ptr(cnt), _ptr(order))
+    if n2 != n:
+        raise RuntimeError(lib.mrt_last_error().decode())
+    return boxes, off, cnt, order[:int(cnt[0])] if n == 1 else order
+
+
 _active: List[Renderer] = []
 
 

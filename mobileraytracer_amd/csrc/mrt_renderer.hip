@@ -763,6 +763,35 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
     return -1;
 }
 
+int64_t mrt_triangle_bvh(const mrt_config* cfg, float* boxes, int32_t* offsets, int32_t* counts, int32_t* order) {
+    using namespace mrt;
+    int64_t n = -1;
+    const int rc = guarded([&] {
+        HScene sc;
+        if (cfg->sceneIndex >= 0 && cfg->sceneIndex <= 3) {
+            sc = builtinScene(cfg->sceneIndex);
+        } else {
+            std::string err;
+            if (!loadObjScene(cfg->objFilePath ? cfg->objFilePath : "", cfg->mtlFilePath ? cfg->mtlFilePath : "", &sc,
+                              &err))
+                throw std::runtime_error(err);
+        }
+        std::vector<int32_t> perm;
+        const std::vector<HBVHNode> nodes = buildBVH(&sc.triangles, &perm);
+        n = static_cast<int64_t>(nodes.size());
+        if (boxes == nullptr) return;
+        for (size_t i = 0; i < nodes.size(); ++i) {
+            const HBVHNode& b = nodes[i];
+            const float v[6] = {b.box.mn.x, b.box.mn.y, b.box.mn.z, b.box.mx.x, b.box.mx.y, b.box.mx.z};
+            std::memcpy(boxes + 6 * i, v, sizeof(v));
+            offsets[i] = b.indexOffset;
+            counts[i] = b.numPrimitives;
+        }
+        std::memcpy(order, perm.data(), perm.size() * sizeof(int32_t));
+    });
+    return rc == 0 ? n : -1;
+}
+
 int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
     if (key == 1) {
         *value = r->ds.variant;

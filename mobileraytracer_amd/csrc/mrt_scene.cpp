@@ -2,6 +2,7 @@
 #include "mrt_scene.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -9,6 +10,7 @@
 #include <fstream>
 #include <random>
 #include <sstream>
+#include <thread>
 #include <unordered_map>
 
 namespace mrt {
@@ -683,6 +685,61 @@ struct BuildNode {
 
 }  // namespace
 
+// One node of the build (BVH.hpp:161-283 loop body): bucket partition of bn[begin, end) along
+// the longest axis, the node box, then leaf (<= 4 prims) or SAH split.  Children go to slots
+// freeBase and freeBase + 1; a subtree of m prims owns 2m - 1 slots (its root's slot plus
+// 2m - 2 for descendants), so disjoint subtrees can be built concurrently and every node's
+// partition - hence the primitive order and every box - is the serial build's.
+struct BuildTask {
+    int32_t slot, begin, end, freeBase;
+};
+
+static int processNode(std::vector<BuildNode>& bn, std::vector<HBVHNode>& nodes, const BuildTask& t,
+                       std::vector<HAABB>& boxes, BuildTask* children) {
+    const int32_t begin = t.begin, end = t.end;
+    // getSurroundingBox (BVH.hpp:451-460)
+    HAABB sur{bn[static_cast<size_t>(begin)].box.mn, bn[static_cast<size_t>(begin)].box.mx};
+    for (int32_t i = begin + 1; i < end; ++i) sur = surrounding(sur, bn[static_cast<size_t>(i)].box);
+    const v3 maxDist = sur.mx - sur.mn;
+    const int axis = (maxDist.x >= maxDist.y && maxDist.x >= maxDist.z)
+                         ? 0
+                         : ((maxDist.y >= maxDist.x && maxDist.y >= maxDist.z) ? 1 : 2);
+    const int numBuckets = 10;
+    const v3 step = maxDist / static_cast<float>(numBuckets);
+    const float stepAxis = comp(step, axis);
+    const float startBox = comp(sur.mn, axis);
+    const float limit1 = startBox + stepAxis;
+    auto first = bn.begin() + begin;
+    auto last = bn.begin() + end;
+    auto itBucket = pinnedPartition(first, last, [axis, limit1](const BuildNode& x) { return comp(x.c, axis) < limit1; });
+    for (int32_t bi = 2; bi < numBuckets; ++bi) {
+        const float limit = startBox + stepAxis * static_cast<float>(bi);
+        itBucket = pinnedPartition(itBucket, last, [axis, limit](const BuildNode& x) { return comp(x.c, axis) < limit; });
+    }
+    HBVHNode& node = nodes[static_cast<size_t>(t.slot)];
+    node.box = bn[static_cast<size_t>(begin)].box;
+    boxes.clear();
+    boxes.push_back(node.box);
+    for (int32_t i = begin + 1; i < end; ++i) {
+        const HAABB nb = bn[static_cast<size_t>(i)].box;
+        node.box = surrounding(nb, node.box);
+        boxes.push_back(nb);
+    }
+    const int32_t count = end - begin;
+    if (count <= 4) {  // maxPrimitivesInBoxLeaf (BVH.hpp:239-251)
+        node.indexOffset = begin;
+        node.numPrimitives = count;
+        return 0;
+    }
+    const int32_t split = splitIndexSah(boxes);
+    node.indexOffset = t.freeBase;
+    node.numPrimitives = 0;
+    const int32_t leftFree = t.freeBase + 2;
+    children[0] = BuildTask{t.freeBase, begin, begin + split, leftFree};
+    children[1] = BuildTask{t.freeBase + 1, begin + split, end, leftFree + 2 * split - 2};
+    return 2;
+}
+
 template <class T>
 std::vector<HBVHNode> buildBVH(std::vector<T>* primsPtr, std::vector<int32_t>* order) {
     std::vector<T>& prims = *primsPtr;
@@ -700,67 +757,62 @@ std::vector<HBVHNode> buildBVH(std::vector<T>* primsPtr, std::vector<int32_t>* o
         const HAABB b = aabbOf(prims[static_cast<size_t>(i)]);
         bn.push_back(BuildNode{b, centroid(b), i});
     }
-    std::vector<int32_t> stIdx(64, 0), stBegin(64, 0), stEnd(64, 0);
-    size_t sp = 1;
-    int32_t cur = 0, begin = 0, end = n, maxNode = 0;
-    std::vector<HAABB> boxes;
-    do {
-        // getSurroundingBox (BVH.hpp:451-460)
-        HAABB sur{bn[static_cast<size_t>(begin)].box.mn, bn[static_cast<size_t>(begin)].box.mx};
-        for (int32_t i = begin + 1; i < end; ++i) sur = surrounding(sur, bn[static_cast<size_t>(i)].box);
-        const v3 maxDist = sur.mx - sur.mn;
-        const int axis = (maxDist.x >= maxDist.y && maxDist.x >= maxDist.z)
-                             ? 0
-                             : ((maxDist.y >= maxDist.x && maxDist.y >= maxDist.z) ? 1 : 2);
-        const int numBuckets = 10;
-        const v3 step = maxDist / static_cast<float>(numBuckets);
-        const float stepAxis = comp(step, axis);
-        const float startBox = comp(sur.mn, axis);
-        const float limit1 = startBox + stepAxis;
-        auto first = bn.begin() + begin;
-        auto last = bn.begin() + end;
-        auto itBucket = pinnedPartition(first, last, [axis, limit1](const BuildNode& x) { return comp(x.c, axis) < limit1; });
-        for (int32_t bi = 2; bi < numBuckets; ++bi) {
-            const float limit = startBox + stepAxis * static_cast<float>(bi);
-            itBucket = pinnedPartition(itBucket, last, [axis, limit](const BuildNode& x) { return comp(x.c, axis) < limit; });
-        }
-        HBVHNode& node = nodes[static_cast<size_t>(cur)];
-        node.box = bn[static_cast<size_t>(begin)].box;
-        boxes.clear();
-        boxes.push_back(node.box);
-        for (int32_t i = begin + 1; i < end; ++i) {
-            const HAABB nb = bn[static_cast<size_t>(i)].box;
-            node.box = surrounding(nb, node.box);
-            boxes.push_back(nb);
-        }
-        const int32_t count = end - begin;
-        if (count <= 4) {  // maxPrimitivesInBoxLeaf (BVH.hpp:239-251)
-            node.indexOffset = begin;
-            node.numPrimitives = count;
-            --sp;
-            cur = stIdx[sp];
-            begin = stBegin[sp];
-            end = stEnd[sp];
-        } else {
-            const int32_t left = maxNode + 1;
-            const int32_t right = left + 1;
-            const int32_t split = splitIndexSah(boxes);
-            node.indexOffset = left;
-            maxNode = std::max(right, maxNode);
-            if (sp >= stIdx.size()) {
-                stIdx.resize(sp * 2);
-                stBegin.resize(sp * 2);
-                stEnd.resize(sp * 2);
+    // the top of the tree level by level (the nodes of a level in parallel) until there are
+    // enough subtrees ...
+    const int workers = static_cast<int>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    constexpr int32_t kSerialBelow = 2048;  // subtrees smaller than this are not worth a hand-off
+    std::vector<BuildTask> frontier{BuildTask{0, 0, n, 1}};
+    std::vector<BuildTask> subtrees;
+    while (!frontier.empty() && static_cast<int>(frontier.size() + subtrees.size()) < 8 * workers) {
+        std::vector<BuildTask> level;
+        for (const BuildTask& t : frontier) {
+            if (workers == 1 || t.end - t.begin < kSerialBelow) {
+                subtrees.push_back(t);
+            } else {
+                level.push_back(t);
             }
-            stIdx[sp] = right;
-            stBegin[sp] = begin + split;
-            stEnd[sp] = end;
-            ++sp;
-            cur = left;
-            end = begin + split;
         }
-    } while (sp > 0);
-    nodes.resize(static_cast<size_t>(maxNode + 1));
+        std::vector<BuildTask> kids(2 * level.size());
+        std::vector<int> nk(level.size(), 0);
+        std::vector<std::thread> lt;
+        for (size_t i = 0; i < level.size(); ++i) {
+            lt.emplace_back([&, i]() {
+                std::vector<HAABB> scratch;
+                nk[i] = processNode(bn, nodes, level[i], scratch, &kids[2 * i]);
+            });
+        }
+        for (auto& th : lt) th.join();
+        frontier.clear();
+        for (size_t i = 0; i < level.size(); ++i)
+            for (int c = 0; c < nk[i]; ++c) frontier.push_back(kids[2 * i + static_cast<size_t>(c)]);
+    }
+    subtrees.insert(subtrees.end(), frontier.begin(), frontier.end());
+    std::sort(subtrees.begin(), subtrees.end(),
+              [](const BuildTask& x, const BuildTask& y) { return x.end - x.begin > y.end - y.begin; });
+    // ... then the subtrees depth-first, largest first, on a pool of threads
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+        std::vector<HAABB> scratch;
+        std::vector<BuildTask> stack;
+        BuildTask kids[2];
+        for (size_t i = next.fetch_add(1); i < subtrees.size(); i = next.fetch_add(1)) {
+            stack.assign(1, subtrees[i]);
+            while (!stack.empty()) {
+                const BuildTask t = stack.back();
+                stack.pop_back();
+                const int k = processNode(bn, nodes, t, scratch, kids);
+                if (k == 2) {  // left first (the serial order; results do not depend on it)
+                    stack.push_back(kids[1]);
+                    stack.push_back(kids[0]);
+                }
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    const int spawn = std::min<int>(workers, static_cast<int>(subtrees.size())) - 1;
+    for (int w = 0; w < spawn; ++w) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
     std::vector<T> permuted;
     permuted.reserve(prims.size());
     order->reserve(prims.size());

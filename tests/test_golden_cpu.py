@@ -106,3 +106,32 @@ def test_ctypes_layouts_match_header(tmp_path):
 def test_library_built_for_gfx950(native_lib_path):
     out = subprocess.run(["strings", native_lib_path], capture_output=True, text=True, check=True)
     assert "amdgcn-amd-amdhsa--gfx950" in out.stdout
+
+
+def _bvh_walk(boxes, off, cnt):
+    """Nodes in left-first depth-first order: (box bytes, numPrimitives, leaf offset)."""
+    out, st = [], [0]
+    while st:
+        i = st.pop()
+        leaf = cnt[i] > 0 or len(cnt) == 1
+        out.append((boxes[i].tobytes(), int(cnt[i]), int(off[i]) if leaf else -1))
+        if not leaf:
+            st += [int(off[i]) + 1, int(off[i])]
+    return out
+
+
+@pytest.mark.parametrize("scene", ["conference", "water", "teapot", 0, 1, 2, 3])
+def test_parallel_bvh_build_equals_reference_build(oracle_mod, scene):
+    """The renderer's multi-threaded BVH build (f1) yields the reference build's tree: same
+    boxes, leaves and primitive order as the oracle's serial restatement of BVH.hpp:161-283."""
+    import mobileraytracer_amd as m
+    from mobileraytracer_amd import scenes
+    cfg = m.Config(width=64, height=64, sceneIndex=scene if isinstance(scene, int) else -1)
+    if not isinstance(scene, int):
+        cfg.objFilePath, cfg.mtlFilePath, cfg.camFilePath = {
+            "conference": scenes.conference, "water": scenes.cornell_water, "teapot": scenes.teapot}[scene]()
+    boxes, off, cnt, order = m.triangle_bvh(cfg)
+    o = oracle_mod.Oracle(64, 64, 1, cfg.sceneIndex, obj=cfg.objFilePath, mtl=cfg.mtlFilePath, cam=cfg.camFilePath)
+    oboxes, ooff, ocnt, oorder = o.triangle_bvh()
+    assert _bvh_walk(boxes, off, cnt) == _bvh_walk(oboxes, ooff, ocnt)
+    assert np.array_equal(order, oorder)
