@@ -53,6 +53,8 @@ struct Level {
     float4* sO;      // shadow ray origin, w = source primitive bits
     float4* sD;      // shadow ray direction, w = distance to the light
     float4* sC;      // light contribution Le*cos, w = occluded flag
+    const int* order;        // trace visit order of the rays (null: queue order)
+    const int* shadowOrder;  // the same for the shadow rays
     int cap;
     int shadowCap;
 };
@@ -108,6 +110,11 @@ void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, in
 void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st);
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);
 void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st);
-int traceResidentThreadsPerCU();  // max over trace variants of resident threads per CU
+int traceResidentThreadsPerCU();
+// Ray reordering for traversal coherence: keys = direction octant | Morton code of the origin
+// in the scene box, radix-sorted with the ray index; `order` receives the visit order.
+size_t sortRaysTempBytes(int cap);
+void sortRays(const float4* rO, const float4* rD, const int* count, int cap, const GRoot& box, uint32_t* keys,
+              uint32_t* keysAlt, int* vals, int* order, void* temp, size_t tempBytes, hipStream_t st);  // max over trace variants of resident threads per CU
 
 }  // namespace mrt

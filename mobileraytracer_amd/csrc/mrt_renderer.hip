@@ -123,6 +123,16 @@ struct mrt_renderer {
     hipStream_t shadowStream = nullptr;  // any-hit launches, overlapped with the next level
     std::vector<hipEvent_t> syncPool;    // ordering events between the two streams
     int overlap = 1;                     // tuning key 3: shadow rays on their own stream
+    int sortRays = 0;                    // tuning key 4: reorder rays before tracing (1 closest-hit, 2 shadow)
+    struct SortBufs {
+        uint32_t* keys = nullptr;
+        uint32_t* keysAlt = nullptr;
+        int* vals = nullptr;
+        int* order = nullptr;
+        void* temp = nullptr;
+        size_t tempBytes = 0;
+        int cap = 0;
+    } sortRay, sortShadow;
 
     // state (Renderer.hpp:30-40)
     std::atomic<bool> stopFlag{false};
@@ -373,6 +383,17 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
             lv.sC = nullptr;
         }
     }
+    auto sortBufs = [&](mrt_renderer::SortBufs* b, size_t cap) {
+        b->cap = static_cast<int>(cap);
+        b->keys = r->queueMem.alloc<uint32_t>(cap);
+        b->keysAlt = r->queueMem.alloc<uint32_t>(cap);
+        b->vals = r->queueMem.alloc<int>(cap);
+        b->order = r->queueMem.alloc<int>(cap);
+        b->tempBytes = sortRaysTempBytes(b->cap);
+        b->temp = r->queueMem.alloc<uint8_t>(b->tempBytes);
+    };
+    sortBufs(&r->sortRay, capN);
+    sortBufs(&r->sortShadow, capN * spl);
     r->counters = r->queueMem.alloc<int>(kNumCounters);
     r->stats = r->queueMem.alloc<unsigned long long>(kNumStats);
     r->gdepth = std::max(1, r->stackNeed - kLdsStackMin);
@@ -438,6 +459,15 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             MRT_HIP(hipStreamWaitEvent(sb, start, 0));
         }
         for (int l = 1; l <= nLevels; ++l) {
+            Level& lv = r->levels[l];
+            lv.order = nullptr;
+            lv.shadowOrder = nullptr;
+            if ((r->sortRays & 1) != 0 && l >= 2) {
+                const auto& b = r->sortRay;
+                sortRays(lv.rO, lv.rD, r->counters + cntRays(l), std::min(lv.cap, b.cap), r->ds.triRoot, b.keys,
+                         b.keysAlt, b.vals, b.order, b.temp, b.tempBytes, st);
+                lv.order = b.order;
+            }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
             launchTrace(r->ds, r->levels[l], r->counters, l, r->gstack, r->gdepth, r->stats, counting, r->traceThreads, st);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
@@ -448,6 +478,12 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 const hipEvent_t shaded = syncEvent(r, sync++);
                 MRT_HIP(hipEventRecord(shaded, st));
                 MRT_HIP(hipStreamWaitEvent(sb, shaded, 0));
+            }
+            if (l < nLevels && (r->sortRays & 2) != 0) {
+                const auto& b = r->sortShadow;
+                sortRays(lv.sO, lv.sD, r->counters + cntShadows(l), std::min(lv.shadowCap, b.cap), r->ds.triRoot, b.keys,
+                         b.keysAlt, b.vals, b.order, b.temp, b.tempBytes, sb);
+                lv.shadowOrder = b.order;
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), sb));
             if (l < nLevels) {  // the last level (depth > RayDepthMax) shades nothing: no shadow rays
@@ -759,6 +795,10 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->overlap = value;
         return 0;
     }
+    if (key == 4 && value >= 0 && value <= 3) {
+        r->sortRays = value;
+        return 0;
+    }
     gLastError = "unknown tuning key/value";
     return -1;
 }
@@ -803,6 +843,10 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
     }
     if (key == 3) {
         *value = r->overlap;
+        return 0;
+    }
+    if (key == 4) {
+        *value = r->sortRays;
         return 0;
     }
     gLastError = "unknown tuning key";

@@ -131,7 +131,8 @@ __device__ __forceinline__ int innerStep4(const GNode4* node, v3 o, v3 inv, floa
 template <bool kAny, bool kCount, int kWide, int kRefill, int kShards, int kTop, bool kFastSlab>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                TStack& st, TravCount* cnt, const GNode* ldsTop) {
+                                                TStack& st, TravCount* cnt, const GNode* ldsTop,
+                                                const int* __restrict__ order) {
     const int top = kTop > 0 ? min(kTop, s.triTop) : 0;
     const int lane = static_cast<int>(threadIdx.x & 63u);
     int rayIdx = -1;
@@ -218,7 +219,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 }
             }
             if (need) {
-                rayIdx = got;
+                rayIdx = (got >= 0 && order != nullptr) ? order[got] : got;
                 if (rayIdx < 0) {
                     exhausted = true;
                 } else {
