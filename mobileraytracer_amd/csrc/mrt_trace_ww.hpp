@@ -18,6 +18,24 @@ namespace mrt {
 
 constexpr int kRefDone = 0x7FFFFFFF;  // sentinel: no node (never a valid inner index)
 
+// Buffer loads for the scene gathers: exact widths (the 8-byte child-reference load is not
+// widened to 16 bytes, which costs texture-data cycles), a 32-bit VGPR offset instead of a
+// 64-bit address, and the base in SGPRs.
+using BufRes = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ BufRes bufferOf(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), static_cast<short>(0), 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ float4 bload4(BufRes r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ float4 bload3(BufRes r, uint32_t off) {  // xyz; w undefined
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), 0.0F);
+}
+__device__ __forceinline__ int2 bload2i(BufRes r, uint32_t off) {
+    return __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
 // number of set bits of a wave mask below this lane
 __device__ __forceinline__ int lanesBelowIn(uint64_t m) {
     return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
@@ -37,7 +55,7 @@ __device__ __forceinline__ int popCulled(TStack& st, float lim, bool cull) {
 // top: nodes [0, top) are read from the LDS copy ldsTop (the breadth-first top of the tree)
 // finite: wave-uniform, every active lane's 1/d is finite (slabFinite applies)
 template <int kTop>
-__device__ __forceinline__ int innerStep2(const GNode* nodes, const GNode* ldsTop, int top, int ref, v3 o, v3 inv,
+__device__ __forceinline__ int innerStep2(BufRes nodes, const GNode* ldsTop, int top, int ref, v3 o, v3 inv,
                                           float lim, bool cull, TStack& st, TravCount* cnt, bool count, bool finite) {
     float4 n0, n1, n2;
     int2 n3;
@@ -48,11 +66,11 @@ __device__ __forceinline__ int innerStep2(const GNode* nodes, const GNode* ldsTo
         n2 = np[2];
         n3 = reinterpret_cast<const int2*>(np)[6];
     } else {
-        const float4* np = reinterpret_cast<const float4*>(nodes + ref);
-        n0 = np[0];
-        n1 = np[1];
-        n2 = np[2];
-        n3 = reinterpret_cast<const int2*>(np)[6];  // child refs (the rest is padding)
+        const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(GNode));
+        n0 = bload4(nodes, off);
+        n1 = bload4(nodes, off + 16u);
+        n2 = bload4(nodes, off + 32u);
+        n3 = bload2i(nodes, off + 48u);  // child refs (the rest is padding)
     }
     if (count) cnt->nodes += 2;
     float tl, tr;
@@ -134,6 +152,8 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                                                 TStack& st, TravCount* cnt, const GNode* ldsTop,
                                                 const int* __restrict__ order) {
     const int top = kTop > 0 ? min(kTop, s.triTop) : 0;
+    const BufRes nodeBuf = bufferOf(s.triNodes);
+    const BufRes triBuf = bufferOf(s.triGeom);
     const int lane = static_cast<int>(threadIdx.x & 63u);
     int rayIdx = -1;
     bool exhausted = false;
@@ -272,7 +292,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 ref = innerStep4(s.triNodes4 + ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
             } else {
                 const bool finite = kFastSlab && __ballot(!finiteInv(inv)) == 0;
-                ref = innerStep2<kTop>(s.triNodes, ldsTop, top, ref, o, inv, curLim, s.cull != 0, st, cnt, kCount,
+                ref = innerStep2<kTop>(nodeBuf, ldsTop, top, ref, o, inv, curLim, s.cull != 0, st, cnt, kCount,
                                        finite);
             }
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
@@ -289,10 +309,11 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 const int j = first + k;
                 const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
                 if (code == src) continue;
-                const float4* g = s.triGeom + 3 * j;
+                const uint32_t off = static_cast<uint32_t>(j) * 48u;
                 float t, u, v;
                 if (kCount) ++cnt->tris;
-                if (!triTest(g[0], g[1], g[2], o, d, &t, &u, &v)) continue;
+                if (!triTest(bload3(triBuf, off), bload3(triBuf, off + 16u), bload3(triBuf, off + 32u), o, d, &t, &u, &v))
+                    continue;
                 if (t < kEpsilon) continue;
                 if (kAny) {
                     if (!(t >= bt)) {
