@@ -78,10 +78,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MRT_BENCH_BACKEND=gloo (rehearsal only: several ranks sharing one GPU, gather through host
+    # memory); the measured multi-GPU path is RCCL ("nccl") with one GPU per rank
+    backend = os.environ.get("MRT_BENCH_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        local = local % torch.cuda.device_count() if backend == "gloo" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     scene = scenes.conference()
@@ -103,7 +110,14 @@ def main():
             r.render_frame_device(bitmap.data_ptr(), 0, sh)
         else:
             r.render_frame_device(0, packed.data_ptr(), sh)
-            dist.gather(packed, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if backend == "gloo":
+                host = packed.cpu()
+                parts = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+                dist.gather(host, parts, dst=0)
+                if rank == 0:
+                    gathered.copy_(torch.stack(parts))
+            else:
+                dist.gather(packed, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
             if rank == 0:
                 r.unpack_gathered(gathered.data_ptr(), bitmap.data_ptr(), sh)
 
@@ -135,14 +149,15 @@ def main():
     rays = r.get_total_casted_rays() - rays0
 
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        red = "cpu" if backend == "gloo" else "cuda"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        n = torch.tensor([rays], dtype=torch.float64, device="cuda")
+        n = torch.tensor([rays], dtype=torch.float64, device=red)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         rays = int(n.item())
         agg = torch.tensor([counted["rays"], counted["nodeRecords"], counted["triTests"], trace_ms, trace_launches],
-                           dtype=torch.float64, device="cuda")
+                           dtype=torch.float64, device=red)
         dist.all_reduce(agg, op=dist.ReduceOp.SUM)
         c_rays, c_nodes, c_tris, trace_ms, trace_launches = [float(x) for x in agg.tolist()]
     else:
@@ -184,7 +199,8 @@ def main():
             "rendered_pixels": int(info["pixelSlots"]) if world == 1 else None,
             "spp": args.spp, "max_depth": args.max_depth, "samples_light": 1,
             "shader": "PathTracer" if args.shader == 2 else "Whitted",
-            "parallelism": f"screen-tile shard x{world} + RCCL gather" if world > 1 else "single GPU",
+            "parallelism": (f"screen-tile shard x{world} + " + ("RCCL gather" if backend == "nccl" else "gloo gather (rehearsal)"))
+            if world > 1 else "single GPU",
             "rays_per_frame": rays / frames,
         },
         "roofline": {
