@@ -800,6 +800,8 @@ void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStre
 // ray reordering (tuning key 4, off by default).  Measured on C4: closest-hit traversal of
 // levels 2-6 drops 10 % (9.5 -> 8.5 ms) with the full 30-bit key, but the radix sort of each
 // level costs ~0.9 ms, more than it saves; octant-only or coarse keys save under 0.4 ms.
+// Keying by the origin's primitive (BVH order) instead of the Morton code gains the same;
+// with only its top 10 bits (a counting sort's budget) the gain falls to 0.65 ms.
 __device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 9 bits -> every third bit
     v &= 0x1FFu;
     v = (v | (v << 16)) & 0x030000FFu;
