@@ -93,6 +93,7 @@ typedef struct mrt_frame_stats {
     uint64_t levelShadowRays[16]; /* shadow rays built at depth 1..16 */
     double levelTraceMs[16];      /* profiling: closest-hit trace time per depth */
     double levelShadowMs[16];     /* profiling: any-hit trace time per depth */
+    uint64_t maxNodeRecordsPerRay; /* counting pass only: most node records one ray fetched */
 } mrt_frame_stats;
 
 const char *mrt_last_error(void);

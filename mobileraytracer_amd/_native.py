@@ -50,6 +50,7 @@ class MrtFrameStats(ctypes.Structure):
         ("shadeMs", ctypes.c_double),
         ("levelRays", ctypes.c_uint64 * 16), ("levelShadowRays", ctypes.c_uint64 * 16),
         ("levelTraceMs", ctypes.c_double * 16), ("levelShadowMs", ctypes.c_double * 16),
+        ("maxNodeRecordsPerRay", ctypes.c_uint64),
     ]
 
 

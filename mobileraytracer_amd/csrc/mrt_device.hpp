@@ -227,6 +227,8 @@ __device__ __forceinline__ bool leafSpheres(const DScene& s, int first, int coun
 struct TravCount {
     uint32_t nodes;  // child records fetched (2 per inner visit)
     uint32_t tris;   // triangle tests
+    uint32_t rayStart = 0;  // nodes at the current ray's fetch (per-ray maximum, counting builds)
+    uint32_t rayMax = 0;
 };
 
 // Generic BVH walk.  kKind selects the leaf routine.  Returns true on an any-hit.

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
             atomicAdd(stats + kStatNodes, n);
             atomicAdd(stats + kStatTris, t);
         }
+        atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
     }
 }
 

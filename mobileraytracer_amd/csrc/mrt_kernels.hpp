@@ -39,7 +39,8 @@ constexpr int kStatNodesShadow = 6; // any-hit kernel: child node records fetche
 constexpr int kStatTrisShadow = 7;  // any-hit kernel: triangle tests (counting pass only)
 constexpr int kStatLevelRays = 8;                     // + level - 1: rays of each level
 constexpr int kStatLevelShadows = 8 + kMaxLevels;     // + level - 1: shadow rays of each level
-constexpr int kNumStats = 8 + 2 * kMaxLevels;
+constexpr int kStatMaxNodesRay = 8 + 2 * kMaxLevels;  // counting builds: most node records of one ray
+constexpr int kNumStats = kStatMaxNodesRay + 1;
 
 // One level of the wavefront (SoA queues).
 struct Level {

@@ -534,6 +534,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->triTests += hs[kStatTris];
     fs->shadowNodeRecords += hs[kStatNodesShadow];
     fs->shadowTriTests += hs[kStatTrisShadow];
+    fs->maxNodeRecordsPerRay = std::max<uint64_t>(fs->maxNodeRecordsPerRay, hs[kStatMaxNodesRay]);
     for (int l = 0; l < kMaxLevels; ++l) {
         fs->levelRays[l] += hs[kStatLevelRays + l];
         fs->levelShadowRays[l] += hs[kStatLevelShadows + l];
@@ -608,6 +609,7 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs.triTests += prev.triTests;
                     fs.shadowNodeRecords += prev.shadowNodeRecords;
                     fs.shadowTriTests += prev.shadowTriTests;
+                    fs.maxNodeRecordsPerRay = std::max(fs.maxNodeRecordsPerRay, prev.maxNodeRecordsPerRay);
                     fs.traceMs += prev.traceMs;
                     fs.shadowMs += prev.shadowMs;
                     fs.shadeMs += prev.shadeMs;

@@ -170,6 +170,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
     while (true) {
         // ---- lanes whose triangle walk is over: lights (closest only), write the result ----
         if (rayIdx >= 0 && ref == kRefDone && leaf >= 0) {
+            if (kCount) cnt->rayMax = max(cnt->rayMax, cnt->nodes - cnt->rayStart);
             if (kAny) {
                 out[rayIdx].w = 0.0F;
             } else {
@@ -221,11 +222,27 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 while (pending != 0 && segsLeft > 0) {
                     const int n = __popcll(pending);
                     const int leader = __ffsll(static_cast<unsigned long long>(pending)) - 1;
+                    const int segStart = static_cast<int>((static_cast<long long>(count) * seg) / kShards);
+                    const int segEnd = static_cast<int>((static_cast<long long>(count) * (seg + 1)) / kShards);
+                    // once its own range is drained, a wave probes the others with a plain load
+                    // before any atomic: at the end of a level every wave of the grid walks the
+                    // ranges, and same-address atomics serialise.  The cursor only grows, so a
+                    // stale value under-reports.
+                    if (segsLeft < kShards) {
+                        int seen = 0;
+                        if (lane == leader)
+                            seen = __hip_atomic_load(fetch + seg * kFetchStride, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                        seen = __shfl(seen, leader, 64);
+                        if (segStart + seen >= segEnd) {
+                            seg = (seg + 1) % kShards;
+                            --segsLeft;
+                            continue;
+                        }
+                    }
                     int base = 0;
                     if (lane == leader) base = atomicAdd(fetch + seg * kFetchStride, n);
                     base = __shfl(base, leader, 64);
-                    const int segStart = static_cast<int>((static_cast<long long>(count) * seg) / kShards);
-                    const int segEnd = static_cast<int>((static_cast<long long>(count) * (seg + 1)) / kShards);
                     const bool mine = ((pending >> lane) & 1ull) != 0;
                     if (mine) {
                         const int idx = segStart + base + lanesBelowIn(pending);
@@ -240,6 +257,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             }
             if (need) {
                 rayIdx = (got >= 0 && order != nullptr) ? order[got] : got;
+                if (kCount) cnt->rayStart = cnt->nodes;
                 if (rayIdx < 0) {
                     exhausted = true;
                 } else {

@@ -11,20 +11,23 @@ def main():
     o, l, c = scenes.conference()
     w, h = int(os.environ.get("W", 1920)), int(os.environ.get("H", 1080))
     cfg = m.Config(width=w, height=h, shader=2, sceneIndex=-1, samplesPixel=int(os.environ.get("SPP", 4)),
-                   maxDepth=5, objFilePath=o, mtlFilePath=l, camFilePath=c)
+                   maxDepth=5, objFilePath=o, mtlFilePath=l, camFilePath=c,
+                   rankIndex=0, rankCount=int(os.environ.get("RANKS", 1)))
     r = m.Renderer(cfg)
     if "VARIANT" in os.environ:
         r.set_tuning(1, int(os.environ["VARIANT"]))
     if "SORT" in os.environ:
         r.set_tuning(4, int(os.environ["SORT"]))
-    d = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    d = torch.zeros(max(w * h, r.scene_info()["pixelSlotsMax"]), dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
     r.set_profiling(timing=True)
-    r.render_frame_device(d.data_ptr(), 0, sh)
+    ranks = int(os.environ.get("RANKS", 1))
+    bm, pk = (d.data_ptr(), 0) if ranks == 1 else (0, d.data_ptr())
+    r.render_frame_device(bm, pk, sh)
     acc = None
     n = 5
     for _ in range(n):
-        r.render_frame_device(d.data_ptr(), 0, sh)
+        r.render_frame_device(bm, pk, sh)
         st = r.frame_stats()
         cur = np.array([st["levelTraceMs"], st["levelShadowMs"]])
         acc = cur if acc is None else acc + cur
