@@ -108,22 +108,6 @@ struct mrt_renderer {
 
     // queues
     DeviceMem sceneMem, queueMem, frameMem;  // frameMem: bitmaps, kept when the queues are resized
-    mrt::Level levels[mrt::kMaxLevels]{};
-    int chunkSlots = 0;
-    int* counters = nullptr;
-    unsigned long long* stats = nullptr;
-    int2* gstack = nullptr;        // spill stacks of the closest-hit kernel ...
-    int2* gstackShadow = nullptr;  // ... and of the any-hit kernel (the two can run together)
-    int gdepth = 0;
-    int traceThreads = 0, workGrid = 0;  // traceThreads: resident trace threads, whole device
-    int32_t* dBitmap = nullptr;  // for the host-bitmap entry point
-    int32_t* dBackup = nullptr;  // progressive mode: the running average before the current pass
-    size_t backupN = 0;
-    hipStream_t stream = nullptr;
-    hipStream_t shadowStream = nullptr;  // any-hit launches, overlapped with the next level
-    std::vector<hipEvent_t> syncPool;    // ordering events between the two streams
-    int overlap = 1;                     // tuning key 3: shadow rays on their own stream
-    int sortRays = 0;                    // tuning key 4: reorder rays before tracing (1 closest-hit, 2 shadow)
     struct SortBufs {
         uint32_t* keys = nullptr;
         uint32_t* keysAlt = nullptr;
@@ -132,7 +116,35 @@ struct mrt_renderer {
         void* temp = nullptr;
         size_t tempBytes = 0;
         int cap = 0;
-    } sortRay, sortShadow;
+    };
+    // A pipeline renders chunks of pixel slots on its own pair of streams with its own queues.
+    // Chunks of different pipelines run concurrently, so one chunk's level-to-level drains
+    // (every level waits for its slowest ray) are filled by another chunk's work.
+    struct Pipe {
+        mrt::Level levels[mrt::kMaxLevels]{};
+        int* counters = nullptr;
+        unsigned long long* stats = nullptr;
+        int2* gstack = nullptr;        // spill stacks of the closest-hit kernel ...
+        int2* gstackShadow = nullptr;  // ... and of the any-hit kernel (the two can run together)
+        SortBufs sortRay, sortShadow;
+        hipStream_t stream = nullptr;        // raygen, closest-hit, shade, resolve, accumulate
+        hipStream_t shadowStream = nullptr;  // any-hit launches, overlapped with the next level
+        std::vector<hipEvent_t> syncPool;    // ordering events between the streams
+        std::vector<hipEvent_t> evPool;      // profiling: 5 timing events per level and chunk
+        size_t evCount = 0;
+    };
+    std::vector<Pipe> pipes;
+    int nPipes = 1;                      // tuning key 5 (more pipelines measured slower)
+    int chunkSlots = 0;
+    int gdepth = 0;
+    int traceThreads = 0, workGrid = 0;  // traceThreads: resident trace threads, whole device
+    int32_t* dBitmap = nullptr;  // for the host-bitmap entry point
+    int32_t* dBackup = nullptr;  // progressive mode: the running average before the current pass
+    size_t backupN = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t forkEvent = nullptr;
+    int overlap = 1;                     // tuning key 3: shadow rays on their own stream
+    int sortRays = 0;                    // tuning key 4: reorder rays before tracing (1 closest-hit, 2 shadow)
 
     // state (Renderer.hpp:30-40)
     std::atomic<bool> stopFlag{false};
@@ -140,13 +152,16 @@ struct mrt_renderer {
     std::atomic<uint64_t> totalRays{0};
     int profileFlags = 0;
     mrt_frame_stats last{};
-    std::vector<hipEvent_t> evPool;
 
     ~mrt_renderer() {
-        for (hipEvent_t e : evPool) (void)hipEventDestroy(e);
-        for (hipEvent_t e : syncPool) (void)hipEventDestroy(e);
+        for (Pipe& p : pipes) {
+            for (hipEvent_t e : p.evPool) (void)hipEventDestroy(e);
+            for (hipEvent_t e : p.syncPool) (void)hipEventDestroy(e);
+            if (p.stream != nullptr) (void)hipStreamDestroy(p.stream);
+            if (p.shadowStream != nullptr) (void)hipStreamDestroy(p.shadowStream);
+        }
+        if (forkEvent != nullptr) (void)hipEventDestroy(forkEvent);
         if (stream != nullptr) (void)hipStreamDestroy(stream);
-        if (shadowStream != nullptr) (void)hipStreamDestroy(shadowStream);
     }
 };
 
@@ -340,89 +355,121 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     const size_t n1 = static_cast<size_t>(chunkSlots) * static_cast<size_t>(spp);
     const size_t capN = n1 * static_cast<size_t>(growth);
     const int nLevels = r->nLevels;
-    // ping-pong ray / hit buffers (dead after k_shade of their level)
-    float4* rO[2];
-    float4* rD[2];
-    uint32_t* tree[2];
-    float4* hit[2];
-    for (int k = 0; k < 2; ++k) {
-        rO[k] = r->queueMem.alloc<float4>(capN);
-        rD[k] = r->queueMem.alloc<float4>(capN);
-        tree[k] = r->queueMem.alloc<uint32_t>(capN);
-        hit[k] = r->queueMem.alloc<float4>(capN);
-    }
-    // shadow rays: ping-pong too, so k_shade of level L+1 can run while the any-hit kernel
-    // of level L still reads its rays
-    float4* sO[2];
-    float4* sD[2];
-    for (int k = 0; k < 2; ++k) {
-        sO[k] = r->queueMem.alloc<float4>(capN * spl);
-        sD[k] = r->queueMem.alloc<float4>(capN * spl);
-    }
-    for (int l = 1; l <= nLevels + 1 && l < kMaxLevels; ++l) {
-        Level& lv = r->levels[l];
-        const size_t cap = (l == 1) ? n1 : capN;
-        const bool real = l <= nLevels;
-        lv.cap = real ? static_cast<int>(cap) : 0;
-        lv.shadowCap = real ? static_cast<int>(cap * spl) : 0;
-        lv.rO = rO[l & 1];
-        lv.rD = rD[l & 1];
-        lv.tree = tree[l & 1];
-        lv.hit = hit[l & 1];
-        lv.sO = sO[l & 1];
-        lv.sD = sD[l & 1];
-        if (real) {
-            lv.vtxA = r->queueMem.alloc<int4>(cap);
-            lv.vtxB = r->queueMem.alloc<int4>(cap);
-            lv.res = r->queueMem.alloc<float4>(cap);
-            lv.sC = r->queueMem.alloc<float4>(cap * spl);
-        } else {
-            lv.vtxA = nullptr;
-            lv.vtxB = nullptr;
-            lv.res = nullptr;
-            lv.sC = nullptr;
-        }
-    }
-    auto sortBufs = [&](mrt_renderer::SortBufs* b, size_t cap) {
-        b->cap = static_cast<int>(cap);
-        b->keys = r->queueMem.alloc<uint32_t>(cap);
-        b->keysAlt = r->queueMem.alloc<uint32_t>(cap);
-        b->vals = r->queueMem.alloc<int>(cap);
-        b->order = r->queueMem.alloc<int>(cap);
-        b->tempBytes = sortRaysTempBytes(b->cap);
-        b->temp = r->queueMem.alloc<uint8_t>(b->tempBytes);
-    };
-    sortBufs(&r->sortRay, capN);
-    sortBufs(&r->sortShadow, capN * spl);
-    r->counters = r->queueMem.alloc<int>(kNumCounters);
-    r->stats = r->queueMem.alloc<unsigned long long>(kNumStats);
     r->gdepth = std::max(1, r->stackNeed - kLdsStackMin);
-    r->gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
-    r->gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
+    const size_t nChunks = (static_cast<size_t>(r->nSlots) + chunkSlots - 1) / static_cast<size_t>(chunkSlots);
+    const size_t nPipes = std::max<size_t>(1, std::min<size_t>(static_cast<size_t>(r->nPipes), nChunks));
+    while (r->pipes.size() < nPipes) {
+        r->pipes.emplace_back();
+        if (r->pipes.size() > 1) MRT_HIP(hipStreamCreateWithFlags(&r->pipes.back().stream, hipStreamNonBlocking));
+        MRT_HIP(hipStreamCreateWithFlags(&r->pipes.back().shadowStream, hipStreamNonBlocking));
+    }
+    for (size_t pi = 0; pi < r->pipes.size(); ++pi) {
+        mrt_renderer::Pipe& pp = r->pipes[pi];
+        if (pi >= nPipes) {  // idle pipeline: no queues
+            for (Level& lv : pp.levels) lv = Level{};
+            pp.counters = nullptr;
+            continue;
+        }
+        // ping-pong ray / hit buffers (dead after k_shade of their level)
+        float4* rO[2];
+        float4* rD[2];
+        uint32_t* tree[2];
+        float4* hit[2];
+        for (int k = 0; k < 2; ++k) {
+            rO[k] = r->queueMem.alloc<float4>(capN);
+            rD[k] = r->queueMem.alloc<float4>(capN);
+            tree[k] = r->queueMem.alloc<uint32_t>(capN);
+            hit[k] = r->queueMem.alloc<float4>(capN);
+        }
+        // shadow rays: ping-pong too, so k_shade of level L+1 can run while the any-hit
+        // kernel of level L still reads its rays
+        float4* sO[2];
+        float4* sD[2];
+        for (int k = 0; k < 2; ++k) {
+            sO[k] = r->queueMem.alloc<float4>(capN * spl);
+            sD[k] = r->queueMem.alloc<float4>(capN * spl);
+        }
+        for (int l = 1; l <= nLevels + 1 && l < kMaxLevels; ++l) {
+            Level& lv = pp.levels[l];
+            const size_t cap = (l == 1) ? n1 : capN;
+            const bool real = l <= nLevels;
+            lv.cap = real ? static_cast<int>(cap) : 0;
+            lv.shadowCap = real ? static_cast<int>(cap * spl) : 0;
+            lv.rO = rO[l & 1];
+            lv.rD = rD[l & 1];
+            lv.tree = tree[l & 1];
+            lv.hit = hit[l & 1];
+            lv.sO = sO[l & 1];
+            lv.sD = sD[l & 1];
+            lv.order = nullptr;
+            lv.shadowOrder = nullptr;
+            if (real) {
+                lv.vtxA = r->queueMem.alloc<int4>(cap);
+                lv.vtxB = r->queueMem.alloc<int4>(cap);
+                lv.res = r->queueMem.alloc<float4>(cap);
+                lv.sC = r->queueMem.alloc<float4>(cap * spl);
+            } else {
+                lv.vtxA = nullptr;
+                lv.vtxB = nullptr;
+                lv.res = nullptr;
+                lv.sC = nullptr;
+            }
+        }
+        auto sortBufs = [&](mrt_renderer::SortBufs* b, size_t cap) {
+            b->cap = static_cast<int>(cap);
+            b->keys = r->queueMem.alloc<uint32_t>(cap);
+            b->keysAlt = r->queueMem.alloc<uint32_t>(cap);
+            b->vals = r->queueMem.alloc<int>(cap);
+            b->order = r->queueMem.alloc<int>(cap);
+            b->tempBytes = sortRaysTempBytes(b->cap);
+            b->temp = r->queueMem.alloc<uint8_t>(b->tempBytes);
+        };
+        sortBufs(&pp.sortRay, capN);
+        sortBufs(&pp.sortShadow, capN * spl);
+        pp.counters = r->queueMem.alloc<int>(kNumCounters);
+        pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats);
+        pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
+        pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
+    }
 }
 
-hipEvent_t syncEvent(mrt_renderer* r, size_t i) {
-    while (r->syncPool.size() <= i) {
+// Chunk size for a target pipeline count: every pipeline gets work, within the path budget.
+int chunkFor(const mrt_renderer* r, int nPipes) {
+    const size_t spp = static_cast<size_t>(std::max(1, r->cfg.samplesPixel));
+    const size_t maxPaths = r->cfg.maxPathsPerPass > 0 ? static_cast<size_t>(r->cfg.maxPathsPerPass) : (size_t{1} << 24);
+    const size_t nSlots = static_cast<size_t>(r->nSlots);
+    const size_t perPipe = (nSlots + static_cast<size_t>(nPipes) - 1) / static_cast<size_t>(std::max(1, nPipes));
+    return static_cast<int>(std::max<size_t>(1, std::min(perPipe, maxPaths / spp)));
+}
+
+hipEvent_t syncEvent(mrt_renderer::Pipe& p, size_t i) {
+    while (p.syncPool.size() <= i) {
         hipEvent_t e;
         MRT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        r->syncPool.push_back(e);
+        p.syncPool.push_back(e);
     }
-    return r->syncPool[i];
+    return p.syncPool[i];
 }
 
-hipEvent_t poolEvent(mrt_renderer* r, size_t i) {
-    while (r->evPool.size() <= i) {
+hipEvent_t poolEvent(mrt_renderer::Pipe& p) {
+    const size_t i = p.evCount++;
+    while (p.evPool.size() <= i) {
         hipEvent_t e;
         MRT_HIP(hipEventCreate(&e));
-        r->evPool.push_back(e);
+        p.evPool.push_back(e);
     }
-    return r->evPool[i];
+    return p.evPool[i];
 }
 
 // One pass over this shard's pixel slots: samples [sampleBase, sampleBase + spp).
 // Returns false if the queues overflowed (caller grows them and re-renders).
-bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp,
-                size_t* evCount) {
+int activePipes(const mrt_renderer* r) {
+    int n = 0;
+    while (n < static_cast<int>(r->pipes.size()) && r->pipes[static_cast<size_t>(n)].counters != nullptr) ++n;
+    return n;
+}
+
+bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp) {
     using namespace mrt;
     const int shader = r->shader;
     const bool timing = (r->profileFlags & 1) != 0;
@@ -430,10 +477,28 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     ShadeArgs sa{r->maxDepth, std::max(1, r->cfg.samplesLight), {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z}};
     const int nLevels = r->nLevels;
     const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
-    for (int slot0 = 0; slot0 < r->nSlots; slot0 += r->chunkSlots) {
-        if (r->stopFlag.load()) return true;
+    // fork: every pipeline starts after the work already queued on st
+    // Pipeline 0 runs on the caller's stream st (each extra stream costs a hardware queue:
+    // GPU_MAX_HW_QUEUES is 4, and two streams sharing one serialise); pipelines 1.. fork
+    // from st and join back.
+    const int nPipes = activePipes(r);
+    auto mainStream = [&](int pi) { return pi == 0 ? st : r->pipes[static_cast<size_t>(pi)].stream; };
+    if (nPipes > 1) {
+        if (r->forkEvent == nullptr) MRT_HIP(hipEventCreateWithFlags(&r->forkEvent, hipEventDisableTiming));
+        MRT_HIP(hipEventRecord(r->forkEvent, st));
+    }
+    for (int pi = 0; pi < nPipes; ++pi) {
+        mrt_renderer::Pipe& pp = r->pipes[static_cast<size_t>(pi)];
+        if (pi > 0) MRT_HIP(hipStreamWaitEvent(pp.stream, r->forkEvent, 0));
+        MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * kNumStats, mainStream(pi)));
+        pp.evCount = 0;
+    }
+    int chunk = 0;
+    for (int slot0 = 0; slot0 < r->nSlots && !r->stopFlag.load(); slot0 += r->chunkSlots, ++chunk) {
+        mrt_renderer::Pipe& pp = r->pipes[static_cast<size_t>(chunk % nPipes)];
+        const hipStream_t ps = mainStream(chunk % nPipes);
         const int nChunk = std::min(r->chunkSlots, r->nSlots - slot0);
-        MRT_HIP(hipMemsetAsync(r->counters, 0, sizeof(int) * kNumCounters, st));
+        MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, ps));
         RaygenArgs ra{};
         ra.cam = r->cam;
         ra.map = map;
@@ -445,60 +510,60 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.spp = spp;
         ra.sppTotal = r->cfg.samplesPixel;
         ra.sampleBase = sampleBase;
-        launchRaygen(ra, r->levels[1], r->counters, st);
+        launchRaygen(ra, pp.levels[1], pp.counters, ps);
         // Any-hit (shadow) rays of level L run on a second stream, overlapped with the
         // closest-hit trace and shading of level L+1: the persistent kernels' drain phases fill
         // each other.  Orders: shade(L) -> shadow(L); shadow(L) -> shade(L+2) (the shadow ray
         // buffers alternate by level); every shadow(L) -> resolve.
-        hipStream_t sb = r->overlap ? r->shadowStream : st;
+        hipStream_t sb = r->overlap ? pp.shadowStream : ps;
         size_t sync = 0;
         hipEvent_t shadowDone[kMaxLevels] = {};
-        if (sb != st) {
-            const hipEvent_t start = syncEvent(r, sync++);
-            MRT_HIP(hipEventRecord(start, st));
+        if (sb != ps) {
+            const hipEvent_t start = syncEvent(pp, sync++);
+            MRT_HIP(hipEventRecord(start, ps));
             MRT_HIP(hipStreamWaitEvent(sb, start, 0));
         }
         for (int l = 1; l <= nLevels; ++l) {
-            Level& lv = r->levels[l];
+            Level& lv = pp.levels[l];
             lv.order = nullptr;
             lv.shadowOrder = nullptr;
             if ((r->sortRays & 1) != 0 && l >= 2) {
-                const auto& b = r->sortRay;
-                sortRays(lv.rO, lv.rD, r->counters + cntRays(l), std::min(lv.cap, b.cap), r->ds.triRoot, b.keys,
-                         b.keysAlt, b.vals, b.order, b.temp, b.tempBytes, st);
+                const auto& b = pp.sortRay;
+                sortRays(lv.rO, lv.rD, pp.counters + cntRays(l), std::min(lv.cap, b.cap), r->ds.triRoot, b.keys,
+                         b.keysAlt, b.vals, b.order, b.temp, b.tempBytes, ps);
                 lv.order = b.order;
             }
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
-            launchTrace(r->ds, r->levels[l], r->counters, l, r->gstack, r->gdepth, r->stats, counting, r->traceThreads, st);
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
-            if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
-            launchShade(shader, r->ds, r->levels[l], r->levels[l + 1], r->counters, l, sa, r->workGrid, st);
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), st));
-            if (sb != st) {
-                const hipEvent_t shaded = syncEvent(r, sync++);
-                MRT_HIP(hipEventRecord(shaded, st));
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
+            launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, ps);
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
+            if (sb != ps && l >= 3) MRT_HIP(hipStreamWaitEvent(ps, shadowDone[l - 2], 0));
+            launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
+            if (sb != ps) {
+                const hipEvent_t shaded = syncEvent(pp, sync++);
+                MRT_HIP(hipEventRecord(shaded, ps));
                 MRT_HIP(hipStreamWaitEvent(sb, shaded, 0));
             }
             if (l < nLevels && (r->sortRays & 2) != 0) {
-                const auto& b = r->sortShadow;
-                sortRays(lv.sO, lv.sD, r->counters + cntShadows(l), std::min(lv.shadowCap, b.cap), r->ds.triRoot, b.keys,
+                const auto& b = pp.sortShadow;
+                sortRays(lv.sO, lv.sD, pp.counters + cntShadows(l), std::min(lv.shadowCap, b.cap), r->ds.triRoot, b.keys,
                          b.keysAlt, b.vals, b.order, b.temp, b.tempBytes, sb);
                 lv.shadowOrder = b.order;
             }
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), sb));
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
             if (l < nLevels) {  // the last level (depth > RayDepthMax) shades nothing: no shadow rays
-                launchShadow(r->ds, r->levels[l], r->counters, l, r->gstackShadow, r->gdepth, r->stats, counting,
+                launchShadow(r->ds, pp.levels[l], pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
                              r->traceThreads, sb);
             }
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(r, (*evCount)++), sb));
-            if (sb != st) {
-                shadowDone[l] = syncEvent(r, sync++);
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
+            if (sb != ps) {
+                shadowDone[l] = syncEvent(pp, sync++);
                 MRT_HIP(hipEventRecord(shadowDone[l], sb));
             }
         }
-        if (sb != st) MRT_HIP(hipStreamWaitEvent(st, shadowDone[nLevels], 0));
+        if (sb != ps) MRT_HIP(hipStreamWaitEvent(ps, shadowDone[nLevels], 0));
         for (int l = nLevels; l >= 1; --l) {
-            launchResolve(shader, r->ds, r->levels[l], r->levels[l + 1], r->counters, l, sa, r->workGrid, st);
+            launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
         }
         AccumArgs aa{};
         aa.map = map;
@@ -507,8 +572,15 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         aa.nSlots = nChunk;
         aa.spp = spp;
         aa.sampleBase = sampleBase;
-        launchAccumulate(aa, r->levels[1].res, dBitmap, dPacked, st);
-        launchTally(r->counters, nLevels, r->stats, st);
+        launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, ps);
+        launchTally(pp.counters, nLevels, pp.stats, ps);
+    }
+    // join: st continues after every pipeline
+    for (int pi = 1; pi < nPipes; ++pi) {
+        mrt_renderer::Pipe& pp = r->pipes[static_cast<size_t>(pi)];
+        const hipEvent_t done = syncEvent(pp, 4 * kMaxLevels);
+        MRT_HIP(hipEventRecord(done, pp.stream));
+        MRT_HIP(hipStreamWaitEvent(st, done, 0));
     }
     return true;
 }
@@ -518,14 +590,20 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
 bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp,
              mrt_frame_stats* fs) {
     using namespace mrt;
-    MRT_HIP(hipMemsetAsync(r->stats, 0, sizeof(unsigned long long) * kNumStats, st));
-    size_t evCount = 0;
     const auto t0 = std::chrono::steady_clock::now();
-    renderPass(r, dBitmap, dPacked, st, sampleBase, spp, &evCount);
-    unsigned long long hs[kNumStats];
-    MRT_HIP(hipMemcpyAsync(hs, r->stats, sizeof(hs), hipMemcpyDeviceToHost, st));
+    renderPass(r, dBitmap, dPacked, st, sampleBase, spp);
+    const int nPipes = activePipes(r);
+    std::vector<unsigned long long> all(static_cast<size_t>(nPipes) * kNumStats);
+    for (int pi = 0; pi < nPipes; ++pi)
+        MRT_HIP(hipMemcpyAsync(all.data() + static_cast<size_t>(pi) * kNumStats, r->pipes[static_cast<size_t>(pi)].stats,
+                               sizeof(unsigned long long) * kNumStats, hipMemcpyDeviceToHost, st));
     MRT_HIP(hipStreamSynchronize(st));
     const auto t1 = std::chrono::steady_clock::now();
+    unsigned long long hs[kNumStats] = {};
+    for (int pi = 0; pi < nPipes; ++pi) {
+        const unsigned long long* ps = all.data() + static_cast<size_t>(pi) * kNumStats;
+        for (int k = 0; k < kNumStats; ++k) hs[k] = (k == kStatMaxNodesRay) ? std::max(hs[k], ps[k]) : hs[k] + ps[k];
+    }
     if (hs[kStatOverflow] != 0) return false;
     fs->rays += hs[kStatRays];
     fs->shadowRays += hs[kStatShadowRays];
@@ -541,19 +619,22 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     }
     fs->frameMs += std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (r->profileFlags & 1) {
-        for (size_t e = 0; e + 4 < evCount; e += 5) {
-            float ta = 0.0F, tb = 0.0F, tc = 0.0F;
-            MRT_HIP(hipEventElapsedTime(&ta, r->evPool[e], r->evPool[e + 1]));
-            MRT_HIP(hipEventElapsedTime(&tc, r->evPool[e + 1], r->evPool[e + 2]));
-            MRT_HIP(hipEventElapsedTime(&tb, r->evPool[e + 3], r->evPool[e + 4]));
-            fs->traceMs += ta;
-            fs->shadeMs += tc;
-            fs->shadowMs += tb;
-            const size_t lvl = (e / 5) % static_cast<size_t>(r->nLevels);
-            fs->levelTraceMs[lvl] += ta;
-            fs->levelShadowMs[lvl] += tb;
-            fs->traceLaunches += 1;
-            fs->shadowLaunches += 1;
+        for (int pi = 0; pi < nPipes; ++pi) {
+            const mrt_renderer::Pipe& pp = r->pipes[static_cast<size_t>(pi)];
+            for (size_t e = 0; e + 4 < pp.evCount; e += 5) {
+                float ta = 0.0F, tb = 0.0F, tc = 0.0F;
+                MRT_HIP(hipEventElapsedTime(&ta, pp.evPool[e], pp.evPool[e + 1]));
+                MRT_HIP(hipEventElapsedTime(&tc, pp.evPool[e + 1], pp.evPool[e + 2]));
+                MRT_HIP(hipEventElapsedTime(&tb, pp.evPool[e + 3], pp.evPool[e + 4]));
+                fs->traceMs += ta;
+                fs->shadeMs += tc;
+                fs->shadowMs += tb;
+                const size_t lvl = (e / 5) % static_cast<size_t>(r->nLevels);
+                fs->levelTraceMs[lvl] += ta;
+                fs->levelShadowMs[lvl] += tb;
+                fs->traceLaunches += 1;
+                fs->shadowLaunches += 1;
+            }
         }
     }
     return true;
@@ -663,7 +744,6 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
     if (cfg->device >= 0) MRT_HIP(hipSetDevice(cfg->device));
     MRT_HIP(hipGetDevice(&r->device));
     MRT_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-    MRT_HIP(hipStreamCreateWithFlags(&r->shadowStream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     MRT_HIP(hipGetDeviceProperties(&prop, r->device));
     r->traceThreads = prop.multiProcessorCount * traceResidentThreadsPerCU();
@@ -684,10 +764,7 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
     }
     uploadScene(r.get(), sc);
     buildUnits(r.get());
-    const size_t spp = static_cast<size_t>(cfg->samplesPixel);
-    size_t maxPaths = cfg->maxPathsPerPass > 0 ? static_cast<size_t>(cfg->maxPathsPerPass) : (size_t{1} << 24);
-    size_t slots = std::max<size_t>(1, std::min<size_t>(static_cast<size_t>(r->nSlots), maxPaths / spp));
-    allocQueues(r.get(), static_cast<int>(slots), 2);
+    allocQueues(r.get(), chunkFor(r.get(), r->nPipes), 2);
     const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
     r->dBitmap = r->frameMem.alloc<int32_t>(npx);
     MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * npx, r->stream));
@@ -801,6 +878,13 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->sortRays = value;
         return 0;
     }
+    if (key == 5 && value >= 1 && value <= 8) {
+        return guarded([&] {
+            MRT_HIP(hipDeviceSynchronize());
+            r->nPipes = value;
+            allocQueues(r, chunkFor(r, value), 2);
+        });
+    }
     gLastError = "unknown tuning key/value";
     return -1;
 }
@@ -851,6 +935,10 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         *value = r->sortRays;
         return 0;
     }
+    if (key == 5) {
+        *value = r->nPipes;
+        return 0;
+    }
     gLastError = "unknown tuning key";
     return -1;
 }
@@ -872,7 +960,8 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
         }
         const auto& units = r->unitsByRank[static_cast<size_t>(r->rankIndex)];
         const auto& prefix = r->prefixByRank[static_cast<size_t>(r->rankIndex)];
-        const int cap = r->levels[1].cap;
+        mrt_renderer::Pipe& pp = r->pipes[0];
+        const int cap = pp.levels[1].cap;
         int32_t* dk = static_cast<int32_t*>(nullptr);
         int32_t* di = nullptr;
         float* dt = nullptr;
@@ -884,7 +973,7 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
         try {
             for (int slot0 = 0; slot0 < r->nSlots; slot0 += cap) {
                 const int n = std::min(cap, r->nSlots - slot0);
-                MRT_HIP(hipMemsetAsync(r->counters, 0, sizeof(int) * kNumCounters, st));
+                MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
                 RaygenArgs ra{};
                 ra.cam = r->cam;
                 ra.map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
@@ -896,9 +985,9 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
                 ra.spp = 1;
                 ra.sppTotal = r->cfg.samplesPixel;
                 ra.sampleBase = 0;
-                launchRaygen(ra, r->levels[1], r->counters, st);
-                launchTrace(r->ds, r->levels[1], r->counters, 1, r->gstack, r->gdepth, r->stats, false, r->traceThreads, st);
-                launchDumpHits(r->levels[1], n, dk, di, dt, st);
+                launchRaygen(ra, pp.levels[1], pp.counters, st);
+                launchTrace(r->ds, pp.levels[1], pp.counters, 1, pp.gstack, r->gdepth, pp.stats, false, r->traceThreads, st);
+                launchDumpHits(pp.levels[1], n, dk, di, dt, st);
                 MRT_HIP(hipMemcpyAsync(hk.data(), dk, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
                 MRT_HIP(hipMemcpyAsync(hi.data(), di, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
                 MRT_HIP(hipMemcpyAsync(ht.data(), dt, sizeof(float) * n, hipMemcpyDeviceToHost, st));

@@ -224,22 +224,6 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     const int leader = __ffsll(static_cast<unsigned long long>(pending)) - 1;
                     const int segStart = static_cast<int>((static_cast<long long>(count) * seg) / kShards);
                     const int segEnd = static_cast<int>((static_cast<long long>(count) * (seg + 1)) / kShards);
-                    // once its own range is drained, a wave probes the others with a plain load
-                    // before any atomic: at the end of a level every wave of the grid walks the
-                    // ranges, and same-address atomics serialise.  The cursor only grows, so a
-                    // stale value under-reports.
-                    if (segsLeft < kShards) {
-                        int seen = 0;
-                        if (lane == leader)
-                            seen = __hip_atomic_load(fetch + seg * kFetchStride, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                        seen = __shfl(seen, leader, 64);
-                        if (segStart + seen >= segEnd) {
-                            seg = (seg + 1) % kShards;
-                            --segsLeft;
-                            continue;
-                        }
-                    }
                     int base = 0;
                     if (lane == leader) base = atomicAdd(fetch + seg * kFetchStride, n);
                     base = __shfl(base, leader, 64);

@@ -261,16 +261,17 @@ def test_trace_kernel_variants_are_identical():
 
 
 def test_shadow_stream_overlap_is_invariant():
-    """Any-hit launches on their own stream (overlapping the next level) and ray reordering
-    before traversal change nothing."""
+    """Any-hit launches on their own stream (overlapping the next level), ray reordering before
+    traversal and concurrent chunk pipelines change nothing."""
     import mobileraytracer_amd as m
     for cfg in (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
                 make_cfg(64, 64, shader=1)):
         outs = []
         with m.Renderer(cfg) as r:
-            for ov, srt in ((0, 0), (1, 0), (0, 3), (1, 3), (1, 1), (1, 2)):
+            for ov, srt, pipes in ((0, 0, 1), (1, 0, 1), (0, 3, 2), (1, 3, 3), (1, 1, 2), (1, 2, 1), (1, 0, 4)):
                 r.set_tuning(3, ov)
                 r.set_tuning(4, srt)  # ray reordering before traversal
+                r.set_tuning(5, pipes)  # concurrent chunk pipelines
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
                 r.render_frame(bm)
                 st = r.frame_stats()

@@ -12,6 +12,8 @@ def frame_ms(n, w=1920, h=1080, spp=4, frames=10):
     cfg = m.Config(width=w, height=h, shader=2, sceneIndex=-1, samplesPixel=spp, maxDepth=5, objFilePath=o,
                    mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=n)
     with m.Renderer(cfg) as r:
+        if "PIPES" in os.environ:
+            r.set_tuning(5, int(os.environ["PIPES"]))
         packed = torch.zeros(r.scene_info()["pixelSlotsMax"], dtype=torch.int32, device="cuda")
         sh = torch.cuda.current_stream().cuda_stream
         for _ in range(3):
