@@ -7,13 +7,15 @@ import mobileraytracer_amd as m
 from mobileraytracer_amd import scenes
 
 
-def frame_ms(n, w=1920, h=1080, spp=4, frames=10):
+def frame_ms(n, w=1920, h=1080, spp=4, frames=10, rank=0):
     o, l, c = scenes.conference()
     cfg = m.Config(width=w, height=h, shader=2, sceneIndex=-1, samplesPixel=spp, maxDepth=5, objFilePath=o,
-                   mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=n)
+                   mtlFilePath=l, camFilePath=c, rankIndex=rank, rankCount=n)
     with m.Renderer(cfg) as r:
         if "PIPES" in os.environ:
             r.set_tuning(5, int(os.environ["PIPES"]))
+        if "OVERLAP" in os.environ:
+            r.set_tuning(3, int(os.environ["OVERLAP"]))
         packed = torch.zeros(r.scene_info()["pixelSlotsMax"], dtype=torch.int32, device="cuda")
         sh = torch.cuda.current_stream().cuda_stream
         for _ in range(3):
@@ -27,6 +29,12 @@ def frame_ms(n, w=1920, h=1080, spp=4, frames=10):
 
 
 def main():
+    if "ALLRANKS" in os.environ:
+        n = int(os.environ["ALLRANKS"])
+        ts = [frame_ms(n, rank=k, frames=5) for k in range(n)]
+        t1 = frame_ms(1, frames=5)
+        print(f"N={n} per-rank ms: " + " ".join(f"{t:.2f}" for t in ts) + f"  max {max(ts):.2f}  efficiency {t1 / (n * max(ts)):.3f}")
+        return
     w, h, spp = int(os.environ.get("W", 1920)), int(os.environ.get("H", 1080)), int(os.environ.get("SPP", 4))
     t1 = None
     for n in (1, 2, 4, 8):
