@@ -165,18 +165,18 @@ constexpr TraceCfgRow kTraceCfg[] = {
     {2, 1, kLdsStack, 1, 1, 0},   // 0  per-wave batches, if-if
     {2, 1, kLdsStack, 1, 1, 0},   // 1  while-while, per-lane refill
     {4, 1, kLdsStack, 1, 1, 0},   // 2  as 1, 4-wide BVH
-    {2, 16, kLdsStack, 1, 1, 0},  // 3
-    {2, 32, kLdsStack, 1, 1, 0},  // 4
-    {2, 16, 8, 1, 1, 0},          // 5
-    {4, 16, kLdsStack, 1, 1, 0},  // 6
+    {2, 32, 8, 8, 1, 0, 64, 1},   // 3  as 14 without the LDS top, one wave per workgroup
+    {2, 32, 8, 8, 1, 0, 128, 1},  // 4  as 3, two waves per workgroup
+    {2, 32, 8, 8, 1, 64, 128, 1}, // 5  as 4 with the top 64 nodes in LDS
+    {2, 32, 8, 8, 1, 128, 128, 1},// 6  as 4 with the top 128 nodes in LDS
     {2, 32, kLdsStack, 8, 1, 0},  // 7
-    {2, 32, 8, 8, 1, 0},          // 8  default
-    {2, 48, kLdsStack, 1, 1, 0},  // 9
+    {2, 32, 8, 8, 1, 0},          // 8
+    {2, 16, 8, 8, 1, 0, 64, 1},   // 9  as 3, refill at 16 idle lanes
     {2, 32, 8, 8, 8, 0},          // 10 as 8, compiled for 8 waves per SIMD
     {2, 32, 8, 32, 1, 0},         // 11 as 8, 32 cursors
     {2, 32, 8, 8, 1, 64},         // 12 as 8, top 64 nodes in LDS
     {2, 32, 8, 8, 1, 128},        // 13 as 8, top 128 nodes in LDS
-    {2, 32, 8, 8, 1, 128, 256, 1},  // 14 as 13, IEEE min/max slab test for finite 1/d
+    {2, 32, 8, 8, 1, 128, 256, 1},  // 14 as 13, IEEE min/max slab test for finite 1/d (default)
     {2, 32, 8, 8, 1, 256, 512},     // 15 as 13, top 256 nodes, 512-thread workgroups
 };
 constexpr int kNumTraceVariants = sizeof(kTraceCfg) / sizeof(kTraceCfg[0]);
