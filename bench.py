@@ -24,6 +24,7 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+BASELINE_METRIC = "Mrays/s + ms/frame, Conference OBJ 1920\u00d71080 4spp, 1/2/4/8 GPU"  # BASELINE.json "metric"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 PEAK_L2_GBS = 34500.0  # aggregate L2 (8 x 4 MiB) read rate, same guide, section "L2 (per XCD)"
 
@@ -178,7 +179,7 @@ def main():
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     traffic = pmc_traffic_per_launch() if world == 1 else None
     out = {
-        "metric": "Mrays/s (Conference 1920x1080 4spp PathTracer)",
+        "metric": BASELINE_METRIC,
         "value": rays / elapsed / 1e6,
         "unit": "Mrays/s",
         "n_gpus": world,
