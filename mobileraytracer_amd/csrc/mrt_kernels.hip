@@ -293,6 +293,53 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
     }
 }
 
+// Closest-hit rays of `level` and then, in the same launch, the shadow rays of level - 1:
+// one persistent drain per level instead of two (tuning key 3 = 2).  Workgroups switch to
+// the shadow queue as the closest-hit queue runs dry, so the shadow work fills the tail.
+template <bool kCount, int kVariant>
+__global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::kMinWaves) void k_combo(
+    DScene s, Level lv, Level prev, int* counters, int level, int2* gstack, int gdepth, unsigned long long* stats) {
+    using C = TraceCfg<kVariant>;
+    static_assert(kVariant > 0, "while-while variants only");
+    __shared__ int2 ldsStack[C::kStack * C::kThreads];
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * C::kThreads + threadIdx.x) * gdepth, 0,
+              C::kStack, C::kThreads};
+    __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
+    stageTop<C::kTop, C::kThreads>(s, ldsTop);
+    TravCount cnt{0u, 0u}, cntS{0u, 0u};
+    {
+        const int count = min(counters[cntRays(level)], lv.cap);
+        int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride
+                                    : counters + kCntFetchTrace + level;
+        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab>(
+            s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, lv.order);
+    }
+    if (level >= 2) {
+        const int pl = level - 1;
+        const int count = min(counters[cntShadows(pl)], prev.shadowCap);
+        int* fetch = C::kShards > 1 ? counters + kCntFetchShards + (kMaxLevels + pl) * kMaxFetchShards * kFetchStride
+                                    : counters + kCntFetchShadow + pl;
+        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab>(
+            s, prev.sO, prev.sD, prev.sC, count, fetch, st, &cntS, ldsTop, prev.shadowOrder);
+    }
+    if (kCount) {
+        unsigned long long n = cnt.nodes, t = cnt.tris, ns = cntS.nodes, ts = cntS.tris;
+        for (int off = 32; off > 0; off >>= 1) {
+            n += __shfl_down(n, off, 64);
+            t += __shfl_down(t, off, 64);
+            ns += __shfl_down(ns, off, 64);
+            ts += __shfl_down(ts, off, 64);
+        }
+        if (laneId() == 0) {
+            atomicAdd(stats + kStatNodes, n);
+            atomicAdd(stats + kStatTris, t);
+            atomicAdd(stats + kStatNodesShadow, ns);
+            atomicAdd(stats + kStatTrisShadow, ts);
+        }
+        atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 struct HitGeom {
     v3 P, N;
@@ -694,7 +741,7 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
 // the spill stacks were sized for.
 template <typename K>
 int persistentGrid(K kernel, int variant, int kind, int threads, int maxThreads) {
-    static int occ[2][kTraceVariants] = {};
+    static int occ[3][kTraceVariants] = {};  // kind: 0 closest, 1 shadow, 2 combined
     static int cus = 0;
     const int cap = std::max(1, maxThreads / threads);
     if (cus == 0) {
@@ -737,6 +784,41 @@ int persistentGrid(K kernel, int variant, int kind, int threads, int maxThreads)
         MRT_LAUNCH_ONE(KERNEL, KIND, 14)                                                                     \
         default: MRT_LAUNCH_ONE(KERNEL, KIND, 15)                                                            \
     }
+
+#define MRT_LAUNCH_COMBO_ONE(V)                                                                              \
+    case V: {                                                                                                \
+        constexpr int kT = TraceCfg<V>::kThreads;                                                            \
+        const int g = persistentGrid(k_combo<false, V>, V, 2, kT, maxThreads);                              \
+        if (countStats)                                                                                      \
+            hipLaunchKernelGGL((k_combo<true, V>), dim3(g), dim3(kT), 0, st, s, lv, prev, counters, level, gstack, gdepth, stats); \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_combo<false, V>), dim3(g), dim3(kT), 0, st, s, lv, prev, counters, level, gstack, gdepth, stats); \
+        break;                                                                                               \
+    }
+
+bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,
+                 int gdepth, unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
+    switch (s.variant) {
+        MRT_LAUNCH_COMBO_ONE(1)
+        MRT_LAUNCH_COMBO_ONE(2)
+        MRT_LAUNCH_COMBO_ONE(3)
+        MRT_LAUNCH_COMBO_ONE(4)
+        MRT_LAUNCH_COMBO_ONE(5)
+        MRT_LAUNCH_COMBO_ONE(6)
+        MRT_LAUNCH_COMBO_ONE(7)
+        MRT_LAUNCH_COMBO_ONE(8)
+        MRT_LAUNCH_COMBO_ONE(9)
+        MRT_LAUNCH_COMBO_ONE(10)
+        MRT_LAUNCH_COMBO_ONE(11)
+        MRT_LAUNCH_COMBO_ONE(12)
+        MRT_LAUNCH_COMBO_ONE(13)
+        MRT_LAUNCH_COMBO_ONE(14)
+        MRT_LAUNCH_COMBO_ONE(15)
+        default:
+            return false;  // variant 0 (per-wave batches): separate launches
+    }
+    return true;
+}
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {

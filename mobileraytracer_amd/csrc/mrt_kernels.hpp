@@ -101,6 +101,10 @@ struct AccumArgs {
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
+// closest-hit rays of `level` then shadow rays of level - 1 in one launch; false if the trace
+// variant has no such form (the caller then launches them separately)
+bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,
+                 int gdepth, unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,

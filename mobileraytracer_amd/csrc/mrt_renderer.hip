@@ -463,6 +463,8 @@ hipEvent_t poolEvent(mrt_renderer::Pipe& p) {
 
 // One pass over this shard's pixel slots: samples [sampleBase, sampleBase + spp).
 // Returns false if the queues overflowed (caller grows them and re-renders).
+bool s_comboCapable(int variant) { return variant > 0; }  // k_combo exists for while-while variants
+
 int activePipes(const mrt_renderer* r) {
     int n = 0;
     while (n < static_cast<int>(r->pipes.size()) && r->pipes[static_cast<size_t>(n)].counters != nullptr) ++n;
@@ -515,7 +517,8 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // closest-hit trace and shading of level L+1: the persistent kernels' drain phases fill
         // each other.  Orders: shade(L) -> shadow(L); shadow(L) -> shade(L+2) (the shadow ray
         // buffers alternate by level); every shadow(L) -> resolve.
-        hipStream_t sb = r->overlap ? pp.shadowStream : ps;
+        hipStream_t sb = r->overlap == 1 ? pp.shadowStream : ps;
+        const bool comboMode = r->overlap == 2 && s_comboCapable(r->ds.variant);
         size_t sync = 0;
         hipEvent_t shadowDone[kMaxLevels] = {};
         if (sb != ps) {
@@ -534,7 +537,13 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 lv.order = b.order;
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
-            launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, ps);
+            // overlap 2: this level's closest-hit rays and the previous level's shadow rays in
+            // one launch (the previous level's shadow launch below was skipped)
+            const bool combined =
+                r->overlap == 2 && launchCombo(r->ds, pp.levels[l], pp.levels[l - 1], pp.counters, l, pp.gstack, r->gdepth,
+                                               pp.stats, counting, r->traceThreads, ps);
+            if (!combined)
+                launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, ps);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
             if (sb != ps && l >= 3) MRT_HIP(hipStreamWaitEvent(ps, shadowDone[l - 2], 0));
             launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
@@ -551,7 +560,9 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 lv.shadowOrder = b.order;
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
-            if (l < nLevels) {  // the last level (depth > RayDepthMax) shades nothing: no shadow rays
+            // the last level (depth > RayDepthMax) shades nothing: no shadow rays; in combined
+            // mode the next level's launch takes them
+            if (l < nLevels && !comboMode) {
                 launchShadow(r->ds, pp.levels[l], pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
                              r->traceThreads, sb);
             }
@@ -870,7 +881,7 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.cull = value;
         return 0;
     }
-    if (key == 3 && (value == 0 || value == 1)) {
+    if (key == 3 && value >= 0 && value <= 2) {
         r->overlap = value;
         return 0;
     }

@@ -268,7 +268,8 @@ def test_shadow_stream_overlap_is_invariant():
                 make_cfg(64, 64, shader=1)):
         outs = []
         with m.Renderer(cfg) as r:
-            for ov, srt, pipes in ((0, 0, 1), (1, 0, 1), (0, 3, 2), (1, 3, 3), (1, 1, 2), (1, 2, 1), (1, 0, 4)):
+            for ov, srt, pipes in ((0, 0, 1), (1, 0, 1), (0, 3, 2), (1, 3, 3), (1, 1, 2), (1, 2, 1), (1, 0, 4),
+                                   (2, 0, 1), (2, 3, 2)):
                 r.set_tuning(3, ov)
                 r.set_tuning(4, srt)  # ray reordering before traversal
                 r.set_tuning(5, pipes)  # concurrent chunk pipelines
