@@ -507,7 +507,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
         if (!active) continue;
         if (terminal) {
             lv.res[i] = leaf;
-            lv.vtxA[i] = make_int4(-1, 0, 0, 0);
+            lv.vtx[i] = make_int4(-1, 0, 0, 0);
             continue;
         }
         // shadow rays (Whitted.cpp:53, PathTracer.cpp:67)
@@ -534,25 +534,24 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
                 }
             }
         }
-        // child rays: diffuse (PathTracer.cpp:90-91), specular (:118-120), transmission (:129-131)
-        int4 child = make_int4(-1, -1, -1, 0);
+        // child rays: diffuse (PathTracer.cpp:90-91), specular (:118-120), transmission (:129-131),
+        // stored consecutively from childBase
         int c = childBase;
-        auto emit = [&](v3 dir, uint32_t slot) -> int {
+        auto emit = [&](v3 dir, uint32_t slot) {
             const int j = c++;
             if (j >= nx.cap) {
-                atomicOr(counters + kCntOverflow, 1);
-                return -1;
+                atomicOr(counters + kCntOverflow, 1);  // the frame is redone in smaller passes
+                return;
             }
             nx.rO[j] = make_float4(g.P.x, g.P.y, g.P.z, bitsf(key));
             nx.rD[j] = make_float4(dir.x, dir.y, dir.z, bitsf(g.src));
             nx.tree[j] = tc * 4u + slot;
-            return j;
         };
-        if (wantD) child.x = emit(cosineHemisphere(g.N, hemi1, hemi2), 1u);
-        if (wantS) child.y = emit(reflect(d, g.N), 2u);
-        if (wantT) child.z = emit(refract(d, g.N, 1.0F / ior), 3u);
-        lv.vtxA[i] = make_int4(mat, shadowBase, nShadow, 0);
-        lv.vtxB[i] = child;
+        if (wantD) emit(cosineHemisphere(g.N, hemi1, hemi2), 1u);
+        if (wantS) emit(reflect(d, g.N), 2u);
+        if (wantT) emit(refract(d, g.N, 1.0F / ior), 3u);
+        const int mask = (wantD ? 1 : 0) | (wantS ? 2 : 0) | (wantT ? 4 : 0);
+        lv.vtx[i] = make_int4(mat, shadowBase, childBase, (nShadow << 3) | mask);
     }
 }
 
@@ -620,7 +619,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int
             }
         }
         lv.res[i] = make_float4(rgb.x, rgb.y, rgb.z, hitLight);
-        lv.vtxA[i] = make_int4(-1, 0, 0, 0);
+        lv.vtx[i] = make_int4(-1, 0, 0, 0);
     }
 }
 
@@ -630,15 +629,25 @@ __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, i
     const int count = min(counters[cntRays(level)], lv.cap);
     for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
          i += static_cast<int>(gridDim.x * blockDim.x)) {
-        const int4 va = lv.vtxA[i];
+        const int4 va = lv.vtx[i];
         if (va.x < 0) continue;  // terminal: res written by k_shade
-        const int4 vb = lv.vtxB[i];
+        // children (consecutive from va.z in the order diffuse, specular, transmission); an
+        // index past the queue only occurs in an overflowed pass, which is redone
+        int c = va.z;
+        int4 vb = make_int4(-1, -1, -1, 0);
+        if (va.w & 1) vb.x = c++;
+        if (va.w & 2) vb.y = c++;
+        if (va.w & 4) vb.z = c++;
+        if (vb.x >= nx.cap) vb.x = -1;
+        if (vb.y >= nx.cap) vb.y = -1;
+        if (vb.z >= nx.cap) vb.z = -1;
+        const int nShadow = va.w >> 3;
         const float4* m = s.mats + 4 * va.x;
         const v3 Kd = xyz(m[1]), Ks = xyz(m[2]), Kt = xyz(m[3]);
         const bool direct = hasPositive(Kd) && s.nLights > 0;
         v3 Ld{0.0F, 0.0F, 0.0F};
         if (direct) {
-            for (int k = 0; k < va.z; ++k) {
+            for (int k = 0; k < nShadow; ++k) {
                 const int j = va.y + k;
                 if (j >= lv.shadowCap) break;
                 const float4 c = lv.sC[j];

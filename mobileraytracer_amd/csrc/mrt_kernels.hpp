@@ -48,8 +48,9 @@ struct Level {
     float4* rD;      // direction xyz, w = source primitive code bits
     uint32_t* tree;  // vertex code in the ray tree
     float4* hit;     // t, u, v, hit primitive code bits
-    int4* vtxA;      // material (-1 terminal), first shadow ray, shadow ray count
-    int4* vtxB;      // child indices in the next level: diffuse, specular, transmission
+    int4* vtx;       // material (-1 terminal), first shadow ray, first child in the next level,
+                     // shadow ray count << 3 | children (1 diffuse, 2 specular, 4 transmission,
+                     // stored consecutively in that order)
     float4* res;     // resolved radiance xyz, w = "intersected light" flag
     float4* sO;      // shadow ray origin, w = source primitive bits
     float4* sD;      // shadow ray direction, w = distance to the light

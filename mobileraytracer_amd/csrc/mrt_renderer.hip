@@ -404,13 +404,11 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
             lv.order = nullptr;
             lv.shadowOrder = nullptr;
             if (real) {
-                lv.vtxA = r->queueMem.alloc<int4>(cap);
-                lv.vtxB = r->queueMem.alloc<int4>(cap);
+                lv.vtx = r->queueMem.alloc<int4>(cap);
                 lv.res = r->queueMem.alloc<float4>(cap);
                 lv.sC = r->queueMem.alloc<float4>(cap * spl);
             } else {
-                lv.vtxA = nullptr;
-                lv.vtxB = nullptr;
+                lv.vtx = nullptr;
                 lv.res = nullptr;
                 lv.sC = nullptr;
             }
