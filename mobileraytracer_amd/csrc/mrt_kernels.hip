@@ -417,6 +417,165 @@ __device__ __forceinline__ bool lightSample(const DScene& s, const HitGeom& g, f
     return true;
 }
 
+// One shading vertex (Whitted.cpp:13-93, PathTracer.cpp:22-142), split in two halves so the
+// caller can allocate queue slots for all lanes in between: shadePrepare reads the hit and
+// decides the shadow and child rays, shadeEmit writes them and the vertex record.
+struct ShadeState {
+    HitGeom g;
+    v3 d;
+    float ior;
+    int mat;
+    uint32_t key, tc;
+    bool terminal, direct, wantD, wantS, wantT, ok0;
+    float4 leaf;  // terminal: the vertex's final radiance (Le), w = hit-a-light flag
+    v3 ld0, lc0;  // light sample 0 (kept in registers)
+    float dist0, hemi1, hemi2;
+    int nShadow, nChild;
+};
+
+template <int kShader>
+__device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, float4 d4, float4 h, uint32_t tc,
+                                                   int level, const ShadeArgs& a) {
+    ShadeState v{};
+    v.terminal = true;
+    v.leaf = make_float4(0.0F, 0.0F, 0.0F, 0.0F);
+    v.ior = 1.0F;
+    v.mat = -1;
+    v.key = fbits(o4.w);
+    v.tc = tc;
+    v.d = xyz(d4);
+    // issue every table gather of this vertex at once: their latencies overlap
+    const float pick0 = s.tables[sampleIndex(v.key, tc, purposeLightPick(0))].x;
+    const float lr0 = s.tables[sampleIndex(v.key, tc, purposeLightR(0))].y;
+    const float lq0 = s.tables[sampleIndex(v.key, tc, purposeLightS(0))].y;
+    const float rr = s.tables[sampleIndex(v.key, tc, kPRussian)].y;
+    v.hemi1 = s.tables[sampleIndex(v.key, tc, kPHemi1)].x;
+    v.hemi2 = s.tables[sampleIndex(v.key, tc, kPHemi2)].x;
+    const uint32_t code = fbits(h.w);
+    const uint32_t kind = primKind(code);
+    // Shader.cpp:122: shade only if hit; Whitted.cpp:14-17 / PathTracer.cpp:25-28: depth cap
+    if (kind == kMiss || level > a.maxDepth) return v;
+    v3 Le, Kd{0, 0, 0}, Ks{0, 0, 0}, Kt{0, 0, 0};
+    if (kind == kLight) {
+        Le = xyz(s.lights[4 * primIndex(code) + 3]);
+    } else {
+        v.mat = hitMaterial(s, code);
+        const float4* m = s.mats + 4 * v.mat;
+        const float4 le4 = m[0];
+        Le = xyz(le4);
+        v.ior = le4.w;
+        Kd = xyz(m[1]);
+        Ks = xyz(m[2]);
+        Kt = xyz(m[3]);
+    }
+    if (hasPositive(Le)) {  // Whitted.cpp:19-24
+        v.leaf = make_float4(Le.x, Le.y, Le.z, 1.0F);
+        return v;
+    }
+    v.terminal = false;
+    v.g = hitGeometry(s, xyz(o4), v.d, h);
+    v.direct = hasPositive(Kd) && s.nLights > 0;
+    if (v.direct) {
+        v.ok0 = lightSample(s, v.g, pick0, lr0, lq0, &v.ld0, &v.dist0, &v.lc0);
+        v.nShadow = static_cast<int>(v.ok0);
+        for (int k = 1; k < a.samplesLight; ++k) {
+            v3 ld, lc;
+            float dist;
+            if (lightSample(s, v.g, s.tables[sampleIndex(v.key, tc, purposeLightPick(k))].x,
+                            s.tables[sampleIndex(v.key, tc, purposeLightR(k))].y,
+                            s.tables[sampleIndex(v.key, tc, purposeLightS(k))].y, &ld, &dist, &lc))
+                ++v.nShadow;
+        }
+    }
+    if (kShader == kShaderPathTracer && hasPositive(Kd)) {  // PathTracer.cpp:89
+        v.wantD = level <= kRayDepthMin || rr > 0.5F;
+    }
+    v.wantS = hasPositive(Ks);
+    v.wantT = hasPositive(Kt);
+    v.nChild = static_cast<int>(v.wantD) + static_cast<int>(v.wantS) + static_cast<int>(v.wantT);
+    return v;
+}
+
+// Payload stores: plain, or (kPublish) `sc1` buffer stores for rays that other waves of the
+// same launch will read (the hand-off protocol of the microarchitecture guide: sc1 stores,
+// the storing wave's vmcnt(0), then the ready flag).
+template <bool kPublish>
+__device__ __forceinline__ void storeF4(float4* base, int j, float4 v) {
+    if (kPublish) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                               __builtin_amdgcn_make_buffer_rsrc(base, static_cast<short>(0), 0x7FFFFFFF,
+                                                                                 0x00020000),
+                                               static_cast<uint32_t>(j) * 16u, 0, 16);
+    } else {
+        base[j] = v;
+    }
+}
+template <bool kPublish>
+__device__ __forceinline__ void storeU32(uint32_t* base, int j, uint32_t v) {
+    if (kPublish) {
+        __builtin_amdgcn_raw_buffer_store_b32(v, __builtin_amdgcn_make_buffer_rsrc(base, static_cast<short>(0), 0x7FFFFFFF,
+                                                                                  0x00020000),
+                                              static_cast<uint32_t>(j) * 4u, 0, 16);
+    } else {
+        base[j] = v;
+    }
+}
+
+// Writes vertex i's shadow rays (level lv, from shadowBase) and children (level nx, from
+// childBase) and its record.  Slots past a queue's capacity set the overflow flag (the frame is
+// then redone in smaller passes).
+template <bool kPublish>
+__device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, int i, const Level& lv, const Level& nx,
+                                          int shadowBase, int childBase, int* counters, const ShadeArgs& a) {
+    if (v.terminal) {
+        lv.res[i] = v.leaf;
+        lv.vtx[i] = make_int4(-1, 0, 0, 0);
+        return;
+    }
+    // shadow rays (Whitted.cpp:53, PathTracer.cpp:67)
+    int written = 0;
+    if (v.direct) {
+        for (int k = 0; k < a.samplesLight; ++k) {
+            v3 ld = v.ld0, lc = v.lc0;
+            float dist = v.dist0;
+            if (k == 0) {
+                if (!v.ok0) continue;
+            } else if (!lightSample(s, v.g, s.tables[sampleIndex(v.key, v.tc, purposeLightPick(k))].x,
+                                    s.tables[sampleIndex(v.key, v.tc, purposeLightR(k))].y,
+                                    s.tables[sampleIndex(v.key, v.tc, purposeLightS(k))].y, &ld, &dist, &lc)) {
+                continue;
+            }
+            const int j = shadowBase + written;
+            ++written;
+            if (j < lv.shadowCap) {
+                storeF4<kPublish>(lv.sO, j, make_float4(v.g.P.x, v.g.P.y, v.g.P.z, bitsf(v.g.src)));
+                storeF4<kPublish>(lv.sD, j, make_float4(ld.x, ld.y, ld.z, dist));
+                lv.sC[j] = make_float4(lc.x, lc.y, lc.z, 0.0F);
+            } else {
+                atomicOr(counters + kCntOverflow, 1);
+            }
+        }
+    }
+    // child rays: diffuse (PathTracer.cpp:90-91), specular (:118-120), transmission (:129-131),
+    // stored consecutively from childBase
+    int c = childBase;
+    auto emit = [&](v3 dir, uint32_t slot) {
+        const int j = c++;
+        if (j >= nx.cap) {
+            atomicOr(counters + kCntOverflow, 1);
+            return;
+        }
+        storeF4<kPublish>(nx.rO, j, make_float4(v.g.P.x, v.g.P.y, v.g.P.z, bitsf(v.key)));
+        storeF4<kPublish>(nx.rD, j, make_float4(dir.x, dir.y, dir.z, bitsf(v.g.src)));
+        storeU32<kPublish>(nx.tree, j, v.tc * 4u + slot);
+    };
+    if (v.wantD) emit(cosineHemisphere(v.g.N, v.hemi1, v.hemi2), 1u);
+    if (v.wantS) emit(reflect(v.d, v.g.N), 2u);
+    if (v.wantT) emit(refract(v.d, v.g.N, 1.0F / v.ior), 3u);
+    const int mask = (v.wantD ? 1 : 0) | (v.wantS ? 2 : 0) | (v.wantT ? 4 : 0);
+    lv.vtx[i] = make_int4(v.mat, shadowBase, childBase, (v.nShadow << 3) | mask);
+}
+
 template <int kShader>
 __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
     const int count = min(counters[cntRays(level)], lv.cap);
@@ -429,129 +588,12 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
          base += static_cast<int>(gridDim.x * blockDim.x)) {
         const int i = base + static_cast<int>(threadIdx.x);
         const bool active = i < count;
-        int nShadow = 0, nChild = 0;
-        bool terminal = true;
-        float4 leaf = make_float4(0.0F, 0.0F, 0.0F, 0.0F);
-        HitGeom g{};
-        v3 d{0, 0, 0}, Kd{0, 0, 0}, Ks{0, 0, 0}, Kt{0, 0, 0};
-        float ior = 1.0F;
-        int mat = -1;
-        uint32_t key = 0, tc = 0;
-        bool wantD = false, wantS = false, wantT = false, direct = false;
-        // light sample 0 (kept in registers) and the prefetched table draws
-        v3 ld0{0, 0, 0}, lc0{0, 0, 0};
-        float dist0 = 0.0F;
-        bool ok0 = false;
-        float hemi1 = 0.0F, hemi2 = 0.0F;
-        if (active) {
-            const float4 o4 = lv.rO[i];
-            const float4 d4 = lv.rD[i];
-            const float4 h = lv.hit[i];
-            key = fbits(o4.w);
-            tc = lv.tree[i];
-            d = xyz(d4);
-            // issue every table gather of this vertex at once: their latencies overlap
-            const float pick0 = s.tables[sampleIndex(key, tc, purposeLightPick(0))].x;
-            const float lr0 = s.tables[sampleIndex(key, tc, purposeLightR(0))].y;
-            const float lq0 = s.tables[sampleIndex(key, tc, purposeLightS(0))].y;
-            const float rr = s.tables[sampleIndex(key, tc, kPRussian)].y;
-            hemi1 = s.tables[sampleIndex(key, tc, kPHemi1)].x;
-            hemi2 = s.tables[sampleIndex(key, tc, kPHemi2)].x;
-            const uint32_t code = fbits(h.w);
-            const uint32_t kind = primKind(code);
-            // Shader.cpp:122: shade only if hit; Whitted.cpp:14-17 / PathTracer.cpp:25-28: depth cap
-            if (kind != kMiss && level <= a.maxDepth) {
-                v3 Le;
-                if (kind == kLight) {
-                    Le = xyz(s.lights[4 * primIndex(code) + 3]);
-                } else {
-                    mat = hitMaterial(s, code);
-                    const float4* m = s.mats + 4 * mat;
-                    const float4 le4 = m[0];
-                    Le = xyz(le4);
-                    ior = le4.w;
-                    Kd = xyz(m[1]);
-                    Ks = xyz(m[2]);
-                    Kt = xyz(m[3]);
-                }
-                if (hasPositive(Le)) {  // Whitted.cpp:19-24
-                    leaf = make_float4(Le.x, Le.y, Le.z, 1.0F);
-                } else {
-                    terminal = false;
-                    g = hitGeometry(s, xyz(o4), d, h);
-                    direct = hasPositive(Kd) && s.nLights > 0;
-                    if (direct) {
-                        ok0 = lightSample(s, g, pick0, lr0, lq0, &ld0, &dist0, &lc0);
-                        nShadow = static_cast<int>(ok0);
-                        for (int k = 1; k < a.samplesLight; ++k) {
-                            v3 ld, lc;
-                            float dist;
-                            if (lightSample(s, g, s.tables[sampleIndex(key, tc, purposeLightPick(k))].x,
-                                            s.tables[sampleIndex(key, tc, purposeLightR(k))].y,
-                                            s.tables[sampleIndex(key, tc, purposeLightS(k))].y, &ld, &dist, &lc))
-                                ++nShadow;
-                        }
-                    }
-                    if (kShader == kShaderPathTracer && hasPositive(Kd)) {  // PathTracer.cpp:89
-                        wantD = level <= kRayDepthMin || rr > 0.5F;
-                    }
-                    wantS = hasPositive(Ks);
-                    wantT = hasPositive(Kt);
-                    nChild = static_cast<int>(wantD) + static_cast<int>(wantS) + static_cast<int>(wantT);
-                }
-            }
-        }
+        ShadeState v{};
+        if (active) v = shadePrepare<kShader>(s, lv.rO[i], lv.rD[i], lv.hit[i], lv.tree[i], level, a);
         int childBase, shadowBase;
-        blockAllocPair(pair, nChild, nShadow, &childBase, &shadowBase, allocLds, parity);
+        blockAllocPair(pair, active ? v.nChild : 0, active ? v.nShadow : 0, &childBase, &shadowBase, allocLds, parity);
         parity ^= 1;
-        if (!active) continue;
-        if (terminal) {
-            lv.res[i] = leaf;
-            lv.vtx[i] = make_int4(-1, 0, 0, 0);
-            continue;
-        }
-        // shadow rays (Whitted.cpp:53, PathTracer.cpp:67)
-        int written = 0;
-        if (direct) {
-            for (int k = 0; k < a.samplesLight; ++k) {
-                v3 ld = ld0, lc = lc0;
-                float dist = dist0;
-                if (k == 0) {
-                    if (!ok0) continue;
-                } else if (!lightSample(s, g, s.tables[sampleIndex(key, tc, purposeLightPick(k))].x,
-                                        s.tables[sampleIndex(key, tc, purposeLightR(k))].y,
-                                        s.tables[sampleIndex(key, tc, purposeLightS(k))].y, &ld, &dist, &lc)) {
-                    continue;
-                }
-                const int j = shadowBase + written;
-                ++written;
-                if (j < lv.shadowCap) {
-                    lv.sO[j] = make_float4(g.P.x, g.P.y, g.P.z, bitsf(g.src));
-                    lv.sD[j] = make_float4(ld.x, ld.y, ld.z, dist);
-                    lv.sC[j] = make_float4(lc.x, lc.y, lc.z, 0.0F);
-                } else {
-                    atomicOr(counters + kCntOverflow, 1);
-                }
-            }
-        }
-        // child rays: diffuse (PathTracer.cpp:90-91), specular (:118-120), transmission (:129-131),
-        // stored consecutively from childBase
-        int c = childBase;
-        auto emit = [&](v3 dir, uint32_t slot) {
-            const int j = c++;
-            if (j >= nx.cap) {
-                atomicOr(counters + kCntOverflow, 1);  // the frame is redone in smaller passes
-                return;
-            }
-            nx.rO[j] = make_float4(g.P.x, g.P.y, g.P.z, bitsf(key));
-            nx.rD[j] = make_float4(dir.x, dir.y, dir.z, bitsf(g.src));
-            nx.tree[j] = tc * 4u + slot;
-        };
-        if (wantD) emit(cosineHemisphere(g.N, hemi1, hemi2), 1u);
-        if (wantS) emit(reflect(d, g.N), 2u);
-        if (wantT) emit(refract(d, g.N, 1.0F / ior), 3u);
-        const int mask = (wantD ? 1 : 0) | (wantS ? 2 : 0) | (wantT ? 4 : 0);
-        lv.vtx[i] = make_int4(mat, shadowBase, childBase, (nShadow << 3) | mask);
+        if (active) shadeEmit<false>(s, v, i, lv, nx, shadowBase, childBase, counters, a);
     }
 }
 
