@@ -550,7 +550,9 @@ __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, 
             if (j < lv.shadowCap) {
                 storeF4<kPublish>(lv.sO, j, make_float4(v.g.P.x, v.g.P.y, v.g.P.z, bitsf(v.g.src)));
                 storeF4<kPublish>(lv.sD, j, make_float4(ld.x, ld.y, ld.z, dist));
-                lv.sC[j] = make_float4(lc.x, lc.y, lc.z, 0.0F);
+                // sc1 too when published: the shadow walk, maybe on another XCD, later writes the
+                // occlusion flag into this line, and a dirty copy here must not overwrite it
+                storeF4<kPublish>(lv.sC, j, make_float4(lc.x, lc.y, lc.z, 0.0F));
             } else {
                 atomicOr(counters + kCntOverflow, 1);
             }
@@ -594,6 +596,41 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
         blockAllocPair(pair, active ? v.nChild : 0, active ? v.nShadow : 0, &childBase, &shadowBase, allocLds, parity);
         parity ^= 1;
         if (active) shadeEmit<false>(s, v, i, lv, nx, shadowBase, childBase, counters, a);
+    }
+}
+
+}  // namespace mrt
+#include "mrt_stream.hpp"
+namespace mrt {
+
+constexpr int kStreamMinWaves = 5;  // caps registers: the shading code would otherwise take 144 VGPRs
+
+template <int kShader, int kVariant>
+__global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, kStreamMinWaves) void k_stream(
+    DScene s, StreamArgs A, int* counters, int2* gstack, int gdepth) {
+    using C = TraceCfg<kVariant>;
+    static_assert(C::kWide == 2, "streaming mode walks the BVH2");
+    __shared__ int2 ldsStack[C::kStack * C::kThreads];
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * C::kThreads + threadIdx.x) * gdepth, 0,
+              C::kStack, C::kThreads};
+    __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
+    stageTop<C::kTop, C::kThreads>(s, ldsTop);
+    streamLoop<kShader, C::kWide, C::kRefill, C::kTop, C::kFastSlab>(s, A, counters, st, ldsTop);
+}
+
+// level counts for resolve / tally from the streaming counters; overflow and error flags
+__global__ void k_stream_finish(int* counters, int nLevels, StreamArgs A) {
+    const int l = static_cast<int>(threadIdx.x);
+    if (l < 1 || l > nLevels) return;
+    const int rays = l == 1 ? counters[cntRays(1)] : *streamCnt(counters, l, 0);
+    const int shadows = *streamCnt(counters, l, 2);
+    if (l > 1) counters[cntRays(l)] = min(rays, A.lv[l].cap);
+    counters[cntShadows(l)] = min(shadows, A.lv[l].shadowCap);
+    if (rays > A.lv[l].cap || shadows > A.lv[l].shadowCap) atomicOr(counters + kCntOverflow, 1);
+    if (l == 1) {
+        const int err = counters[kCntStream + (kMaxLevels * 4 + 1) * kFetchStride];
+        const int left = counters[kCntStream + kMaxLevels * 4 * kFetchStride];
+        if (err != 0 || left != 0) atomicOr(counters + kCntOverflow, 2);
     }
 }
 
@@ -778,7 +815,7 @@ __global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats) 
     stats[kStatRays] += rays;
     stats[kStatShadowRays] += shadows;
     stats[kStatPrimary] += static_cast<unsigned long long>(counters[cntRays(1)]);
-    if (counters[kCntOverflow] != 0) stats[kStatOverflow] = 1ull;
+    if (counters[kCntOverflow] != 0) stats[kStatOverflow] |= static_cast<unsigned long long>(counters[kCntOverflow]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -792,7 +829,7 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
 // the spill stacks were sized for.
 template <typename K>
 int persistentGrid(K kernel, int variant, int kind, int threads, int maxThreads) {
-    static int occ[3][kTraceVariants] = {};  // kind: 0 closest, 1 shadow, 2 combined
+    static int occ[5][kTraceVariants] = {};  // kind: 0 closest, 1 shadow, 2 combined, 3/4 streaming
     static int cus = 0;
     const int cap = std::max(1, maxThreads / threads);
     if (cus == 0) {
@@ -846,6 +883,48 @@ int persistentGrid(K kernel, int variant, int kind, int threads, int maxThreads)
             hipLaunchKernelGGL((k_combo<false, V>), dim3(g), dim3(kT), 0, st, s, lv, prev, counters, level, gstack, gdepth, stats); \
         break;                                                                                               \
     }
+
+template <int kShader, int V>
+void launchStreamV(const DScene& s, const StreamArgs& A, int* counters, int2* gstack, int gdepth, int maxThreads,
+                   hipStream_t st) {
+    constexpr int kT = TraceCfg<V>::kThreads;
+    const int g = persistentGrid(k_stream<kShader, V>, V, kShader == kShaderWhitted ? 3 : 4, kT, maxThreads);
+    hipLaunchKernelGGL((k_stream<kShader, V>), dim3(g), dim3(kT), 0, st, s, A, counters, gstack, gdepth);
+}
+
+bool launchStream(int shader, const DScene& s, const Level* lv, int nLevels, uint32_t epoch, const ShadeArgs& a,
+                  int* counters, int2* gstack, int gdepth, int maxThreads, hipStream_t st) {
+    if (shader != kShaderWhitted && shader != kShaderPathTracer) return false;
+    if (s.variant != 14 && s.variant != 13 && s.variant != 8) return false;
+    StreamArgs A{};
+    for (int l = 0; l < kMaxLevels; ++l) A.lv[l] = lv[l];
+    A.nLevels = nLevels;
+    A.epoch = epoch;
+    A.sa = a;
+    const bool w = shader == kShaderWhitted;
+    switch (s.variant) {
+        case 8:
+            w ? launchStreamV<kShaderWhitted, 8>(s, A, counters, gstack, gdepth, maxThreads, st)
+              : launchStreamV<kShaderPathTracer, 8>(s, A, counters, gstack, gdepth, maxThreads, st);
+            break;
+        case 13:
+            w ? launchStreamV<kShaderWhitted, 13>(s, A, counters, gstack, gdepth, maxThreads, st)
+              : launchStreamV<kShaderPathTracer, 13>(s, A, counters, gstack, gdepth, maxThreads, st);
+            break;
+        default:
+            w ? launchStreamV<kShaderWhitted, 14>(s, A, counters, gstack, gdepth, maxThreads, st)
+              : launchStreamV<kShaderPathTracer, 14>(s, A, counters, gstack, gdepth, maxThreads, st);
+            break;
+    }
+    return true;
+}
+
+void launchStreamFinish(int* counters, int nLevels, const Level* lv, hipStream_t st) {
+    StreamArgs A{};
+    for (int l = 0; l < kMaxLevels; ++l) A.lv[l] = lv[l];
+    A.nLevels = nLevels;
+    hipLaunchKernelGGL(k_stream_finish, dim3(1), dim3(64), 0, st, counters, nLevels, A);
+}
 
 bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,
                  int gdepth, unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {

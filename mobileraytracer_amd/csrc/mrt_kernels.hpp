@@ -24,7 +24,10 @@ constexpr int kCntOverflow = kCntFetchShadow + kMaxLevels;
 constexpr int kMaxFetchShards = 32;                   // sharded work cursors per level
 constexpr int kFetchStride = 32;                      // ints between cursors (a 128-byte line each)
 constexpr int kCntFetchShards = 128;                  // 2 kinds x kMaxLevels x kMaxFetchShards lines
-constexpr int kNumCounters = kCntFetchShards + 2 * kMaxLevels * kMaxFetchShards * kFetchStride;
+constexpr int kCntStream = kCntFetchShards + 2 * kMaxLevels * kMaxFetchShards * kFetchStride;
+// streaming mode: per level 4 lines (ray alloc, ray claim, shadow alloc, shadow claim), then
+// `pending` and the error flag
+constexpr int kNumCounters = kCntStream + (kMaxLevels * 4 + 2) * kFetchStride;
 MRT_HD constexpr int cntRays(int level) { return kCntPairs + 2 * (level - 1); }
 MRT_HD constexpr int cntShadows(int level) { return kCntPairs + 2 * level + 1; }
 
@@ -55,6 +58,8 @@ struct Level {
     float4* sO;      // shadow ray origin, w = source primitive bits
     float4* sD;      // shadow ray direction, w = distance to the light
     float4* sC;      // light contribution Le*cos, w = occluded flag
+    uint32_t* ready;         // streaming mode: per ray slot, = epoch once its payload is stored
+    uint32_t* sReady;        // the same for the shadow ray slots
     const int* order;        // trace visit order of the rays (null: queue order)
     const int* shadowOrder;  // the same for the shadow rays
     int cap;
@@ -102,6 +107,11 @@ struct AccumArgs {
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
+// streaming mode: every level of the pass in one persistent launch (mrt_stream.hpp); returns
+// false for shaders / variants without that form.  lv[0..kMaxLevels), epoch as StreamArgs.
+bool launchStream(int shader, const DScene& s, const Level* lv, int nLevels, uint32_t epoch, const ShadeArgs& a,
+                  int* counters, int2* gstack, int gdepth, int maxThreads, hipStream_t st);
+void launchStreamFinish(int* counters, int nLevels, const Level* lv, hipStream_t st);
 // closest-hit rays of `level` then shadow rays of level - 1 in one launch; false if the trace
 // variant has no such form (the caller then launches them separately)
 bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,

@@ -135,6 +135,8 @@ struct mrt_renderer {
     };
     std::vector<Pipe> pipes;
     int nPipes = 1;                      // tuning key 5 (more pipelines measured slower)
+    int streamMode = 0;                  // tuning key 6: every level of a pass in one launch
+    uint32_t epoch = 0;                  // streaming mode: ready-flag value of the current pass
     int chunkSlots = 0;
     int gdepth = 0;
     int traceThreads = 0, workGrid = 0;  // traceThreads: resident trace threads, whole device
@@ -370,24 +372,28 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
             pp.counters = nullptr;
             continue;
         }
-        // ping-pong ray / hit buffers (dead after k_shade of their level)
-        float4* rO[2];
-        float4* rD[2];
-        uint32_t* tree[2];
-        float4* hit[2];
-        for (int k = 0; k < 2; ++k) {
-            rO[k] = r->queueMem.alloc<float4>(capN);
-            rD[k] = r->queueMem.alloc<float4>(capN);
-            tree[k] = r->queueMem.alloc<uint32_t>(capN);
-            hit[k] = r->queueMem.alloc<float4>(capN);
-        }
-        // shadow rays: ping-pong too, so k_shade of level L+1 can run while the any-hit
-        // kernel of level L still reads its rays
-        float4* sO[2];
-        float4* sD[2];
-        for (int k = 0; k < 2; ++k) {
-            sO[k] = r->queueMem.alloc<float4>(capN * spl);
-            sD[k] = r->queueMem.alloc<float4>(capN * spl);
+        // ray / hit / shadow buffers: one set per level (the streaming mode keeps every level
+        // live at once; the level-by-level mode could alternate two sets)
+        const int nBuf = std::min(nLevels + 1, kMaxLevels - 1);
+        std::vector<float4*> rO(nBuf + 1), rD(nBuf + 1), hit(nBuf + 1), sO(nBuf + 1), sD(nBuf + 1);
+        std::vector<uint32_t*> tree(nBuf + 1), ready(nBuf + 1), sReady(nBuf + 1);
+        for (int k = 1; k <= nBuf; ++k) {
+            const size_t cap = (k == 1) ? n1 : capN;
+            rO[k] = r->queueMem.alloc<float4>(cap);
+            rD[k] = r->queueMem.alloc<float4>(cap);
+            tree[k] = r->queueMem.alloc<uint32_t>(cap);
+            hit[k] = r->queueMem.alloc<float4>(cap);
+            ready[k] = r->queueMem.alloc<uint32_t>(cap);
+            MRT_HIP(hipMemset(ready[k], 0, cap * sizeof(uint32_t)));
+            if (k <= nLevels) {
+                sO[k] = r->queueMem.alloc<float4>(cap * spl);
+                sD[k] = r->queueMem.alloc<float4>(cap * spl);
+                sReady[k] = r->queueMem.alloc<uint32_t>(cap * spl);
+                MRT_HIP(hipMemset(sReady[k], 0, cap * spl * sizeof(uint32_t)));
+            } else {
+                sO[k] = sD[k] = nullptr;
+                sReady[k] = nullptr;
+            }
         }
         for (int l = 1; l <= nLevels + 1 && l < kMaxLevels; ++l) {
             Level& lv = pp.levels[l];
@@ -395,12 +401,14 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
             const bool real = l <= nLevels;
             lv.cap = real ? static_cast<int>(cap) : 0;
             lv.shadowCap = real ? static_cast<int>(cap * spl) : 0;
-            lv.rO = rO[l & 1];
-            lv.rD = rD[l & 1];
-            lv.tree = tree[l & 1];
-            lv.hit = hit[l & 1];
-            lv.sO = sO[l & 1];
-            lv.sD = sD[l & 1];
+            lv.rO = rO[l];
+            lv.rD = rD[l];
+            lv.tree = tree[l];
+            lv.hit = hit[l];
+            lv.sO = sO[l];
+            lv.sD = sD[l];
+            lv.ready = ready[l];
+            lv.sReady = sReady[l];
             lv.order = nullptr;
             lv.shadowOrder = nullptr;
             if (real) {
@@ -511,6 +519,35 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.sppTotal = r->cfg.samplesPixel;
         ra.sampleBase = sampleBase;
         launchRaygen(ra, pp.levels[1], pp.counters, ps);
+        if (r->streamMode != 0 && !counting) {
+            // streaming mode: `pending` starts at the camera-ray count; the flags of a new pass
+            // compare against a fresh epoch (no clearing between passes)
+            const uint32_t epoch = ++r->epoch;
+            int* pendingPtr = pp.counters + kCntStream + kMaxLevels * 4 * kFetchStride;
+            MRT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(pendingPtr), ra.nPaths, 1, ps));
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
+            const bool ok = launchStream(shader, r->ds, pp.levels, nLevels, epoch, sa, pp.counters, pp.gstack, r->gdepth,
+                                         r->traceThreads, ps);
+            if (ok) {
+                if (timing) {
+                    for (int k = 0; k < 4; ++k) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
+                }
+                launchStreamFinish(pp.counters, nLevels, pp.levels, ps);
+                for (int l = nLevels; l >= 1; --l)
+                    launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
+                AccumArgs aa{};
+                aa.map = map;
+                aa.width = r->cfg.width;
+                aa.slotBase = slot0;
+                aa.nSlots = nChunk;
+                aa.spp = spp;
+                aa.sampleBase = sampleBase;
+                launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, ps);
+                launchTally(pp.counters, nLevels, pp.stats, ps);
+                continue;
+            }
+            if (timing) pp.evCount -= 1;  // not launched: fall back to the level-by-level form
+        }
         // Any-hit (shadow) rays of level L run on a second stream, overlapped with the
         // closest-hit trace and shading of level L+1: the persistent kernels' drain phases fill
         // each other.  Orders: shade(L) -> shadow(L); shadow(L) -> shade(L+2) (the shadow ray
@@ -613,6 +650,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
         const unsigned long long* ps = all.data() + static_cast<size_t>(pi) * kNumStats;
         for (int k = 0; k < kNumStats; ++k) hs[k] = (k == kStatMaxNodesRay) ? std::max(hs[k], ps[k]) : hs[k] + ps[k];
     }
+    if ((hs[kStatOverflow] & 2) != 0) throw std::runtime_error("streaming kernel: bounded wait exceeded or items left");
     if (hs[kStatOverflow] != 0) return false;
     fs->rays += hs[kStatRays];
     fs->shadowRays += hs[kStatShadowRays];
@@ -887,6 +925,10 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->sortRays = value;
         return 0;
     }
+    if (key == 6 && (value == 0 || value == 1)) {
+        r->streamMode = value;
+        return 0;
+    }
     if (key == 5 && value >= 1 && value <= 8) {
         return guarded([&] {
             MRT_HIP(hipDeviceSynchronize());
@@ -946,6 +988,10 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
     }
     if (key == 5) {
         *value = r->nPipes;
+        return 0;
+    }
+    if (key == 6) {
+        *value = r->streamMode;
         return 0;
     }
     gLastError = "unknown tuning key";

@@ -13,8 +13,8 @@ def main():
     r = m.Renderer(cfg)
     d = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
-    # "V[:O[:S[:P]]]": trace variant V, shadow-stream overlap O (default 1), ray sorting S
-    # (default 0), chunk pipelines P (default 1)
+    # "V[:O[:S[:P[:M]]]]": trace variant V, shadow-stream overlap O (default 1), ray sorting S
+    # (default 0), chunk pipelines P (default 1), streaming mode M (default 0)
     variants = os.environ.get("VARIANTS", "8,8:0,13,14").split(",")
     imgs = {}
     res = {v: [] for v in variants}
@@ -22,11 +22,12 @@ def main():
     for rnd in range(3):
         for v in variants:
             parts = v.split(":")
-            parts += ["1", "0", "1"][len(parts) - 1:]
+            parts += ["1", "0", "1", "0"][len(parts) - 1:]
             r.set_tuning(1, int(parts[0]))
             r.set_tuning(3, int(parts[1]))
             r.set_tuning(4, int(parts[2]))
             r.set_tuning(5, int(parts[3]))
+            r.set_tuning(6, int(parts[4]))
             r.render_frame_device(d.data_ptr(), 0, sh)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
