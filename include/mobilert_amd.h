@@ -94,6 +94,8 @@ typedef struct mrt_frame_stats {
     double levelTraceMs[16];      /* profiling: closest-hit trace time per depth */
     double levelShadowMs[16];     /* profiling: any-hit trace time per depth */
     uint64_t maxNodeRecordsPerRay; /* counting pass only: most node records one ray fetched */
+    uint64_t assistedSubtrees;     /* tail-assist trace variants: subtrees handed to idle lanes */
+    uint64_t maxRayMicros;         /* tail-assist trace variants: longest fetch-to-result time of one ray */
 } mrt_frame_stats;
 
 const char *mrt_last_error(void);

@@ -39,6 +39,9 @@ struct DScene {
     int32_t cull;              // 1: near-first + conservative t-culling, 0: reference visit set
     int32_t variant;           // trace kernel organisation (mrt_kernels.hip kTraceCfg)
     int32_t triTop;            // triNodes[0, triTop) are the breadth-first top of the tree
+    const CNode* triCNodes;    // compressed copy of triNodes (same numbering; [triTop, ..) used)
+    const float* leafBoxes;    // exact box of every triangle leaf, 8 floats at its first primitive
+    int32_t compOk;            // triCNodes / leafBoxes are valid (else compressed variants fall back)
 };
 
 __device__ __forceinline__ float4 ld4(const float4* p) { return *p; }
@@ -229,6 +232,8 @@ struct TravCount {
     uint32_t tris;   // triangle tests
     uint32_t rayStart = 0;  // nodes at the current ray's fetch (per-ray maximum, counting builds)
     uint32_t rayMax = 0;
+    uint32_t assists = 0;   // tail-assist builds: subtrees this lane handed over
+    uint32_t ticksMax = 0;  // tail-assist builds: longest fetch-to-result time (100 MHz ticks)
 };
 
 // Generic BVH walk.  kKind selects the leaf routine.  Returns true on an any-hit.

@@ -160,6 +160,9 @@ struct TraceCfgRow {
     int top;                                    // BVH2 top nodes staged in LDS (<= kTopNodesMax)
     int threads = kBlock;                       // per workgroup (the LDS top is shared by them)
     int fastSlab = 0;                           // IEEE min/max slab test when every 1/d is finite
+    int assist = 0;                             // tail assist: idle lanes take subtrees of walking ones
+    int trim = 0;                               // grid trimmed to ~2 lanes per ray; drained cursors read first
+    int comp = 0;                               // compressed nodes (CNode) below the LDS top
 };
 constexpr TraceCfgRow kTraceCfg[] = {
     {2, 1, kLdsStack, 1, 1, 0},   // 0  per-wave batches, if-if
@@ -177,7 +180,13 @@ constexpr TraceCfgRow kTraceCfg[] = {
     {2, 32, 8, 8, 1, 64},         // 12 as 8, top 64 nodes in LDS
     {2, 32, 8, 8, 1, 128},        // 13 as 8, top 128 nodes in LDS
     {2, 32, 8, 8, 1, 128, 256, 1},  // 14 as 13, IEEE min/max slab test for finite 1/d (default)
-    {2, 32, 8, 8, 1, 256, 512},     // 15 as 13, top 256 nodes, 512-thread workgroups
+    {2, 32, 8, 8, 1, 128, 512},     // 15 as 13, 512-thread workgroups
+    {2, 32, 8, 8, 1, 128, 256, 1, 1},     // 16 as 14 with tail assist
+    {2, 32, 8, 8, 1, 128, 256, 1, 1, 1},  // 17 as 16, trimmed grid
+    {2, 32, 8, 8, 1, 128, 256, 1, 0, 1},  // 18 as 14, trimmed grid
+    {2, 32, 8, 8, 1, 128, 256, 1, 0, 0, 1},  // 19 as 14, compressed nodes
+    {2, 32, 8, 8, 1, 128, 256, 1, 1, 0, 1},  // 20 as 19 with tail assist
+    {2, 32, 8, 8, 1, 128, 256, 1, 1, 1, 1},  // 21 as 20, trimmed grid
 };
 constexpr int kNumTraceVariants = sizeof(kTraceCfg) / sizeof(kTraceCfg[0]);
 static_assert(kNumTraceVariants == kTraceVariants, "mrt_kernels.hpp kTraceVariants");
@@ -192,9 +201,36 @@ struct TraceCfg {
     static constexpr int kTop = kTraceCfg[kVariant].wide == 2 ? kTraceCfg[kVariant].top : 0;
     static constexpr int kThreads = kTraceCfg[kVariant].threads;
     static constexpr bool kFastSlab = kTraceCfg[kVariant].fastSlab != 0;
+    static constexpr bool kAssist = kTraceCfg[kVariant].assist != 0;
+    static constexpr bool kTrim = kTraceCfg[kVariant].trim != 0;
+    static constexpr bool kComp = kTraceCfg[kVariant].comp != 0;
+    static_assert(!kComp || (kTraceCfg[kVariant].wide == 2 && kTraceCfg[kVariant].fastSlab != 0), "CNode walk: BVH2, finite slab");
     static_assert(kTop <= kTopNodesMax, "top nodes");
     static_assert(kThreads % 64 == 0 && kThreads <= 1024, "workgroup size");
 };
+
+// Trimmed grid (kTrim): a level of `count` rays needs ~2 lanes per ray (the spare lanes assist
+// the slowest walks); the other workgroups of the persistent grid leave at once instead of
+// each paying for the LDS top and a round of cursor atomics.
+template <int kThreads>
+__device__ __forceinline__ bool blockSpare(int count) {
+    const long long need = (2LL * count + kThreads - 1) / kThreads;
+    return static_cast<long long>(blockIdx.x) >= max(need, 8LL);
+}
+
+// Tail-assist variants: handed-over subtrees (sum) and the longest ray (max) of the launch.
+__device__ __forceinline__ void assistStats(const TravCount& c, unsigned long long* stats) {
+    unsigned long long a = c.assists;
+    uint32_t m = c.ticksMax;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_down(a, off, 64);
+        m = max(m, static_cast<uint32_t>(__shfl_down(static_cast<int>(m), off, 64)));
+    }
+    if (laneId() == 0) {
+        if (a != 0) atomicAdd(stats + kStatAssist, a);
+        atomicMax(stats + kStatMaxRayTicks, static_cast<unsigned long long>(m));
+    }
+}
 
 // Copies the BVH2 top into LDS (all threads; ends with a barrier).
 template <int kTop, int kThreads>
@@ -219,9 +255,10 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
                                 : counters + kCntFetchTrace + level;
     TravCount cnt{0u, 0u};
     __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
+    if (C::kTrim && blockSpare<C::kThreads>(count)) return;
     stageTop<C::kTop, C::kThreads>(s, ldsTop);
     if (kVariant > 0)
-        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab>(s, lv.rO, lv.rD, lv.hit, count, fetch,
+        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp>(s, lv.rO, lv.rD, lv.hit, count, fetch,
                                                                                    st, &cnt, ldsTop, lv.order);
     while (kVariant == 0) {
         int base = 0;
@@ -236,6 +273,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
             lv.hit[i] = make_float4(b.t, b.u, b.v, bitsf(b.code));
         }
     }
+    if (C::kAssist && !kCount) assistStats(cnt, stats);
     if (kCount) {
         unsigned long long n = cnt.nodes, t = cnt.tris;
         for (int off = 32; off > 0; off >>= 1) {
@@ -263,9 +301,10 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
                      : counters + kCntFetchShadow + level;
     TravCount cnt{0u, 0u};
     __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
+    if (C::kTrim && blockSpare<C::kThreads>(count)) return;
     stageTop<C::kTop, C::kThreads>(s, ldsTop);
     if (kVariant > 0)
-        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab>(s, lv.sO, lv.sD, lv.sC, count, fetch,
+        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp>(s, lv.sO, lv.sD, lv.sC, count, fetch,
                                                                                   st, &cnt, ldsTop, lv.shadowOrder);
     while (kVariant == 0) {
         int base = 0;
@@ -280,6 +319,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
             lv.sC[i].w = occ ? 1.0F : 0.0F;
         }
     }
+    if (C::kAssist && !kCount) assistStats(cnt, stats);
     if (kCount) {
         unsigned long long n = cnt.nodes, t = cnt.tris;
         for (int off = 32; off > 0; off >>= 1) {
@@ -311,7 +351,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
         const int count = min(counters[cntRays(level)], lv.cap);
         int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride
                                     : counters + kCntFetchTrace + level;
-        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab>(
+        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp>(
             s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, lv.order);
     }
     if (level >= 2) {
@@ -319,7 +359,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
         const int count = min(counters[cntShadows(pl)], prev.shadowCap);
         int* fetch = C::kShards > 1 ? counters + kCntFetchShards + (kMaxLevels + pl) * kMaxFetchShards * kFetchStride
                                     : counters + kCntFetchShadow + pl;
-        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab>(
+        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp>(
             s, prev.sO, prev.sD, prev.sC, count, fetch, st, &cntS, ldsTop, prev.shadowOrder);
     }
     if (kCount) {
@@ -870,7 +910,13 @@ int persistentGrid(K kernel, int variant, int kind, int threads, int maxThreads)
         MRT_LAUNCH_ONE(KERNEL, KIND, 12)                                                                     \
         MRT_LAUNCH_ONE(KERNEL, KIND, 13)                                                                     \
         MRT_LAUNCH_ONE(KERNEL, KIND, 14)                                                                     \
-        default: MRT_LAUNCH_ONE(KERNEL, KIND, 15)                                                            \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 15)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 16)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 17)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 18)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 19)                                                                     \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 20)                                                                     \
+        default: MRT_LAUNCH_ONE(KERNEL, KIND, 21)                                                            \
     }
 
 #define MRT_LAUNCH_COMBO_ONE(V)                                                                              \
@@ -926,6 +972,10 @@ void launchStreamFinish(int* counters, int nLevels, const Level* lv, hipStream_t
     hipLaunchKernelGGL(k_stream_finish, dim3(1), dim3(64), 0, st, counters, nLevels, A);
 }
 
+bool traceVariantCompressed(int variant) {
+    return variant >= 0 && variant < kNumTraceVariants && kTraceCfg[variant].comp != 0;
+}
+
 bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,
                  int gdepth, unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
     switch (s.variant) {
@@ -944,6 +994,12 @@ bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* count
         MRT_LAUNCH_COMBO_ONE(13)
         MRT_LAUNCH_COMBO_ONE(14)
         MRT_LAUNCH_COMBO_ONE(15)
+        MRT_LAUNCH_COMBO_ONE(16)
+        MRT_LAUNCH_COMBO_ONE(17)
+        MRT_LAUNCH_COMBO_ONE(18)
+        MRT_LAUNCH_COMBO_ONE(19)
+        MRT_LAUNCH_COMBO_ONE(20)
+        MRT_LAUNCH_COMBO_ONE(21)
         default:
             return false;  // variant 0 (per-wave batches): separate launches
     }

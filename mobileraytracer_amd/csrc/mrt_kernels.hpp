@@ -11,9 +11,10 @@ constexpr int kShaderDepthMap = 3;    // C_wrapper.cpp:175-179
 constexpr int kShaderDiffuse = 4;     // C_wrapper.cpp:181-186 (DiffuseMaterial)
 constexpr int kShaderNoShadows = 5;   // C_wrapper.cpp:188-193 (the switch's default: 0, 5, ...)
 constexpr int kMaxLevels = 16;           // max ray depth + 2
-constexpr int kTraceVariants = 16;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
+constexpr int kTraceVariants = 22;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
 constexpr int kDefaultTraceVariant = 14;
-constexpr int kTopNodesMax = 256;        // BVH2 nodes numbered breadth-first (LDS-staged by some variants)
+constexpr int kExactTraceVariant = 14;    // stands in for compressed variants when a scene has no CNodes
+constexpr int kTopNodesMax = 128;        // BVH2 nodes numbered breadth-first (LDS-staged by some variants)
 
 // Device counters (ints).  Pair l = {rays of level l+1, shadow rays of level l} sits on two
 // adjacent ints so k_shade allocates both with one 64-bit atomic per block.
@@ -43,7 +44,9 @@ constexpr int kStatTrisShadow = 7;  // any-hit kernel: triangle tests (counting 
 constexpr int kStatLevelRays = 8;                     // + level - 1: rays of each level
 constexpr int kStatLevelShadows = 8 + kMaxLevels;     // + level - 1: shadow rays of each level
 constexpr int kStatMaxNodesRay = 8 + 2 * kMaxLevels;  // counting builds: most node records of one ray
-constexpr int kNumStats = kStatMaxNodesRay + 1;
+constexpr int kStatAssist = kStatMaxNodesRay + 1;    // tail-assist variants: subtrees handed over
+constexpr int kStatMaxRayTicks = kStatAssist + 1;    // tail-assist variants: longest ray (100 MHz ticks)
+constexpr int kNumStats = kStatMaxRayTicks + 1;
 
 // One level of the wavefront (SoA queues).
 struct Level {
@@ -114,6 +117,8 @@ bool launchStream(int shader, const DScene& s, const Level* lv, int nLevels, uin
 void launchStreamFinish(int* counters, int nLevels, const Level* lv, hipStream_t st);
 // closest-hit rays of `level` then shadow rays of level - 1 in one launch; false if the trace
 // variant has no such form (the caller then launches them separately)
+// kTraceCfg row `variant` walks compressed nodes (needs DScene::compOk)
+bool traceVariantCompressed(int variant);
 bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,
                  int gdepth, unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,

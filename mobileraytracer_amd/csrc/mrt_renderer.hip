@@ -254,6 +254,13 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop);
     d.triNodes = r->sceneMem.upload(g, st);
     {
+        std::vector<CNode> cn;
+        std::vector<float> lb;
+        d.compOk = toDeviceCBVH(g, d.triTop, d.triRoot, sc.triangles.size(), &cn, &lb) ? 1 : 0;
+        d.triCNodes = r->sceneMem.upload(cn, st);
+        d.leafBoxes = r->sceneMem.upload(lb, st);
+    }
+    {
         std::vector<GNode4> g4;
         toDeviceBVH4(tn, sc.triangles.size(), &g4, &d.triRoot4);
         d.triNodes4 = r->sceneMem.upload(g4, st);
@@ -333,6 +340,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.cull = r->cfg.cull;
     const char* tv = std::getenv("MRT_TRACE_VARIANT");
     d.variant = tv != nullptr ? std::atoi(tv) : kDefaultTraceVariant;
+    if (traceVariantCompressed(d.variant) && d.compOk == 0) d.variant = kExactTraceVariant;
 
     // the two sample tables interleaved: one vertex's draws (consecutive indices, both
     // tables) share one or two cache lines
@@ -648,7 +656,8 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     unsigned long long hs[kNumStats] = {};
     for (int pi = 0; pi < nPipes; ++pi) {
         const unsigned long long* ps = all.data() + static_cast<size_t>(pi) * kNumStats;
-        for (int k = 0; k < kNumStats; ++k) hs[k] = (k == kStatMaxNodesRay) ? std::max(hs[k], ps[k]) : hs[k] + ps[k];
+        for (int k = 0; k < kNumStats; ++k)
+            hs[k] = (k == kStatMaxNodesRay || k == kStatMaxRayTicks) ? std::max(hs[k], ps[k]) : hs[k] + ps[k];
     }
     if ((hs[kStatOverflow] & 2) != 0) throw std::runtime_error("streaming kernel: bounded wait exceeded or items left");
     if (hs[kStatOverflow] != 0) return false;
@@ -660,6 +669,8 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->shadowNodeRecords += hs[kStatNodesShadow];
     fs->shadowTriTests += hs[kStatTrisShadow];
     fs->maxNodeRecordsPerRay = std::max<uint64_t>(fs->maxNodeRecordsPerRay, hs[kStatMaxNodesRay]);
+    fs->assistedSubtrees += hs[kStatAssist];
+    fs->maxRayMicros = std::max<uint64_t>(fs->maxRayMicros, hs[kStatMaxRayTicks] / 100);
     for (int l = 0; l < kMaxLevels; ++l) {
         fs->levelRays[l] += hs[kStatLevelRays + l];
         fs->levelShadowRays[l] += hs[kStatLevelShadows + l];
@@ -910,7 +921,7 @@ int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
 
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
     if (key == 1 && value >= 0 && value < mrt::kTraceVariants) {
-        r->ds.variant = value;
+        r->ds.variant = (mrt::traceVariantCompressed(value) && r->ds.compOk == 0) ? mrt::kExactTraceVariant : value;
         return 0;
     }
     if (key == 2 && (value == 0 || value == 1)) {

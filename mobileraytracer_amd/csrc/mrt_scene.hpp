@@ -128,6 +128,10 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
 // Collapses the reference BVH2 into 4-wide nodes (greedy: open the largest-area inner child
 // until four children), depth-first order.  root->ref is BVH4 node 0 or a leaf ref.
 void toDeviceBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode4>* out, GRoot* root);
+// Compressed nodes (CNode) for g[top..) and the exact box of every leaf indexed by its first
+// primitive (8 floats each).  False if a node breaks the depth-first layout rules.
+bool toDeviceCBVH(const std::vector<GNode>& g, int top, const GRoot& root, size_t numPrims, std::vector<CNode>* out,
+                  std::vector<float>* leafBoxes);
 
 // Utils.cpp:43-53 haltonSequence
 float haltonSequence(uint32_t index, uint32_t base);

@@ -35,6 +35,9 @@ __device__ __forceinline__ float4 bload3(BufRes r, uint32_t off) {  // xyz; w un
 __device__ __forceinline__ int2 bload2i(BufRes r, uint32_t off) {
     return __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
+__device__ __forceinline__ uint4 bload4u(BufRes r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 
 // number of set bits of a wave mask below this lane
 __device__ __forceinline__ int lanesBelowIn(uint64_t m) {
@@ -48,6 +51,29 @@ __device__ __forceinline__ int popCulled(TStack& st, float lim, bool cull) {
         if (!cull || !(__int_as_float(e.y) > lim)) return e.x;
     }
     return kRefDone;
+}
+
+// Culling, near-first order and the push of the far child, shared by the node formats.
+__device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float tr, int refL, int refR, float lim,
+                                              bool cull, TStack& st) {
+    if (cull) {
+        hl = hl && !(tl > lim);
+        hr = hr && !(tr > lim);
+    }
+    if (hl && hr) {
+        int nearRef = refL, farRef = refR;
+        float farT = tr;
+        if (cull && tr < tl) {
+            nearRef = refR;
+            farRef = refL;
+            farT = tl;
+        }
+        st.push(farRef, farT);
+        return nearRef;
+    }
+    if (hl) return refL;
+    if (hr) return refR;
+    return popCulled(st, lim, cull);
 }
 
 // kAny = false: closest hit -> writes lv.hit;  kAny = true: shadow any-hit -> writes lv.sC.w
@@ -82,24 +108,72 @@ __device__ __forceinline__ int innerStep2(BufRes nodes, const GNode* ldsTop, int
         hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
         hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
     }
-    if (cull) {
-        hl = hl && !(tl > lim);
-        hr = hr && !(tr > lim);
+    return chooseChildren(hl, hr, tl, tr, n3.x, n3.y, lim, cull, st);
+}
+
+// One visit of a compressed node (CNode: 2 loads instead of 4) for waves whose rays all have
+// finite 1/d.  The dequantised child boxes contain the exact ones and the finite-1/d slab is
+// monotone in the bounds (each t = (bound - o) * inv is a monotone function of the bound, and
+// min / max / >= preserve it), so every child whose exact box passes passes here too; a child
+// that passes only its enlarged box costs a visit, never a result, because a leaf's triangles
+// count only once the leaf's exact box passes (leafReachable) - and a leaf whose exact box
+// passes has every ancestor's exact box passing too (they contain it).  Nodes [0, top) are the
+// exact LDS copy.
+template <int kTop>
+__device__ __forceinline__ int innerStepC(BufRes cnodes, const GNode* ldsTop, int top, int ref, v3 o, v3 inv,
+                                          float lim, bool cull, TStack& st, TravCount* cnt, bool count) {
+    float lx0, ly0, lz0, lx1, ly1, lz1, rx0, ry0, rz0, rx1, ry1, rz1;
+    int refL, refR;
+    if (kTop > 0 && ref < top) {
+        const float4* np = reinterpret_cast<const float4*>(ldsTop + ref);
+        const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+        const int2 n3 = reinterpret_cast<const int2*>(np)[6];
+        lx0 = n0.x; ly0 = n0.y; lz0 = n0.z; lx1 = n0.w; ly1 = n1.x; lz1 = n1.y;
+        rx0 = n1.z; ry0 = n1.w; rz0 = n2.x; rx1 = n2.y; ry1 = n2.z; rz1 = n2.w;
+        refL = n3.x;
+        refR = n3.y;
+    } else {
+        const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(CNode));
+        const uint4 a = bload4u(cnodes, off);
+        const uint4 b = bload4u(cnodes, off + 16u);
+        const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
+        const float qx = __uint_as_float((a.w & 0xFFu) << 23);
+        const float qy = __uint_as_float(((a.w >> 8) & 0xFFu) << 23);
+        const float qz = __uint_as_float(((a.w >> 16) & 0xFFu) << 23);
+        auto u8 = [](uint32_t w, int k) { return static_cast<float>((w >> (8 * k)) & 0xFFu); };
+        lx0 = fmaf(qx, u8(b.x, 0), ox);
+        ly0 = fmaf(qy, u8(b.x, 1), oy);
+        lz0 = fmaf(qz, u8(b.x, 2), oz);
+        lx1 = fmaf(qx, u8(b.x, 3), ox);
+        ly1 = fmaf(qy, u8(b.y, 0), oy);
+        lz1 = fmaf(qz, u8(b.y, 1), oz);
+        rx0 = fmaf(qx, u8(b.y, 2), ox);
+        ry0 = fmaf(qy, u8(b.y, 3), oy);
+        rz0 = fmaf(qz, u8(b.z, 0), oz);
+        rx1 = fmaf(qx, u8(b.z, 1), ox);
+        ry1 = fmaf(qy, u8(b.z, 2), oy);
+        rz1 = fmaf(qz, u8(b.z, 3), oz);
+        const uint32_t meta = a.w >> 24;
+        const int v = static_cast<int>(b.w);
+        const int cL = static_cast<int>((meta >> 2) & 3u) + 1, cR = static_cast<int>((meta >> 4) & 3u) + 1;
+        const bool lLeaf = (meta & 1u) != 0, rLeaf = (meta & 2u) != 0;
+        refL = lLeaf ? leafRef(v, cL) : ref + 1;
+        refR = rLeaf ? leafRef(lLeaf ? v + cL : v, cR) : (lLeaf ? ref + 1 : v);
     }
-    if (hl && hr) {
-        int nearRef = n3.x, farRef = n3.y;
-        float farT = tr;
-        if (cull && tr < tl) {
-            nearRef = n3.y;
-            farRef = n3.x;
-            farT = tl;
-        }
-        st.push(farRef, farT);
-        return nearRef;
-    }
-    if (hl) return n3.x;
-    if (hr) return n3.y;
-    return popCulled(st, lim, cull);
+    if (count) cnt->nodes += 2;
+    float tl, tr;
+    const bool hl = slabFinite(lx0, ly0, lz0, lx1, ly1, lz1, o, inv, &tl);
+    const bool hr = slabFinite(rx0, ry0, rz0, rx1, ry1, rz1, o, inv, &tr);
+    return chooseChildren(hl, hr, tl, tr, refL, refR, lim, cull, st);
+}
+
+// The reference reaches a leaf iff its exact box passes (see innerStepC); finite 1/d only.
+__device__ __forceinline__ bool leafReachable(BufRes leafBoxes, int first, v3 o, v3 inv) {
+    const uint32_t off = static_cast<uint32_t>(first) * 32u;
+    const float4 a = bload4(leafBoxes, off);
+    const int2 b = bload2i(leafBoxes, off + 16u);
+    float te;
+    return slabFinite(a.x, a.y, a.z, a.w, __int_as_float(b.x), __int_as_float(b.y), o, inv, &te);
 }
 
 __device__ __forceinline__ void cas(float& ka, int& ra, float& kb, int& rb) {
@@ -146,7 +220,52 @@ __device__ __forceinline__ int innerStep4(const GNode4* node, v3 o, v3 inv, floa
 }
 
 
-template <bool kAny, bool kCount, int kWide, int kRefill, int kShards, int kTop, bool kFastSlab>
+// Position of the r-th (0-based) set bit of m (m must have more than r set bits).
+__device__ __forceinline__ int nthSetBit(uint64_t m, int r) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint64_t low = m & ((1ull << w) - 1ull);
+        const int c = __popcll(low);
+        if (r >= c) {
+            r -= c;
+            m >>= w;
+            pos += w;
+        }
+    }
+    return pos;
+}
+
+// Takes the bottom entry of a non-empty stack (the subtree nearest the root: the largest piece
+// of work to hand over); the top entry moves into its place.  Entry k lives in the global
+// spill area (gofs + k) while k < sp - depth, else in LDS slot k % depth.
+__device__ __forceinline__ int2 takeBottom(TStack& st) {
+    if (st.sp == 1) return st.pop();
+    const int2 top = st.pop();
+    int2 b;
+    if (st.sp > st.depth) {
+        b = st.gbase[st.gofs];
+        st.gbase[st.gofs] = top;
+    } else {
+        b = st.lds[0];
+        st.lds[0] = top;
+    }
+    return b;
+}
+
+// kAssist ("tail assist"): once the queue is empty, lanes without a ray help the rays still
+// walking in their wave.  A walking lane hands the bottom entry of its stack (a whole subtree)
+// to an idle lane, which walks it with a copy of the ray and the owner's best hit so far; when
+// the helper's walk ends its result is merged into the owner lane with the same total order
+// (betterThan) - closest hit and occlusion do not depend on the order in which subtrees are
+// walked, so results are identical.  The last rays of a launch (up to ~8x the mean walk) no
+// longer run on one lane each while the rest of the GPU idles.
+// kTrim: a wave that moves on from a drained cursor reads the next cursor before it takes from
+// it (a load instead of an atomic on an address every wave of the launch hits at the end).
+// kComp: compressed nodes (innerStepC) for all-finite waves, and a leaf's triangles count only
+// once its exact box passes (lanes with finite 1/d; the others only ever take exact steps).
+template <bool kAny, bool kCount, int kWide, int kRefill, int kShards, int kTop, bool kFastSlab, bool kAssist = false,
+          bool kTrim = false, bool kComp = false>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                                 TStack& st, TravCount* cnt, const GNode* ldsTop,
@@ -154,6 +273,9 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
     const int top = kTop > 0 ? min(kTop, s.triTop) : 0;
     const BufRes nodeBuf = bufferOf(s.triNodes);
     const BufRes triBuf = bufferOf(s.triGeom);
+    constexpr bool kC = kComp && !kCount;  // counting builds count the exact walk
+    const BufRes cnodeBuf = bufferOf(kC ? static_cast<const void*>(s.triCNodes) : static_cast<const void*>(s.triNodes));
+    const BufRes leafBuf = bufferOf(kC ? static_cast<const void*>(s.leafBoxes) : static_cast<const void*>(s.triNodes));
     const int lane = static_cast<int>(threadIdx.x & 63u);
     int rayIdx = -1;
     bool exhausted = false;
@@ -167,12 +289,64 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
     int leaf = 0;  // < 0: a postponed leaf
     int seg = static_cast<int>(blockIdx.x % kShards);  // wave-uniform cursor state
     int segsLeft = kShards;
+    constexpr bool kAs = kAssist && !kCount;  // counting builds keep the canonical per-ray walk
+    int helpOf = -1;     // kAs: the owner lane of the ray this lane helps with (-1: not helping)
+    int nHelp = 0;       // kAs, owner: helpers still walking parts of this lane's ray
+    bool occl = false;   // kAs && kAny: occlusion found (by this lane or a helper)
+    uint32_t t0 = 0;     // kAs: fetch time of this lane's ray (100 MHz ticks)
     while (true) {
+        if (kAs) {
+            // ---- helpers whose walk is over: merge into the owner lane (same total order) ----
+            uint64_t hm = __ballot(helpOf >= 0 && ref == kRefDone && leaf >= 0);
+            while (hm != 0) {
+                const int h = __ffsll(static_cast<unsigned long long>(hm)) - 1;
+                const int ho = __builtin_amdgcn_readlane(helpOf, h);
+                const float ht = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bt), h));
+                const uint32_t hc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bcode), h));
+                const int hocc = __builtin_amdgcn_readlane(static_cast<int>(occl), h);
+                if (lane == ho) {
+                    if (kAny) {
+                        occl = occl || hocc != 0;
+                    } else if (betterThan(ht, hc, bt, bcode)) {
+                        bt = ht;
+                        bcode = hc;
+                    }
+                    --nHelp;
+                }
+                hm &= hm - 1ull;
+            }
+            if (helpOf >= 0 && ref == kRefDone && leaf >= 0) {
+                helpOf = -1;
+                occl = false;
+            }
+            if (__ballot(helpOf >= 0) != 0) {
+                // helpers follow the owner: a closer hit tightens their culling; an occluded
+                // shadow ray needs no more walking
+                const int ol = helpOf >= 0 ? helpOf : lane;
+                const float obt = __shfl(bt, ol, 64);
+                const uint32_t oc = static_cast<uint32_t>(__shfl(static_cast<int>(bcode), ol, 64));
+                const int oo = __shfl(static_cast<int>(occl), ol, 64);
+                if (helpOf >= 0) {
+                    if (kAny) {
+                        if (oo != 0) {
+                            st.sp = 0;
+                            ref = kRefDone;
+                            leaf = 0;
+                        }
+                    } else if (betterThan(obt, oc, bt, bcode)) {
+                        bt = obt;
+                        bcode = oc;
+                    }
+                }
+            }
+        }
         // ---- lanes whose triangle walk is over: lights (closest only), write the result ----
-        if (rayIdx >= 0 && ref == kRefDone && leaf >= 0) {
+        if (rayIdx >= 0 && ref == kRefDone && leaf >= 0 && (!kAs || nHelp == 0)) {
             if (kCount) cnt->rayMax = max(cnt->rayMax, cnt->nodes - cnt->rayStart);
+            if (kAs) cnt->ticksMax = max(cnt->ticksMax, static_cast<uint32_t>(wall_clock64()) - t0);
             if (kAny) {
-                out[rayIdx].w = 0.0F;
+                out[rayIdx].w = (kAs && occl) ? 1.0F : 0.0F;
+                occl = false;
             } else {
                 for (int j = 0; j < s.nLights; ++j) {  // Shader.cpp:166-171
                     const float4* l = s.lights + 4 * j;
@@ -201,7 +375,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         bool need = rayIdx < 0 && !exhausted;
         uint64_t needMask = __ballot(need);
         // refill only once enough lanes are idle (fewer, larger fetches), or when none is busy
-        if (kRefill > 1 && __popcll(needMask) < kRefill && __ballot(rayIdx >= 0) != 0) {
+        if (kRefill > 1 && __popcll(needMask) < kRefill && __ballot(rayIdx >= 0 || helpOf >= 0) != 0) {
             need = false;
             needMask = 0;
         }
@@ -225,7 +399,15 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     const int segStart = static_cast<int>((static_cast<long long>(count) * seg) / kShards);
                     const int segEnd = static_cast<int>((static_cast<long long>(count) * (seg + 1)) / kShards);
                     int base = 0;
-                    if (lane == leader) base = atomicAdd(fetch + seg * kFetchStride, n);
+                    if (lane == leader) {
+                        int* cur = fetch + seg * kFetchStride;
+                        if (kTrim && segsLeft < kShards &&
+                            __hip_atomic_load(cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= segEnd - segStart) {
+                            base = segEnd - segStart;
+                        } else {
+                            base = atomicAdd(cur, n);
+                        }
+                    }
                     base = __shfl(base, leader, 64);
                     const bool mine = ((pending >> lane) & 1ull) != 0;
                     if (mine) {
@@ -242,6 +424,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             if (need) {
                 rayIdx = (got >= 0 && order != nullptr) ? order[got] : got;
                 if (kCount) cnt->rayStart = cnt->nodes;
+                if (kAs) t0 = static_cast<uint32_t>(wall_clock64());
                 if (rayIdx < 0) {
                     exhausted = true;
                 } else {
@@ -283,7 +466,58 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 }
             }
         }
-        if (__ballot(rayIdx >= 0) == 0) {
+        if (kAs) {
+            // ---- tail assist: idle lanes (queue empty) take a subtree of a walking lane ----
+            const bool idle = rayIdx < 0 && helpOf < 0 && exhausted;
+            const uint64_t idleMask = __ballot(idle);
+            const bool canGive = (rayIdx >= 0 || helpOf >= 0) && ref != kRefDone && st.sp > 0 && !(kAny && occl);
+            const uint64_t giveMask = __ballot(canGive);
+            if (idleMask != 0 && giveMask != 0) {
+                const int nPairs = min(__popcll(idleMask), __popcll(giveMask));
+                const bool gives = canGive && lanesBelowIn(giveMask) < nPairs;
+                if (gives) ++cnt->assists;
+                int2 e = make_int2(kRefDone, 0);
+                if (gives) e = takeBottom(st);
+                const int ir = lanesBelowIn(idleMask);
+                const bool takes = idle && ir < nPairs;
+                const int from = takes ? nthSetBit(giveMask, ir) : lane;
+                const int ownerOf = helpOf >= 0 ? helpOf : lane;
+                const int eRef = __shfl(e.x, from, 64);
+                const float eT = __int_as_float(__shfl(e.y, from, 64));
+                const int nOwner = __shfl(ownerOf, from, 64);
+                const v3 no{__shfl(o.x, from, 64), __shfl(o.y, from, 64), __shfl(o.z, from, 64)};
+                const v3 nd{__shfl(d.x, from, 64), __shfl(d.y, from, 64), __shfl(d.z, from, 64)};
+                const v3 ni{__shfl(inv.x, from, 64), __shfl(inv.y, from, 64), __shfl(inv.z, from, 64)};
+                const uint32_t nsrc = static_cast<uint32_t>(__shfl(static_cast<int>(src), from, 64));
+                const float nbt = __shfl(bt, from, 64);
+                const uint32_t nbc = static_cast<uint32_t>(__shfl(static_cast<int>(bcode), from, 64));
+                // owners count their new helpers (one per giving lane of their ray)
+                uint64_t gm = __ballot(gives);
+                while (gm != 0) {
+                    const int g = __ffsll(static_cast<unsigned long long>(gm)) - 1;
+                    if (lane == __builtin_amdgcn_readlane(ownerOf, g)) ++nHelp;
+                    gm &= gm - 1ull;
+                }
+                if (takes) {
+                    helpOf = nOwner;
+                    o = no;
+                    d = nd;
+                    inv = ni;
+                    src = nsrc;
+                    bt = nbt;
+                    bcode = nbc;
+                    occl = false;
+                    st.sp = 0;
+                    leaf = 0;
+                    ref = (s.cull != 0 && eT > bt + bt * kCullMargin) ? kRefDone : eRef;  // as popCulled
+                    if (ref < 0) {  // a leaf
+                        leaf = ref;
+                        ref = kRefDone;
+                    }
+                }
+            }
+        }
+        if (__ballot(rayIdx >= 0 || (kAs && helpOf >= 0)) == 0) {
             if (__ballot(!exhausted) == 0) break;
             continue;
         }
@@ -294,8 +528,12 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 ref = innerStep4(s.triNodes4 + ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
             } else {
                 const bool finite = kFastSlab && __ballot(!finiteInv(inv)) == 0;
-                ref = innerStep2<kTop>(nodeBuf, ldsTop, top, ref, o, inv, curLim, s.cull != 0, st, cnt, kCount,
-                                       finite);
+                if (kC && finite) {
+                    ref = innerStepC<kTop>(cnodeBuf, ldsTop, top, ref, o, inv, curLim, s.cull != 0, st, cnt, kCount);
+                } else {
+                    ref = innerStep2<kTop>(nodeBuf, ldsTop, top, ref, o, inv, curLim, s.cull != 0, st, cnt, kCount,
+                                           finite);
+                }
             }
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
@@ -307,6 +545,9 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         while (leaf < 0) {
             const int first = leafFirst(leaf), nprim = leafCount(leaf);
             bool hit = false;
+            // kC: whether the reference reaches this leaf, looked up at its first would-be hit
+            // (-1 not yet known; lanes with a non-finite 1/d walked exact nodes only)
+            int reach = (kC && finiteInv(inv)) ? -1 : 1;
             for (int k = 0; k < nprim; ++k) {
                 const int j = first + k;
                 const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
@@ -317,19 +558,24 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 if (!triTest(bload3(triBuf, off), bload3(triBuf, off + 16u), bload3(triBuf, off + 32u), o, d, &t, &u, &v))
                     continue;
                 if (t < kEpsilon) continue;
+                const bool cand = kAny ? !(t >= bt) : betterThan(t, code, bt, bcode);
+                if (!cand) continue;
+                if (kC && reach < 0) reach = leafReachable(leafBuf, first, o, inv) ? 1 : 0;
+                if (kC && reach == 0) break;  // the reference never tests this leaf's triangles
                 if (kAny) {
-                    if (!(t >= bt)) {
-                        hit = true;
-                        break;
-                    }
-                } else if (betterThan(t, code, bt, bcode)) {
-                    bt = t;
-                    bcode = code;
+                    hit = true;
+                    break;
                 }
+                bt = t;
+                bcode = code;
             }
             if (kAny && hit) {
-                out[rayIdx].w = 1.0F;
-                rayIdx = -1;
+                if (kAs) {
+                    occl = true;  // written when the helpers of this ray are done
+                } else {
+                    out[rayIdx].w = 1.0F;
+                    rayIdx = -1;
+                }
                 st.sp = 0;
                 ref = kRefDone;
                 leaf = 0;

@@ -8,10 +8,13 @@ from mobileraytracer_amd import scenes
 
 def main():
     o, l, c = scenes.conference()
+    # RANKS=N: rank 0's shard of an N-GPU frame (packed output), the per-GPU work at N GPUs
+    ranks = int(os.environ.get("RANKS", 1))
     cfg = m.Config(width=1920, height=1080, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5,
-                   objFilePath=o, mtlFilePath=l, camFilePath=c)
+                   objFilePath=o, mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=ranks)
     r = m.Renderer(cfg)
-    d = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+    d = torch.zeros(max(1920 * 1080, r.scene_info()["pixelSlotsMax"]), dtype=torch.int32, device="cuda")
+    bm, pk = (d.data_ptr(), 0) if ranks == 1 else (0, d.data_ptr())
     sh = torch.cuda.current_stream().cuda_stream
     # "V[:O[:S[:P[:M]]]]": trace variant V, shadow-stream overlap O (default 1), ray sorting S
     # (default 0), chunk pipelines P (default 1), streaming mode M (default 0)
@@ -28,13 +31,13 @@ def main():
             r.set_tuning(4, int(parts[2]))
             r.set_tuning(5, int(parts[3]))
             r.set_tuning(6, int(parts[4]))
-            r.render_frame_device(d.data_ptr(), 0, sh)
+            r.render_frame_device(bm, pk, sh)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             n = 5
             tr = shw = shd = 0.0
             for _ in range(n):
-                r.render_frame_device(d.data_ptr(), 0, sh)
+                r.render_frame_device(bm, pk, sh)
                 st = r.frame_stats()
                 tr += st["traceMs"]; shw += st["shadowMs"]; shd += st["shadeMs"]
             torch.cuda.synchronize()
