@@ -251,7 +251,9 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
 
     std::vector<GNode> g;
     DScene& d = r->ds;
-    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop);
+    // node layout below the LDS top: 0 depth-first pre-order, 1 random (diagnostic), 2 line pairs
+    const char* nl = std::getenv("MRT_NODE_LAYOUT");
+    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop, nl != nullptr ? std::atoi(nl) : 0);
     d.triNodes = r->sceneMem.upload(g, st);
     {
         std::vector<CNode> cn;

@@ -835,7 +835,7 @@ template std::vector<HBVHNode> buildBVH<HSphere>(std::vector<HSphere>*, std::vec
 // so a parent and its left child usually share a 128-byte line.  Node numbering does not
 // affect results (boxes, child order and leaves are the reference's).
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
-                 int topCount, int* topPlaced) {
+                 int topCount, int* topPlaced, int layout) {
     out->clear();
     if (topPlaced != nullptr) *topPlaced = 0;
     const HBVHNode& r = nodes[0];
@@ -868,17 +868,54 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
         if (inner(l + 1)) bfs.push_back(l + 1);
     }
     if (topPlaced != nullptr) *topPlaced = static_cast<int>(order.size());
+    const size_t topEnd = order.size();
+    auto place = [&](int32_t i) {
+        newIdx[static_cast<size_t>(i)] = static_cast<int32_t>(order.size());
+        order.push_back(i);
+    };
     std::vector<int32_t> dfs{0};
-    while (!dfs.empty()) {
-        const int32_t i = dfs.back();
-        dfs.pop_back();
-        if (newIdx[static_cast<size_t>(i)] < 0) {
-            newIdx[static_cast<size_t>(i)] = static_cast<int32_t>(order.size());
-            order.push_back(i);
+    if (layout == 2) {
+        // line pairs: a node at an even index and, right after it (same 128-byte line), its
+        // inner child with the larger box surface - the likelier next visit
+        auto area = [&](int32_t j) {
+            const v3 e = nodes[static_cast<size_t>(j)].box.mx - nodes[static_cast<size_t>(j)].box.mn;
+            return e.x * e.y + e.y * e.z + e.z * e.x;
+        };
+        while (!dfs.empty()) {
+            const int32_t i = dfs.back();
+            dfs.pop_back();
+            bool fresh = false;
+            if (newIdx[static_cast<size_t>(i)] < 0) {
+                if (order.size() % 2 != 0) order.push_back(-1);  // padding slot
+                place(i);
+                fresh = true;
+            }
+            const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
+            int32_t a = inner(l) ? l : -1, b = inner(l + 1) ? l + 1 : -1;
+            if (a >= 0 && b >= 0 && area(b) > area(a)) std::swap(a, b);
+            if (a < 0) std::swap(a, b);
+            if (fresh && a >= 0 && newIdx[static_cast<size_t>(a)] < 0) place(a);
+            if (b >= 0) dfs.push_back(b);
+            if (a >= 0) dfs.push_back(a);
         }
-        const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
-        if (inner(l + 1)) dfs.push_back(l + 1);
-        if (inner(l)) dfs.push_back(l);
+    } else {
+        while (!dfs.empty()) {
+            const int32_t i = dfs.back();
+            dfs.pop_back();
+            if (newIdx[static_cast<size_t>(i)] < 0) place(i);
+            const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
+            if (inner(l + 1)) dfs.push_back(l + 1);
+            if (inner(l)) dfs.push_back(l);
+        }
+        if (layout == 1) {  // diagnostic: the nodes below the top in a fixed random order
+            std::vector<int32_t> rest(order.begin() + static_cast<std::ptrdiff_t>(topEnd), order.end());
+            std::mt19937 rng(12345u);
+            std::shuffle(rest.begin(), rest.end(), rng);
+            for (size_t k = 0; k < rest.size(); ++k) {
+                order[topEnd + k] = rest[k];
+                newIdx[static_cast<size_t>(rest[k])] = static_cast<int32_t>(topEnd + k);
+            }
+        }
     }
     auto ref = [&](int32_t j) {
         const HBVHNode& c = nodes[static_cast<size_t>(j)];
@@ -887,6 +924,10 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
     root->ref = 0;
     out->resize(order.size());
     for (size_t k = 0; k < order.size(); ++k) {
+        if (order[k] < 0) {  // padding
+            (*out)[k] = GNode{};
+            continue;
+        }
         const int32_t l = nodes[static_cast<size_t>(order[k])].indexOffset;
         const HBVHNode& L = nodes[static_cast<size_t>(l)];
         const HBVHNode& R = nodes[static_cast<size_t>(l + 1)];

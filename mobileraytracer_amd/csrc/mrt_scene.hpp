@@ -124,7 +124,7 @@ std::vector<HBVHNode> buildBVH(std::vector<T>* prims, std::vector<int32_t>* orde
 
 // Converts reference nodes to the device child-box layout.
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
-                 int topCount = 0, int* topPlaced = nullptr);
+                 int topCount = 0, int* topPlaced = nullptr, int layout = 0);
 // Collapses the reference BVH2 into 4-wide nodes (greedy: open the largest-area inner child
 // until four children), depth-first order.  root->ref is BVH4 node 0 or a leaf ref.
 void toDeviceBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode4>* out, GRoot* root);
