@@ -260,6 +260,30 @@ def test_trace_kernel_variants_are_identical():
             assert all(np.array_equal(a, b) for a, b in zip(hits, outs[0][3]))
 
 
+def test_node_layouts_and_compressed_nodes_are_invariant(monkeypatch):
+    """Node numbering below the LDS top (depth-first, random, line pairs; MRT_NODE_LAYOUT) and
+    the compressed-node walk (variants 19-21, which need the depth-first numbering and fall back
+    to the exact walk otherwise) change nothing; assist variants report handed-over subtrees."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5)
+    outs = []
+    for layout in ("0", "1", "2"):
+        monkeypatch.setenv("MRT_NODE_LAYOUT", layout)
+        with m.Renderer(cfg) as r:
+            for v in (14, 19, 21):
+                r.set_tuning(1, v)
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"]))
+                # compressed variants run only on the depth-first numbering
+                assert r.get_tuning(1) == (v if layout == "0" or v == 14 else 14)
+                if r.get_tuning(1) == 21:
+                    assert st["assistedSubtrees"] > 0 and st["maxRayMicros"] > 0
+    for bm, rays, shadows in outs[1:]:
+        assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
+
+
 def test_shadow_stream_overlap_is_invariant():
     """Any-hit launches on their own stream (overlapping the next level), ray reordering before
     traversal and concurrent chunk pipelines change nothing."""
