@@ -130,6 +130,11 @@ int mrt_primary_hits(mrt_renderer *r, int32_t *kind, int32_t *index, float *t);
  * (min xyz, max xyz), offsets[N] / counts[N] (BVHNode::indexOffset / numPrimitives) and
  * order[triangles] (input index of each triangle in BVH order). */
 int64_t mrt_triangle_bvh(const mrt_config *cfg, float *boxes, int32_t *offsets, int32_t *counts, int32_t *order);
+/* Host only: decode a map_Kd texture file as the renderer does (Texture::createTexture,
+ * Texture.cpp:83-114: 8-bit channels with stb_image's conventions).  Returns the byte count
+ * width*height*channels (and fills dims[3] = width, height, channels) or -1; with non-NULL
+ * texels copies the image, row-major, channels interleaved. */
+int64_t mrt_decode_texture(const char *path, int32_t *dims, uint8_t *texels);
 
 #ifdef __cplusplus
 }

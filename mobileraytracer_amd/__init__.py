@@ -174,6 +174,19 @@ def triangle_bvh(config: Config):
     return boxes, off, cnt, order[:int(cnt[0])] if n == 1 else order
 
 
+def decode_texture(path: str) -> np.ndarray:
+    """A map_Kd texture decoded as the renderer loads it (Texture::createTexture,
+    Texture.cpp:83-114): (height, width, channels) uint8.  Host only."""
+    lib = _native.lib()
+    dims = np.zeros(3, np.int32)
+    n = lib.mrt_decode_texture(path.encode(), _ptr(dims), None)
+    if n < 0:
+        raise RuntimeError(lib.mrt_last_error().decode())
+    out = np.empty(int(n), np.uint8)
+    lib.mrt_decode_texture(path.encode(), _ptr(dims), _ptr(out))
+    return out.reshape(int(dims[1]), int(dims[0]), int(dims[2]))
+
+
 _active: List[Renderer] = []
 
 

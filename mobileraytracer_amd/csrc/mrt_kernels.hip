@@ -414,6 +414,43 @@ __device__ __forceinline__ int hitMaterial(const DScene& s, uint32_t code) {
     return __float_as_int(s.spheres[2 * j + 1].x);
 }
 
+// Texture::loadColor (Texture.cpp:37-48): the nearest texel, no wrapping (coordinates are in
+// [0, 1)); the first three bytes from the texel on (a 1- or 2-channel texture reads into the next
+// texel, as the reference does; the last texel is clamped where the reference reads past the end).
+__device__ __forceinline__ v3 loadColor(const DScene& s, int tex, float tx, float ty) {
+    const int4 ti = s.texInfo[tex];
+    const int32_t u = static_cast<int32_t>(tx * static_cast<float>(ti.x));
+    const int32_t v = static_cast<int32_t>(ty * static_cast<float>(ti.y));
+    uint32_t index = static_cast<uint32_t>(v * ti.x * ti.z + u * ti.z);
+    const uint32_t size = static_cast<uint32_t>(ti.x * ti.y * ti.z);
+    index = min(index, size >= 3u ? size - 3u : 0u);
+    const uint8_t* p = s.texels + ti.w + index;
+    return v3{static_cast<float>(p[0]) / 255.0F, static_cast<float>(p[1]) / 255.0F, static_cast<float>(p[2]) / 255.0F};
+}
+
+// Shader::rayTrace (Shader.cpp:112-120): a hit on a textured material with texture coordinates
+// >= 0 overwrites that material's Kd with the texel.  The reference's Kd_ is shared by every hit
+// on the material and read by reference in the shaders, so a shade() that traces a child first
+// and reads Kd afterwards sees the last texel written in the child's subtree; k_resolve replays
+// that from the per-vertex records this function fills.  Returns (texel, material index) or w = -1.
+__device__ __forceinline__ float4 textureWrite(const DScene& s, float4 h) {
+    const float4 none = make_float4(0.0F, 0.0F, 0.0F, -1.0F);
+    const uint32_t code = fbits(h.w);
+    if (primKind(code) != kTriangle) return none;
+    const uint32_t j = primIndex(code);
+    const int mat = __float_as_int(s.triShade[3 * j].w);
+    if (mat < 0) return none;
+    const int tex = __float_as_int(s.mats[4 * mat + 1].w);
+    if (tex < 0) return none;
+    const float4 a = s.triTex[2 * j], b = s.triTex[2 * j + 1];
+    const float w = 1.0F - h.y - h.z;  // Triangle.cpp:96-98: tA * w + tB * u + tC * v
+    const float tx = (a.x * w + a.z * h.y) + b.x * h.z;
+    const float ty = (a.y * w + a.w * h.y) + b.y * h.z;
+    if (!(tx >= 0.0F && ty >= 0.0F)) return none;
+    const v3 c = loadColor(s, tex, tx, ty);
+    return make_float4(c.x, c.y, c.z, static_cast<float>(mat));
+}
+
 // Shader::getCosineSampleHemisphere (Shader.cpp:188-216); cos/sin evaluated in double and
 // rounded, which agrees with glibc cosf/sinf except in rare last-ulp cases.
 __device__ __forceinline__ v3 cosineHemisphere(v3 n, float r1, float r2) {
@@ -473,9 +510,11 @@ struct ShadeState {
     int nShadow, nChild;
 };
 
+// kw: textureWrite of this hit (w >= 0: the material's Kd is that texel when shade() runs)
 template <int kShader>
 __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, float4 d4, float4 h, uint32_t tc,
-                                                   int level, const ShadeArgs& a) {
+                                                   int level, const ShadeArgs& a,
+                                                   float4 kw = make_float4(0.0F, 0.0F, 0.0F, -1.0F)) {
     ShadeState v{};
     v.terminal = true;
     v.leaf = make_float4(0.0F, 0.0F, 0.0F, 0.0F);
@@ -504,7 +543,7 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
         const float4 le4 = m[0];
         Le = xyz(le4);
         v.ior = le4.w;
-        Kd = xyz(m[1]);
+        Kd = kw.w >= 0.0F ? xyz(kw) : xyz(m[1]);
         Ks = xyz(m[2]);
         Kt = xyz(m[3]);
     }
@@ -631,7 +670,16 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
         const int i = base + static_cast<int>(threadIdx.x);
         const bool active = i < count;
         ShadeState v{};
-        if (active) v = shadePrepare<kShader>(s, lv.rO[i], lv.rD[i], lv.hit[i], lv.tree[i], level, a);
+        if (active) {
+            const float4 h = lv.hit[i];
+            float4 kw = make_float4(0.0F, 0.0F, 0.0F, -1.0F);
+            if (s.textured != 0) {  // also at the depth cap: rayTrace writes Kd before shade() returns
+                kw = textureWrite(s, h);
+                lv.kd[i] = kw;
+                lv.last[i] = kw;
+            }
+            v = shadePrepare<kShader>(s, lv.rO[i], lv.rD[i], h, lv.tree[i], level, a, kw);
+        }
         int childBase, shadowBase;
         blockAllocPair(pair, active ? v.nChild : 0, active ? v.nShadow : 0, &childBase, &shadowBase, allocLds, parity);
         parity ^= 1;
@@ -699,6 +747,10 @@ __global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int
                 Kd = xyz(m[1]);
                 Ks = xyz(m[2]);
                 Kt = xyz(m[3]);
+                if (s.textured != 0) {
+                    const float4 kw = textureWrite(s, h);
+                    if (kw.w >= 0.0F) Kd = xyz(kw);
+                }
             }
             if (kShader == kShaderDepthMap) {
                 const v3 mp{a.maxPoint[0], a.maxPoint[1], a.maxPoint[2]};
@@ -762,7 +814,20 @@ __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, i
         if (vb.z >= nx.cap) vb.z = -1;
         const int nShadow = va.w >> 3;
         const float4* m = s.mats + 4 * va.x;
-        const v3 Kd = xyz(m[1]), Ks = xyz(m[2]), Kt = xyz(m[3]);
+        v3 Kd = xyz(m[1]);
+        const v3 Ks = xyz(m[2]), Kt = xyz(m[3]);
+        // textured scenes: Kd as shade() reads it - this hit's texel until a child's subtree
+        // writes the material again (exact while at most one material is textured: the subtree
+        // records keep only its last write)
+        float4 lD = make_float4(0.0F, 0.0F, 0.0F, -1.0F), lS = lD, lT = lD, own = lD;
+        if (s.textured != 0) {
+            own = lv.kd[i];
+            if (own.w >= 0.0F) Kd = xyz(own);
+            if (vb.x >= 0) lD = nx.last[vb.x];
+            if (vb.y >= 0) lS = nx.last[vb.y];
+            if (vb.z >= 0) lT = nx.last[vb.z];
+        }
+        const float matF = static_cast<float>(va.x);
         const bool direct = hasPositive(Kd) && s.nLights > 0;
         v3 Ld{0.0F, 0.0F, 0.0F};
         if (direct) {
@@ -780,7 +845,9 @@ __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, i
             v3 rgb = Ld;
             if (hasPositive(Ks) && vb.y >= 0) rgb = rgb + Ks * xyz(nx.res[vb.y]);
             if (hasPositive(Kt) && vb.z >= 0) rgb = rgb + Kt * xyz(nx.res[vb.z]);
-            rgb = rgb + Kd * 0.1F;
+            // the ambient term reads Kd after the specular and transmission subtrees
+            const v3 KdAmb = lT.w == matF ? xyz(lT) : ((lT.w < 0.0F && lS.w == matF) ? xyz(lS) : Kd);
+            rgb = rgb + KdAmb * 0.1F;
             out = make_float4(rgb.x, rgb.y, rgb.z, 0.0F);
         } else {  // PathTracer.cpp:127-142
             v3 LiD{0.0F, 0.0F, 0.0F}, LiS{0.0F, 0.0F, 0.0F}, LiT{0.0F, 0.0F, 0.0F};
@@ -788,7 +855,8 @@ __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, i
             if (vb.x >= 0) {
                 const float4 r = nx.res[vb.x];
                 hitLight = r.w != 0.0F;
-                LiD = LiD + Kd * xyz(r);
+                const v3 KdD = lD.w == matF ? xyz(lD) : Kd;  // Kd after the diffuse subtree
+                LiD = LiD + KdD * xyz(r);
                 if (level > kRayDepthMin) LiD = LiD / (0.5F * 0.5F);
                 if (hasPositive(Ld) && hitLight) LiD = v3{0.0F, 0.0F, 0.0F};
             }
@@ -802,6 +870,7 @@ __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, i
             out = make_float4(rgb.x, rgb.y, rgb.z, hitLight ? 1.0F : 0.0F);
         }
         lv.res[i] = out;
+        if (s.textured != 0) lv.last[i] = lT.w >= 0.0F ? lT : (lS.w >= 0.0F ? lS : (lD.w >= 0.0F ? lD : own));
     }
 }
 
@@ -941,6 +1010,7 @@ void launchStreamV(const DScene& s, const StreamArgs& A, int* counters, int2* gs
 bool launchStream(int shader, const DScene& s, const Level* lv, int nLevels, uint32_t epoch, const ShadeArgs& a,
                   int* counters, int2* gstack, int gdepth, int maxThreads, hipStream_t st) {
     if (shader != kShaderWhitted && shader != kShaderPathTracer) return false;
+    if (s.textured != 0) return false;  // the Kd replay of textured scenes needs the level-by-level resolve
     if (s.variant != 14 && s.variant != 13 && s.variant != 8) return false;
     StreamArgs A{};
     for (int l = 0; l < kMaxLevels; ++l) A.lv[l] = lv[l];

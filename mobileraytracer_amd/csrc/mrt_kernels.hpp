@@ -65,6 +65,10 @@ struct Level {
     uint32_t* sReady;        // the same for the shadow ray slots
     const int* order;        // trace visit order of the rays (null: queue order)
     const int* shadowOrder;  // the same for the shadow rays
+    // textured scenes: the texel this vertex's hit wrote into its material's Kd (xyz, w = the
+    // material index, -1 none), and the last such write in the vertex's subtree (Shader.cpp:112-120)
+    float4* kd;
+    float4* last;
     int cap;
     int shadowCap;
 };

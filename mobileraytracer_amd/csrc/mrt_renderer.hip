@@ -304,6 +304,29 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     }
     d.triShade = r->sceneMem.upload(v, st);
     v.clear();
+    // textures: triangle texture coordinates, texture table and texels (textured scenes only)
+    d.textured = 0;
+    for (const HMaterial& m : sc.materials) d.textured |= (m.texId >= 0 && !sc.textures.empty()) ? 1 : 0;
+    if (d.textured != 0) {
+        for (const HTriangle& t : sc.triangles) {
+            v.push_back(make_float4(t.tA.x, t.tA.y, t.tB.x, t.tB.y));
+            v.push_back(make_float4(t.tC.x, t.tC.y, 0.0F, 0.0F));
+        }
+        d.triTex = r->sceneMem.upload(v, st);
+        v.clear();
+        std::vector<int4> info;
+        std::vector<uint8_t> bytes;
+        for (const HTexture& t : sc.textures) {
+            info.push_back(make_int4(t.width, t.height, t.channels, static_cast<int>(bytes.size())));
+            bytes.insert(bytes.end(), t.texels.begin(), t.texels.end());
+        }
+        d.texInfo = r->sceneMem.upload(info, st);
+        d.texels = r->sceneMem.upload(bytes, st);
+    } else {
+        d.triTex = nullptr;
+        d.texInfo = nullptr;
+        d.texels = nullptr;
+    }
     for (const HPlane& p : sc.planes) {
         v.push_back(f4(p.normal, asFloat(p.mat)));
         v.push_back(f4(p.point, 0.0F));
@@ -332,7 +355,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     v.clear();
     for (const HMaterial& m : sc.materials) {
         v.push_back(f4(m.Le, m.ior));
-        v.push_back(f4(m.Kd, 0.0F));
+        v.push_back(f4(m.Kd, asFloat(m.texId)));  // w: texture index (-1 none)
         v.push_back(f4(m.Ks, 0.0F));
         v.push_back(f4(m.Kt, 0.0F));
     }
@@ -430,6 +453,9 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
                 lv.res = nullptr;
                 lv.sC = nullptr;
             }
+            const bool tex = real && r->ds.textured != 0;
+            lv.kd = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
+            lv.last = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
         }
         auto sortBufs = [&](mrt_renderer::SortBufs* b, size_t cap) {
             b->cap = static_cast<int>(cap);
@@ -978,6 +1004,23 @@ int64_t mrt_triangle_bvh(const mrt_config* cfg, float* boxes, int32_t* offsets, 
             counts[i] = b.numPrimitives;
         }
         std::memcpy(order, perm.data(), perm.size() * sizeof(int32_t));
+    });
+    return rc == 0 ? n : -1;
+}
+
+int64_t mrt_decode_texture(const char* path, int32_t* dims, uint8_t* texels) {
+    int64_t n = -1;
+    const int rc = guarded([&] {
+        mrt::HTexture t;
+        std::string err;
+        if (!mrt::loadTextureFile(path != nullptr ? path : "", &t, &err)) throw std::runtime_error(err);
+        n = static_cast<int64_t>(t.texels.size());
+        if (dims != nullptr) {
+            dims[0] = t.width;
+            dims[1] = t.height;
+            dims[2] = t.channels;
+        }
+        if (texels != nullptr) std::memcpy(texels, t.texels.data(), t.texels.size());
     });
     return rc == 0 ? n : -1;
 }

@@ -573,6 +573,24 @@ bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene
         }
     }
 
+    // map_Kd textures, loaded once per file name (OBJLoader.cpp:224-242) from the OBJ's directory
+    // (the reference reads filePath + texname, filePath being the OBJ's directory)
+    std::unordered_map<std::string, int32_t> texCache;
+    const std::string objDir = objPath.find('/') == std::string::npos ? std::string() : objPath.substr(0, objPath.rfind('/') + 1);
+    auto textureOf = [&](const std::string& name) -> int32_t {
+        auto it = texCache.find(name);
+        if (it != texCache.end()) return it->second;
+        HTexture tex;
+        std::string terr;
+        int32_t id = -1;
+        if (loadTextureFile(objDir + name, &tex, &terr)) {  // Texture::isValid (Texture.cpp:137-139)
+            id = static_cast<int32_t>(scene->textures.size());
+            scene->textures.push_back(std::move(tex));
+        }
+        texCache[name] = id;
+        return id;
+    };
+    auto fract = [](float x) { return x - std::floor(x); };  // glm::fract (Utils.cpp:177-180)
     const bool hasNormals = !vns.empty();
     auto vert = [&vs](int i) { return v3{-vs[3 * i], vs[3 * i + 1], vs[3 * i + 2]}; };  // OBJLoader.cpp:139-141
     auto nrm = [&vns](int i) { return v3{-vns[3 * i], vns[3 * i + 1], vns[3 * i + 2]}; }; // :170-172
@@ -590,6 +608,7 @@ bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene
             na = nb = nc = normalize(cross(ac, ab));  // OBJLoader.cpp:176-182
         }
         HMaterial m;
+        v2 texA = noTex, texB = noTex, texC = noTex;
         if (tr.mat >= 0) {
             const RawMat& rm = mats[static_cast<size_t>(tr.mat)];
             m.Kd = v3{rm.diffuse[0], rm.diffuse[1], rm.diffuse[2]};
@@ -597,7 +616,25 @@ bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene
             m.Kt = v3{rm.transmittance[0], rm.transmittance[1], rm.transmittance[2]} * (1.0F - rm.dissolve);
             m.Le = normalizeColor(v3{rm.emission[0], rm.emission[1], rm.emission[2]});
             m.ior = rm.ior;
-            m.texture = "";  // textures are not sampled on this path
+            // OBJLoader.cpp:332-364: a texture and texture coordinates -> the texture and the
+            // corners' coordinates wrapped into [0, 1); an invalid texture -> coordinates -1
+            if (!rm.diffuseTex.empty() && !vts.empty()) {
+                m.texture = rm.diffuseTex;
+                m.texId = textureOf(rm.diffuseTex);
+                if (m.texId < 0) m.texture = "";  // unreadable: the reference would throw (Texture.cpp:88-92)
+                bool allVt = true;
+                for (int k = 0; k < 3; ++k) allVt = allVt && tr.i[k].vt >= 0;
+                if (m.texId >= 0 && allVt) {
+                    v2 tc[3];
+                    for (int k = 0; k < 3; ++k) {
+                        const int t = tr.i[k].vt;
+                        tc[k] = v2{fract(vts[2 * static_cast<size_t>(t)]), fract(vts[2 * static_cast<size_t>(t) + 1])};
+                    }
+                    texA = tc[0];
+                    texB = tc[1];
+                    texC = tc[2];
+                }
+            }
         } else {
             const int vi = tr.i[0].v;  // OBJLoader.cpp:423-433 vertex colour of the first vertex
             m.Kd = v3{cols[3 * vi], cols[3 * vi + 1], cols[3 * vi + 2]};
@@ -622,7 +659,7 @@ bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene
             matIndex = static_cast<int32_t>(scene->materials.size());
             scene->materials.push_back(m);
         }
-        scene->triangles.push_back(makeTriangle(a, b, c, na, nb, nc, noTex, noTex, noTex, matIndex));
+        scene->triangles.push_back(makeTriangle(a, b, c, na, nb, nc, texA, texB, texC, matIndex));
     }
     return true;
 }

@@ -22,8 +22,18 @@ struct v2 {
 struct HMaterial {
     v3 Le{0, 0, 0}, Kd{0, 0, 0}, Ks{0, 0, 0}, Kt{0, 0, 0};
     float ior{1.0F};
-    std::string texture;  // map_Kd file name ("" = none); textures are not sampled
+    std::string texture;  // map_Kd file name ("" = none)
+    int32_t texId{-1};    // index into HScene::textures (-1: none)
 };
+
+// Texture (Texture.hpp): 8-bit channels as stb_image returns them (Texture.cpp:83-114)
+struct HTexture {
+    int32_t width{0}, height{0}, channels{0};
+    std::vector<uint8_t> texels;
+};
+// mrt_texture.cpp: PNG bytes -> texture (stb_image's conventions); false + err when unsupported
+bool decodePng(const std::vector<uint8_t>& file, HTexture* out, std::string* err);
+bool loadTextureFile(const std::string& path, HTexture* out, std::string* err);
 bool materialEqual(const HMaterial& a, const HMaterial& b);  // Material.cpp:106-115
 
 // Triangle.hpp:18-27 (field order kept: AC, AB, A, normals, texcoords, material)
@@ -68,6 +78,7 @@ struct HScene {
     std::vector<HTriangle> triangles;
     std::vector<HLight> lights;
     std::vector<HMaterial> materials;
+    std::vector<HTexture> textures;  // map_Kd images, cached by file name (OBJLoader.cpp:224-242)
 };
 
 // Reference BVH node (BVH.hpp:56-60): box, indexOffset (leaf: first prim; inner: left),

@@ -24,6 +24,7 @@
 //   * the OBJ fill is single-threaded in file order; textures are not sampled;
 //   * each pixel receives its samples in order (no tile-claim race, Renderer.cpp:190-193).
 #include <algorithm>
+#include <map>
 #include <array>
 #include <atomic>
 #include <cmath>
@@ -96,6 +97,27 @@ inline bool hasPositiveValue(const Vec3& v) { return v[0] > 0 || v[1] > 0 || v[2
 struct Vec2 {
     float x, y;
 };
+inline Vec2 operator*(const Vec2& a, float s) { return Vec2{a.x * s, a.y * s}; }
+inline Vec2 operator+(const Vec2& a, const Vec2& b) { return Vec2{a.x + b.x, a.y + b.y}; }
+
+// Texture (Texture.cpp): 8-bit channels as stb_image returns them.  The oracle does not decode
+// images itself: oracle.py decodes PNGs (its own decoder) and registers them by path.
+struct Texture {
+    int32_t width = 0, height = 0, channels = 0;
+    std::vector<uint8_t> image;
+    Vec3 loadColor(const Vec2& tc) const {  // Texture.cpp:37-48
+        const int32_t u = static_cast<int32_t>(tc.x * width);
+        const int32_t v = static_cast<int32_t>(tc.y * height);
+        size_t index = static_cast<uint32_t>(v * width * channels + u * channels);
+        if (index + 3 > image.size()) index = image.size() >= 3 ? image.size() - 3 : 0;  // the reference reads past the end
+        return Vec3(static_cast<float>(image[index + 0]) / 255.0F, static_cast<float>(image[index + 1]) / 255.0F,
+                    static_cast<float>(image[index + 2]) / 255.0F);
+    }
+};
+std::map<std::string, Texture>& textureRegistry() {
+    static std::map<std::string, Texture> r;
+    return r;
+}
 
 bool equalF(float a, float b) { return std::fabs(a - b) < Epsilon; }
 bool equalV(const Vec3& a, const Vec3& b) { return equalF(a[0], b[0]) && equalF(a[1], b[1]) && equalF(a[2], b[2]); }
@@ -172,10 +194,13 @@ struct Ray {  // Ray.hpp:19-45
 struct Material {  // Material.hpp:18-43
     Vec3 Le, Kd, Ks, Kt;
     float ior = 1.0F;
+    std::string texture;          // map_Kd name ("" none)
+    const Texture* tex = nullptr;
     Material() = default;
     Material(Vec3 kd, Vec3 ks = Vec3(), Vec3 kt = Vec3(), float r = 1.0F, Vec3 le = Vec3()) : Le(le), Kd(kd), Ks(ks), Kt(kt), ior(r) {}
-    bool operator==(const Material& o) const {
-        return equalV(Kd, o.Kd) && equalV(Ks, o.Ks) && equalV(Kt, o.Kt) && equalV(Le, o.Le) && equalF(ior, o.ior);
+    bool operator==(const Material& o) const {  // Material.cpp:36-45
+        return equalV(Kd, o.Kd) && equalV(Ks, o.Ks) && equalV(Kt, o.Kt) && equalV(Le, o.Le) && equalF(ior, o.ior) &&
+               texture == o.texture;
     }
 };
 
@@ -188,6 +213,7 @@ struct Intersection {  // Intersection.hpp:16-27, copied by value through every 
     int32_t materialIndex = -1;
     int kind = 0;      // oracle bookkeeping for hit-id dumps: 1 plane 2 sphere 3 triangle 4 light
     int64_t index = -1;
+    Vec2 texCoords{-1.0F, -1.0F};
     Ray ray;
     Intersection(Ray r, float dist = RayLengthMax) : length(dist), ray(r) {}
 };
@@ -260,6 +286,7 @@ struct Triangle {  // Triangle.hpp:18-27 (AoS, 100 bytes of payload)
         const float w = 1.0F - u - v;
         Intersection res(intersection.ray, distanceToIntersection);
         res.normal = normalize(normalA * w + normalB * u + normalC * v);
+        res.texCoords = texA * w + texB * u + texC * v;
         res.point = intersection.ray.origin + intersection.ray.direction * distanceToIntersection;
         res.primitive = this;
         res.materialIndex = materialIndex;
@@ -782,6 +809,7 @@ struct Tok {
 struct MtlEntry {
     float kd[3] = {0, 0, 0}, ks[3] = {0, 0, 0}, tf[3] = {0, 0, 0}, ke[3] = {0, 0, 0};
     float ior = 1.0F, dissolve = 1.0F;
+    std::string mapKd;
 };
 
 bool startsKey(const char* t, const char* key) {
@@ -820,6 +848,12 @@ bool loadObj(const std::string& objPath, const std::string& mtlPath, Scene* scen
             else if (startsKey(t.p, "Ni")) { t.p += 2; m.ior = t.real(); }
             else if (startsKey(t.p, "d")) { t.p += 1; m.dissolve = t.real(); hasD = true; }
             else if (startsKey(t.p, "Tr")) { t.p += 2; const float v = t.real(); if (!hasD) m.dissolve = 1.0F - v; }
+            else if (startsKey(t.p, "map_Kd")) {
+                t.p += 6;
+                t.skip();
+                m.mapKd = t.p;
+                while (!m.mapKd.empty() && (m.mapKd.back() == ' ' || m.mapKd.back() == '\t')) m.mapKd.pop_back();
+            }
         }
         if (have) {
             names[current] = static_cast<int>(mats.size());
@@ -831,11 +865,11 @@ bool loadObj(const std::string& objPath, const std::string& mtlPath, Scene* scen
         *err = "cannot open " + objPath;
         return false;
     }
-    std::vector<float> vs, vn, cols;
+    std::vector<float> vs, vn, vt, cols;
     std::string line;
     int material = -1;
     int64_t faceCounter = 0;
-    struct Idx { int v, n; };
+    struct Idx { int v, n, t; };
     std::vector<Idx> face;
     std::vector<std::array<Idx, 3>> tris;
     std::vector<int> triMat;
@@ -854,19 +888,25 @@ bool loadObj(const std::string& objPath, const std::string& mtlPath, Scene* scen
             t.p += 2;
             const float x = t.real(), y = t.real(), z = t.real();
             vn.insert(vn.end(), {x, y, z});
+        } else if (p[0] == 'v' && p[1] == 't' && (p[2] == ' ' || p[2] == '\t')) {
+            t.p += 2;
+            const float u = t.real(), v = t.real();
+            vt.insert(vt.end(), {u, v});
         } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
             face.clear();
             const char* q = p + 2;
-            const int nv = static_cast<int>(vs.size() / 3), nn = static_cast<int>(vn.size() / 3);
+            const int nv = static_cast<int>(vs.size() / 3), nn = static_cast<int>(vn.size() / 3),
+                      nt = static_cast<int>(vt.size() / 2);
             auto fix = [](int i, int n) { return i > 0 ? i - 1 : (i == 0 ? 0 : n + i); };
             while (true) {
                 while (*q == ' ' || *q == '\t') ++q;
                 if (*q == 0) break;
-                Idx id{fix(std::atoi(q), nv), -1};
+                Idx id{fix(std::atoi(q), nv), -1, -1};
                 while (*q && *q != '/' && *q != ' ' && *q != '\t') ++q;
                 if (*q == '/') {
                     ++q;
-                    if (*q != '/') {  // texcoord (unused)
+                    if (*q != '/') {  // texcoord
+                        id.t = fix(std::atoi(q), nt);
                         while (*q && *q != '/' && *q != ' ' && *q != '\t') ++q;
                     }
                     if (*q == '/') {
@@ -909,6 +949,7 @@ bool loadObj(const std::string& objPath, const std::string& mtlPath, Scene* scen
         }
         const int mid = triMat[k];
         Material mat;
+        Vec2 tcs[3] = {Vec2{-1.0F, -1.0F}, Vec2{-1.0F, -1.0F}, Vec2{-1.0F, -1.0F}};
         if (mid >= 0) {
             const MtlEntry& e = mats[static_cast<size_t>(mid)];
             Vec3 emission(e.ke[0], e.ke[1], e.ke[2]);
@@ -916,6 +957,22 @@ bool loadObj(const std::string& objPath, const std::string& mtlPath, Scene* scen
             if (mx > 1.0F) emission = emission / mx;  // Utils.cpp:189-196
             mat = Material(Vec3(e.kd[0], e.kd[1], e.kd[2]), Vec3(e.ks[0], e.ks[1], e.ks[2]),
                            Vec3(e.tf[0], e.tf[1], e.tf[2]) * (1.0F - e.dissolve), e.ior, emission);
+            // OBJLoader.cpp:332-364: texture + coordinates wrapped into [0, 1) (glm::fract)
+            if (!e.mapKd.empty() && !vt.empty()) {
+                const std::string dir = objPath.find('/') == std::string::npos ? "" : objPath.substr(0, objPath.rfind('/') + 1);
+                auto it = textureRegistry().find(dir + e.mapKd);
+                if (it != textureRegistry().end()) {
+                    mat.texture = e.mapKd;
+                    mat.tex = &it->second;
+                    if (f[0].t >= 0 && f[1].t >= 0 && f[2].t >= 0) {
+                        auto fr = [](float x) { return x - std::floor(x); };
+                        for (int j = 0; j < 3; ++j) {
+                            const int ti = f[static_cast<size_t>(j)].t;
+                            tcs[j] = Vec2{fr(vt[2 * static_cast<size_t>(ti)]), fr(vt[2 * static_cast<size_t>(ti) + 1])};
+                        }
+                    }
+                }
+            }
             if (hasPositiveValue(emission)) {
                 Light l;
                 l.area = true;
@@ -937,7 +994,11 @@ bool loadObj(const std::string& objPath, const std::string& mtlPath, Scene* scen
             mi = static_cast<int32_t>(scene->materials.size());
             scene->materials.push_back(mat);
         }
-        scene->triangles.push_back(Triangle::build(v[0], v[1], v[2], &n[0], &n[1], &n[2], mi));
+        Triangle tri = Triangle::build(v[0], v[1], v[2], &n[0], &n[1], &n[2], mi);
+        tri.texA = tcs[0];
+        tri.texB = tcs[1];
+        tri.texC = tcs[2];
+        scene->triangles.push_back(tri);
     }
     return true;
 }
@@ -992,6 +1053,7 @@ struct Engine {
 
     struct Ctx {
         uint32_t key;
+        std::vector<Material>* mats;  // this thread's materials: rayTrace writes textured Kd (Shader.cpp:116-120)
     };
 
     Intersection traceLights(Intersection it) const {  // Shader.cpp:166-171
@@ -1021,7 +1083,12 @@ struct Engine {
         Intersection it(ray);
         const float lastDist = it.length;
         it = closest(it);
-        if (it.materialIndex >= 0) it.material = &materials[static_cast<size_t>(it.materialIndex)];
+        if (it.materialIndex >= 0) {  // Shader.cpp:112-121
+            Material& material = (*ctx.mats)[static_cast<size_t>(it.materialIndex)];
+            it.material = &material;
+            if (it.texCoords.x >= 0 && it.texCoords.y >= 0 && material.tex != nullptr)
+                material.Kd = material.tex->loadColor(it.texCoords);
+        }
         return it.length < lastDist && shade(rgb, it, ctx, tc);
     }
 
@@ -1238,6 +1305,9 @@ struct Engine {
         const int W = cfg.width, H = cfg.height, bx = W / 16, by = H / 16;
         std::atomic<size_t> next{0};
         auto worker = [&]() {
+            // per-thread materials: the reference shares them between render threads (a textured
+            // hit writes Kd_ that another thread may read); single-threaded order is the contract
+            std::vector<Material> mats = materials;
             while (true) {
                 const size_t n = next.fetch_add(1);
                 if (n >= list.size()) break;
@@ -1252,7 +1322,7 @@ struct Engine {
                             uint32_t key;
                             const Ray ray = cameraRay(x, y, sample, &key);
                             Vec3 pixelRgb;
-                            rayTrace(&pixelRgb, ray, Ctx{key}, 1u);
+                            rayTrace(&pixelRgb, ray, Ctx{key, &mats}, 1u);
                             bitmap[idx] = incrementalAvg(pixelRgb, bitmap[idx], sample + 1);
                         }
                     }
@@ -1313,6 +1383,16 @@ struct OracleConfig {
     const char* mtl;
     const char* cam;
 };
+
+// a decoded texture for map_Kd lookups (path as the loader forms it: OBJ directory + name)
+void oracle_register_texture(const char* path, int32_t width, int32_t height, int32_t channels, const uint8_t* data) {
+    oracle::Texture t;
+    t.width = width;
+    t.height = height;
+    t.channels = channels;
+    t.image.assign(data, data + static_cast<size_t>(width) * static_cast<size_t>(height) * static_cast<size_t>(channels));
+    oracle::textureRegistry()[path] = std::move(t);
+}
 
 void* oracle_create(const OracleConfig* c) {
     oracle::Config cfg{c->width, c->height, c->shader, c->sceneIndex, c->samplesPixel, c->samplesLight,

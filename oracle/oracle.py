@@ -66,8 +66,107 @@ def lib():
         L.oracle_fast_arctan.restype = ctypes.c_float
         L.oracle_fast_arctan.argtypes = [ctypes.c_float]
         L.oracle_selftest_partition.argtypes = [ctypes.c_uint32, ctypes.c_int]
+        L.oracle_register_texture.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp]
         _lib = L
     return _lib
+
+
+def decode_png(path):
+    """PNG -> (height, width, channels) uint8 with stb_image's conventions (Texture.cpp:83-114:
+    stbi_load_from_memory, req_comp 0): palette -> RGB (RGBA with tRNS), tRNS key adds alpha to
+    grey / RGB, grey below 8 bits scaled to 0..255, 16-bit samples -> high byte.  Non-interlaced."""
+    import struct
+    import zlib
+    data = open(path, "rb").read()
+    if data[:8] != b"\x89PNG\r\n\x1a\n":
+        raise ValueError("not a PNG")
+    pos, idat, plte, trns, hdr = 8, b"", b"", b"", None
+    while pos + 8 <= len(data):
+        n, kind = struct.unpack(">I4s", data[pos:pos + 8])
+        body = data[pos + 8:pos + 8 + n]
+        pos += 12 + n
+        if kind == b"IHDR":
+            hdr = struct.unpack(">IIBBBBB", body)
+        elif kind == b"PLTE":
+            plte = body
+        elif kind == b"tRNS":
+            trns = body
+        elif kind == b"IDAT":
+            idat += body
+        elif kind == b"IEND":
+            break
+    w, h, depth, ctype, _, _, interlace = hdr
+    if interlace:
+        raise ValueError("interlaced PNG")
+    chans = {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}[ctype]
+    row = (w * chans * depth + 7) // 8
+    bpp = max(1, chans * depth // 8)
+    raw = zlib.decompress(idat)
+    out = np.zeros((h, row), np.int32)
+    prev = np.zeros(row, np.int32)
+    for y in range(h):
+        f = raw[y * (row + 1)]
+        cur = np.frombuffer(raw, np.uint8, row, y * (row + 1) + 1).astype(np.int32)
+        rec = np.zeros(row, np.int32)
+        for x in range(row):
+            a = rec[x - bpp] if x >= bpp else 0
+            b = prev[x]
+            c = prev[x - bpp] if x >= bpp else 0
+            if f == 0:
+                pred = 0
+            elif f == 1:
+                pred = a
+            elif f == 2:
+                pred = b
+            elif f == 3:
+                pred = (a + b) // 2
+            else:
+                p = a + b - c
+                pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
+                pred = a if (pa <= pb and pa <= pc) else (b if pb <= pc else c)
+            rec[x] = (cur[x] + pred) & 0xFF
+        out[y] = rec
+        prev = rec
+    # samples
+    if depth == 8:
+        s = out[:, :w * chans].reshape(h, w, chans)
+    elif depth == 16:
+        s = (out[:, 0::2][:, :w * chans] << 8 | out[:, 1::2][:, :w * chans]).reshape(h, w, chans)
+    else:
+        per = 8 // depth
+        bits = np.zeros((h, row * per), np.int32)
+        for k in range(per):
+            bits[:, k::per] = (out >> (8 - depth * (k + 1))) & ((1 << depth) - 1)
+        s = bits[:, :w * chans].reshape(h, w, chans)
+    if ctype == 3:
+        pal = np.frombuffer(plte, np.uint8).reshape(-1, 3)
+        img = pal[s[:, :, 0]]
+        if trns:
+            alpha = np.full(256, 255, np.uint8)
+            alpha[:len(trns)] = np.frombuffer(trns, np.uint8)
+            img = np.concatenate([img, alpha[s[:, :, 0]][:, :, None]], 2)
+        return np.ascontiguousarray(img.astype(np.uint8))
+    img = (s >> 8) if depth == 16 else (s * {1: 0xFF, 2: 0x55, 4: 0x11, 8: 1}[depth])
+    if trns and ctype in (0, 2):
+        key = np.array(struct.unpack(">" + "H" * chans, trns[:2 * chans]))
+        alpha = np.where(np.all(s == key, axis=2), 0, 255)
+        img = np.concatenate([img, alpha[:, :, None]], 2)
+    return np.ascontiguousarray(img.astype(np.uint8))
+
+
+def register_textures(obj, mtl):
+    """Decode the map_Kd images an MTL names (beside the OBJ) and hand them to the oracle."""
+    if not mtl or not os.path.exists(mtl):
+        return
+    base = os.path.dirname(obj)
+    for line in open(mtl):
+        t = line.strip().split(None, 1)
+        if len(t) == 2 and t[0] == "map_Kd":
+            path = os.path.join(base, t[1].strip()) if base else t[1].strip()
+            if os.path.exists(path):
+                img = decode_png(path)
+                lib().oracle_register_texture(path.encode(), img.shape[1], img.shape[0], img.shape[2],
+                                              img.ctypes.data)
 
 
 def fvec(*v):
@@ -82,6 +181,8 @@ class Oracle:
                  obj="", mtl="", cam=""):
         self.width, self.height = width, height
         self._keep = [s.encode() for s in (obj, mtl, cam)]
+        if obj:
+            register_textures(obj, mtl)
         c = _Cfg(width, height, shader, sceneIndex, samplesPixel, samplesLight, maxDepth, *self._keep)
         self._h = lib().oracle_create(ctypes.byref(c))
         if not self._h:

@@ -33,6 +33,9 @@ CASES = {
     "water128_whitted": dict(width=128, height=128, shader=1, sceneIndex=-1, scene="water"),
     "water128_pt4": dict(width=128, height=128, shader=2, sceneIndex=-1, samplesPixel=4, scene="water"),
     "teapot128_whitted": dict(width=128, height=128, shader=1, sceneIndex=-1, scene="teapot"),
+    # the teapot's material is textured (map_Kd default.png): texel Kd, shared-Kd replay
+    "teapot128_pt4": dict(width=128, height=128, shader=2, sceneIndex=-1, samplesPixel=4, scene="teapot"),
+    "teapot128_diffuse": dict(width=128, height=128, shader=4, sceneIndex=-1, scene="teapot"),
     "conference96_whitted": dict(width=96, height=96, shader=1, sceneIndex=-1, scene="conference"),
     "conference96_pt4": dict(width=96, height=96, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5,
                              scene="conference"),

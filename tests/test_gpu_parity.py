@@ -82,7 +82,8 @@ def assert_within_tolerance(gpu, ref, mask=None):
 @pytest.mark.parametrize("case", [
     dict(width=512, height=512),                                 # C2 Cornell built-in
     dict(width=128, height=128, scene="water"),
-    dict(width=128, height=128, scene="teapot"),
+    dict(width=128, height=128, scene="teapot"),                 # textured (map_Kd): texel Kd, shared-Kd replay
+    dict(width=256, height=256, scene="teapot", max_depth=6),
     dict(width=96, height=96, scene="conference"),
     dict(width=30, height=30),                                   # the reference engine tests' size
     dict(width=100, height=60),                                  # non-multiple-of-16 tiling
@@ -105,7 +106,8 @@ def test_primary_hits_bit_exact(oracle_mod, case):
     dict(width=256, height=256),                                 # C1
     dict(width=512, height=512),
     dict(width=128, height=128, scene="water"),
-    dict(width=128, height=128, scene="teapot"),
+    dict(width=128, height=128, scene="teapot"),                 # textured (map_Kd): texel Kd, shared-Kd replay
+    dict(width=256, height=256, scene="teapot", max_depth=6),
     dict(width=96, height=96, scene="conference"),
     dict(width=30, height=30),
     dict(width=100, height=60),
@@ -134,6 +136,8 @@ def test_whitted_bit_exact(oracle_mod, case):
     dict(width=96, height=96, scene="conference", shader=0),
     dict(width=96, height=96, scene="conference", shader=4),
     dict(width=96, height=96, scene="conference", shader=3),
+    dict(width=128, height=128, scene="teapot", shader=4),           # DiffuseMaterial: the texel
+    dict(width=128, height=128, scene="teapot", shader=0),           # NoShadows with texel Kd
     dict(width=100, height=60, sceneIndex=3, shader=2, spp=2),       # PathTracer: tolerance below
 ])
 def test_other_scenes_and_shaders(oracle_mod, case):
@@ -183,6 +187,7 @@ def test_c1_matches_committed_fixture():
     dict(width=96, height=96, spp=4, max_depth=5, scene="conference"),
     dict(width=64, height=64, spp=2, spl=2, scene="water"),
     dict(width=128, height=128, spp=4, sceneIndex=2),             # area lights + transmission sphere
+    dict(width=128, height=128, spp=4, scene="teapot"),           # textured Kd read after the diffuse child
 ])
 def test_pathtracer_within_tolerance(oracle_mod, case):
     cfg = make_cfg(shader=2, **case)
