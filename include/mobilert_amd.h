@@ -45,7 +45,8 @@ typedef struct mrt_config {
     int32_t samplesPixel;
     int32_t samplesLight;
     int32_t repeats;
-    int32_t accelerator;  /* 3 BVH (Shader.hpp:20-24); other values are served by the BVH */
+    int32_t accelerator;  /* Shader.hpp:20-24: 1 Naive, 2 RegularGrid (served by the BVH), 3 BVH;
+                             any other value builds no accelerator (only lights are hit) */
     int32_t printStdOut;
     const char *objFilePath;
     const char *mtlFilePath;

@@ -47,6 +47,12 @@ struct DScene {
     const int4* texInfo;       // per texture: width, height, channels, first byte in texels
     const uint8_t* texels;
     int32_t textured;
+    // Config::accelerator (Shader.hpp:20-24): 1 Naive, 2 RegularGrid (served by the BVH), 3 BVH,
+    // anything else builds no accelerator (only lights are hit, Shader.cpp:86-111)
+    int32_t accel;
+    const int* triNaive;       // Naive: BVH-order index of the i-th triangle / plane / sphere of the input
+    const int* planeNaive;
+    const int* sphereNaive;
 };
 
 __device__ __forceinline__ float4 ld4(const float4* p) { return *p; }
@@ -151,7 +157,8 @@ __device__ __forceinline__ bool betterThan(float t, uint32_t code, float bt, uin
 }
 __device__ __forceinline__ bool better(float t, uint32_t code, const Best& b) { return betterThan(t, code, b.t, b.code); }
 
-template <bool kAny>
+// kTies: the BVH walks' total order (equal t: lower index); false: Naive's plain `<` in input order
+template <bool kAny, bool kTies = true>
 __device__ __forceinline__ bool leafTriangles(const DScene& s, int first, int count, v3 o, v3 d, uint32_t src,
                                               Best* b, uint32_t* nTri) {
     for (int k = 0; k < count; ++k) {
@@ -165,7 +172,7 @@ __device__ __forceinline__ bool leafTriangles(const DScene& s, int first, int co
         if (t < kEpsilon) continue;
         if (kAny) {
             if (!(t >= b->t)) return true;
-        } else if (better(t, code, *b)) {
+        } else if (kTies ? better(t, code, *b) : !(t >= b->t)) {
             b->t = t;
             b->u = u;
             b->v = v;
@@ -175,7 +182,8 @@ __device__ __forceinline__ bool leafTriangles(const DScene& s, int first, int co
     return false;
 }
 
-template <bool kAny>
+// kTies: the BVH walks' total order (equal t: lower index); false: Naive's plain `<` in input order
+template <bool kAny, bool kTies = true>
 __device__ __forceinline__ bool leafPlanes(const DScene& s, int first, int count, v3 o, v3 d, uint32_t src, Best* b) {
     for (int k = 0; k < count; ++k) {  // Plane.cpp:38-72
         const int j = first + k;
@@ -191,7 +199,7 @@ __device__ __forceinline__ bool leafPlanes(const DScene& s, int first, int count
         if (t < kEpsilon) continue;
         if (kAny) {
             if (!(t >= b->t)) return true;
-        } else if (better(t, code, *b)) {
+        } else if (kTies ? better(t, code, *b) : !(t >= b->t)) {
             b->t = t;
             b->u = 0.0F;
             b->v = 0.0F;
@@ -201,7 +209,7 @@ __device__ __forceinline__ bool leafPlanes(const DScene& s, int first, int count
     return false;
 }
 
-template <bool kAny>
+template <bool kAny, bool kTies = true>
 __device__ __forceinline__ bool leafSpheres(const DScene& s, int first, int count, v3 o, v3 d, Best* b) {
     for (int k = 0; k < count; ++k) {  // Sphere.cpp:42-81 (no self-exclusion)
         const int j = first + k;
@@ -222,7 +230,7 @@ __device__ __forceinline__ bool leafSpheres(const DScene& s, int first, int coun
         const uint32_t code = encodePrim(kSphere, static_cast<uint32_t>(j));
         if (kAny) {
             if (!(t >= b->t)) return true;
-        } else if (better(t, code, *b)) {
+        } else if (kTies ? better(t, code, *b) : !(t >= b->t)) {
             b->t = t;
             b->u = 0.0F;
             b->v = 0.0F;
@@ -242,6 +250,21 @@ struct TravCount {
 };
 
 // Generic BVH walk.  kKind selects the leaf routine.  Returns true on an any-hit.
+// Naive::intersect (Naive.hpp): every primitive in input order, planes, spheres, triangles
+// (Shader.cpp:90-94), each test rejecting t >= the current best (so ties go to the earlier
+// primitive); a shadow ray returns at its first hit closer than its distance.  No boxes.
+template <bool kAny>
+__device__ __forceinline__ bool naiveWalk(const DScene& s, v3 o, v3 d, uint32_t src, Best* b) {
+    uint32_t nTri = 0;
+    for (int i = 0; i < s.planeRoot.count; ++i)
+        if (leafPlanes<kAny, false>(s, s.planeNaive[i], 1, o, d, src, b)) return true;
+    for (int i = 0; i < s.sphereRoot.count; ++i)
+        if (leafSpheres<kAny, false>(s, s.sphereNaive[i], 1, o, d, b)) return true;
+    for (int i = 0; i < s.triRoot.count; ++i)
+        if (leafTriangles<kAny, false>(s, s.triNaive[i], 1, o, d, src, b, &nTri)) return true;
+    return false;
+}
+
 template <int kKind, bool kAny>
 __device__ __forceinline__ bool traverse(const DScene& s, const GNode* nodes, const GRoot& root, v3 o, v3 d, v3 inv,
                                          uint32_t src, Best* b, TStack& st, TravCount* cnt) {

@@ -380,6 +380,39 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
     }
 }
 
+// Closest hit (kAny false: lv.rO / rD -> lv.hit) or shadow test (true: lv.sO / sD -> lv.sC.w)
+// without the BVH: Naive (accelerator 1) walks every primitive; any other id except 2 / 3
+// builds no accelerator in the reference, so only the area lights can be hit.
+template <bool kAny>
+__global__ __launch_bounds__(256) void k_trace_other(DScene s, Level lv, int* counters, int level) {
+    const int count = kAny ? min(counters[cntShadows(level)], lv.shadowCap) : min(counters[cntRays(level)], lv.cap);
+    for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
+         i += static_cast<int>(gridDim.x * blockDim.x)) {
+        const float4 o4 = kAny ? lv.sO[i] : lv.rO[i];
+        const float4 d4 = kAny ? lv.sD[i] : lv.rD[i];
+        const v3 o = xyz(o4), d = xyz(d4);
+        const uint32_t src = kAny ? fbits(o4.w) : fbits(d4.w);
+        Best b{kAny ? d4.w : kRayLengthMax, 0.0F, 0.0F, kNoPrim};
+        bool occluded = false;
+        if (s.accel == kAccNaive) occluded = naiveWalk<kAny>(s, o, d, src, &b);
+        if (kAny) {
+            lv.sC[i].w = occluded ? 1.0F : 0.0F;
+            continue;
+        }
+        for (int j = 0; j < s.nLights; ++j) {  // Shader.cpp:166-171
+            const float4* l = s.lights + 4 * j;
+            const float4 a4 = l[0];
+            if (__float_as_int(a4.w) != 1) continue;
+            float t, u, v;
+            if (!triTest(a4, l[1], l[2], o, d, &t, &u, &v)) continue;
+            if (t < kEpsilon) continue;
+            const uint32_t code = encodePrim(kLight, static_cast<uint32_t>(j));
+            if (betterThan(t, code, b.t, b.code)) b = Best{t, u, v, code};
+        }
+        lv.hit[i] = make_float4(b.t, b.u, b.v, bitsf(b.code));
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 struct HitGeom {
     v3 P, N;
@@ -1011,6 +1044,7 @@ bool launchStream(int shader, const DScene& s, const Level* lv, int nLevels, uin
                   int* counters, int2* gstack, int gdepth, int maxThreads, hipStream_t st) {
     if (shader != kShaderWhitted && shader != kShaderPathTracer) return false;
     if (s.textured != 0) return false;  // the Kd replay of textured scenes needs the level-by-level resolve
+    if (s.accel != kAccBVH && s.accel != kAccGrid) return false;
     if (s.variant != 14 && s.variant != 13 && s.variant != 8) return false;
     StreamArgs A{};
     for (int l = 0; l < kMaxLevels; ++l) A.lv[l] = lv[l];
@@ -1048,6 +1082,7 @@ bool traceVariantCompressed(int variant) {
 
 bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,
                  int gdepth, unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
+    if (s.accel != kAccBVH && s.accel != kAccGrid) return false;
     switch (s.variant) {
         MRT_LAUNCH_COMBO_ONE(1)
         MRT_LAUNCH_COMBO_ONE(2)
@@ -1078,11 +1113,19 @@ bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* count
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
+    if (s.accel != kAccBVH && s.accel != kAccGrid) {
+        hipLaunchKernelGGL((k_trace_other<false>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
+        return;
+    }
     MRT_LAUNCH_TRACE(k_trace, 0);
 }
 
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
+    if (s.accel != kAccBVH && s.accel != kAccGrid) {
+        hipLaunchKernelGGL((k_trace_other<true>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
+        return;
+    }
     MRT_LAUNCH_TRACE(k_shadow, 1);
 }
 

@@ -13,6 +13,9 @@ constexpr int kShaderNoShadows = 5;   // C_wrapper.cpp:188-193 (the switch's def
 constexpr int kMaxLevels = 16;           // max ray depth + 2
 constexpr int kTraceVariants = 22;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
 constexpr int kDefaultTraceVariant = 14;
+constexpr int kAccNaive = 1;  // Shader::Accelerator (Shader.hpp:20-24)
+constexpr int kAccGrid = 2;
+constexpr int kAccBVH = 3;
 constexpr int kExactTraceVariant = 14;    // stands in for compressed variants when a scene has no CNodes
 constexpr int kTopNodesMax = 128;        // BVH2 nodes numbered breadth-first (LDS-staged by some variants)
 

@@ -360,6 +360,16 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
         v.push_back(f4(m.Kt, 0.0F));
     }
     d.mats = r->sceneMem.upload(v, st);
+    // Naive (accelerator 1): the BVH-order index of each primitive in input order
+    d.accel = r->cfg.accelerator;
+    auto inverse = [](const std::vector<int32_t>& order) {
+        std::vector<int32_t> inv(std::max<size_t>(order.size(), 1), 0);
+        for (size_t j = 0; j < order.size(); ++j) inv[static_cast<size_t>(order[j])] = static_cast<int32_t>(j);
+        return inv;
+    };
+    d.triNaive = r->sceneMem.upload(inverse(r->triOrder), st);
+    d.planeNaive = r->sceneMem.upload(inverse(r->planeOrder), st);
+    d.sphereNaive = r->sceneMem.upload(inverse(r->sphereOrder), st);
     d.nLights = static_cast<int32_t>(sc.lights.size());
     d.nMats = static_cast<int32_t>(sc.materials.size());
     d.cull = r->cfg.cull;

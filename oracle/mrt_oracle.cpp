@@ -1036,6 +1036,7 @@ struct Config {
     const char* obj;
     const char* mtl;
     const char* cam;
+    int32_t accelerator;  // Shader::Accelerator (Shader.hpp:20-24)
 };
 
 struct Engine {
@@ -1047,6 +1048,9 @@ struct Engine {
     std::unique_ptr<BVH<Plane>> planes;
     std::unique_ptr<BVH<Sphere>> spheres;
     std::unique_ptr<BVH<Triangle>> triangles;
+    std::vector<Plane> naivePlanes;  // input order (Naive accelerator)
+    std::vector<Sphere> naiveSpheres;
+    std::vector<Triangle> naiveTriangles;
     std::vector<float> shaderTable, samplerTable;
     std::atomic<uint64_t> rays{0};
     int64_t numTriangles = 0;
@@ -1071,12 +1075,33 @@ struct Engine {
         return it;
     }
 
-    Intersection closest(Intersection it) const {
-        it = planes->intersect(it);
-        it = spheres->intersect(it);
-        it = triangles->intersect(it);
-        return traceLights(it);
+    // Naive<T>::intersect (Naive.hpp): every primitive in input order; a shadow ray returns at its
+    // first hit closer than its distance
+    template <class T>
+    static Intersection naive(const std::vector<T>& prims, Intersection it) {
+        const float lastDist = it.length;
+        for (const T& p : prims) {
+            it = p.intersect(it);
+            if (it.ray.shadowTrace && it.length < lastDist) return it;
+        }
+        return it;
     }
+
+    // Shader.cpp:88-110: the accelerator switch (an id other than 1-3 builds none: only lights hit)
+    Intersection geometry(Intersection it) const {
+        if (cfg.accelerator == 1) {
+            it = naive(naivePlanes, it);
+            it = naive(naiveSpheres, it);
+            it = naive(naiveTriangles, it);
+        } else if (cfg.accelerator == 2 || cfg.accelerator == 3) {  // RegularGrid served by the BVH
+            it = planes->intersect(it);
+            it = spheres->intersect(it);
+            it = triangles->intersect(it);
+        }
+        return it;
+    }
+
+    Intersection closest(Intersection it) const { return traceLights(geometry(it)); }
 
     // Shader::rayTrace (Shader.cpp:86-123); tc = vertex code in the ray tree
     bool rayTrace(Vec3* rgb, const Ray& ray, Ctx ctx, uint32_t tc) {
@@ -1095,9 +1120,7 @@ struct Engine {
     // Shader::shadowTrace (Shader.cpp:132-158)
     bool shadowTrace(float distance, const Ray& ray) const {
         Intersection it(ray, distance);
-        it = planes->intersect(it);
-        it = spheres->intersect(it);
-        it = triangles->intersect(it);
+        it = geometry(it);
         return it.length < distance;
     }
 
@@ -1367,6 +1390,9 @@ Engine* create(const Config& cfg) {
     e->planes = std::make_unique<BVH<Plane>>(s.planes);
     e->spheres = std::make_unique<BVH<Sphere>>(s.spheres);
     e->triangles = std::make_unique<BVH<Triangle>>(s.triangles);
+    e->naivePlanes = s.planes;
+    e->naiveSpheres = s.spheres;
+    e->naiveTriangles = s.triangles;
     e->shaderTable = haltonTable(0x4D525400u);
     e->samplerTable = haltonTable(0x4D525401u);
     return e.release();
@@ -1382,6 +1408,7 @@ struct OracleConfig {
     const char* obj;
     const char* mtl;
     const char* cam;
+    int32_t accelerator;
 };
 
 // a decoded texture for map_Kd lookups (path as the loader forms it: OBJ directory + name)
@@ -1396,7 +1423,7 @@ void oracle_register_texture(const char* path, int32_t width, int32_t height, in
 
 void* oracle_create(const OracleConfig* c) {
     oracle::Config cfg{c->width, c->height, c->shader, c->sceneIndex, c->samplesPixel, c->samplesLight,
-                       c->maxDepth > 0 ? c->maxDepth : 6, c->obj, c->mtl, c->cam};
+                       c->maxDepth > 0 ? c->maxDepth : 6, c->obj, c->mtl, c->cam, c->accelerator};
     return oracle::create(cfg);
 }
 

@@ -21,7 +21,8 @@ def build():
 class _Cfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
                 ("width", "height", "shader", "sceneIndex", "samplesPixel", "samplesLight", "maxDepth")] + \
-               [("obj", ctypes.c_char_p), ("mtl", ctypes.c_char_p), ("cam", ctypes.c_char_p)]
+               [("obj", ctypes.c_char_p), ("mtl", ctypes.c_char_p), ("cam", ctypes.c_char_p),
+                ("accelerator", ctypes.c_int32)]
 
 
 _lib = None
@@ -178,12 +179,12 @@ class Oracle:
     """CPU reference renderer for one configuration (same meaning as mobileraytracer_amd.Config)."""
 
     def __init__(self, width, height, shader=1, sceneIndex=0, samplesPixel=1, samplesLight=1, maxDepth=6,
-                 obj="", mtl="", cam=""):
+                 obj="", mtl="", cam="", accelerator=3):
         self.width, self.height = width, height
         self._keep = [s.encode() for s in (obj, mtl, cam)]
         if obj:
             register_textures(obj, mtl)
-        c = _Cfg(width, height, shader, sceneIndex, samplesPixel, samplesLight, maxDepth, *self._keep)
+        c = _Cfg(width, height, shader, sceneIndex, samplesPixel, samplesLight, maxDepth, *self._keep, accelerator)
         self._h = lib().oracle_create(ctypes.byref(c))
         if not self._h:
             raise RuntimeError("oracle could not load the scene")

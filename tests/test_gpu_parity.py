@@ -53,7 +53,8 @@ def gpu_hits(cfg):
 
 def oracle_for(oracle_mod, cfg):
     return oracle_mod.Oracle(cfg.width, cfg.height, cfg.shader, cfg.sceneIndex, cfg.samplesPixel, cfg.samplesLight,
-                             cfg.maxDepth, obj=cfg.objFilePath, mtl=cfg.mtlFilePath, cam=cfg.camFilePath)
+                             cfg.maxDepth, obj=cfg.objFilePath, mtl=cfg.mtlFilePath, cam=cfg.camFilePath,
+                             accelerator=cfg.accelerator)
 
 
 def oracle_render(oracle_mod, cfg, first_tile=0, num_tiles=1 << 30):
@@ -152,6 +153,35 @@ def test_other_scenes_and_shaders(oracle_mod, case):
         assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
         assert rays == ref_rays
     assert len(np.unique(bm)) > 1
+
+
+# ---- accelerators (Shader.cpp:48-70, 86-158): Naive walks every primitive in input order (no
+# boxes, ties to the earlier primitive); ids outside 1-3 build none (only lights are hit) -----------
+@pytest.mark.parametrize("case", [
+    dict(width=128, height=128, shader=1, accelerator=1),                   # Cornell: planes, spheres, triangle
+    dict(width=64, height=64, shader=1, scene="water", accelerator=1),      # 7,088 triangles
+    dict(width=128, height=128, sceneIndex=2, shader=1, accelerator=1),     # area lights, transmission
+    dict(width=64, height=64, sceneIndex=3, shader=0, accelerator=1),       # NoShadows
+    dict(width=64, height=64, sceneIndex=2, shader=1, accelerator=0),       # no accelerator
+    dict(width=64, height=64, sceneIndex=0, shader=2, spp=2, accelerator=1),  # PathTracer: tolerance
+])
+def test_naive_and_missing_accelerator(oracle_mod, case):
+    cfg = make_cfg(**case)
+    bm, rays, _ = gpu_render(cfg)
+    ref, ref_rays = oracle_render(oracle_mod, cfg)
+    once = coverage(cfg.width, cfg.height) == 1
+    if cfg.shader == 2:
+        assert_within_tolerance(bm, ref, once & (ref != SENTINEL))
+        assert abs(rays - ref_rays) <= 0.002 * ref_rays, (rays, ref_rays)
+    else:
+        assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
+        assert rays == ref_rays
+    if cfg.accelerator == 1 and cfg.shader == 1:  # primary hit ids, bit-exact
+        g = gpu_hits(cfg)
+        o = oracle_for(oracle_mod, cfg)
+        r = o.primary_hits()
+        o.close()
+        assert all(np.array_equal(a, b) for a, b in zip(g, r))
 
 
 def test_unknown_shader_ids_are_noshadows():
