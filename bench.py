@@ -138,11 +138,13 @@ def main():
     t0 = time.perf_counter()
     trace_ms = 0.0
     trace_launches = 0
+    walked = 0  # closest-hit rays traversed + shadow rays: the rays whose walk ran
     for _ in range(args.steps):
         step()
         st = r.frame_stats()
         trace_ms += st["traceMs"]
         trace_launches += st["traceLaunches"]
+        walked += st["walkedRays"] + st["shadowRays"]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -154,15 +156,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=red)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        n = torch.tensor([rays], dtype=torch.float64, device=red)
+        n = torch.tensor([rays, walked], dtype=torch.float64, device=red)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        rays = int(n.item())
-        agg = torch.tensor([counted["rays"], counted["nodeRecords"], counted["triTests"], trace_ms, trace_launches],
-                           dtype=torch.float64, device=red)
+        rays, walked = [int(x) for x in n.tolist()]
+        agg = torch.tensor([counted["walkedRays"], counted["nodeRecords"], counted["triTests"], trace_ms,
+                            trace_launches], dtype=torch.float64, device=red)
         dist.all_reduce(agg, op=dist.ReduceOp.SUM)
         c_rays, c_nodes, c_tris, trace_ms, trace_launches = [float(x) for x in agg.tolist()]
     else:
-        c_rays, c_nodes, c_tris = counted["rays"], counted["nodeRecords"], counted["triTests"]
+        c_rays, c_nodes, c_tris = counted["walkedRays"], counted["nodeRecords"], counted["triTests"]
 
     if rank != 0:
         dist.destroy_process_group()
@@ -180,7 +182,9 @@ def main():
     traffic = pmc_traffic_per_launch() if world == 1 else None
     out = {
         "metric": BASELINE_METRIC,
-        "value": rays / elapsed / 1e6,
+        # rays whose walk ran: the depth-capped last level's rays (built, shaded to zero, walk
+        # skipped) are not counted; rays_built_per_frame is the reference's ray count
+        "value": walked / elapsed / 1e6,
         "unit": "Mrays/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -202,7 +206,9 @@ def main():
             "shader": "PathTracer" if args.shader == 2 else "Whitted",
             "parallelism": (f"screen-tile shard x{world} + " + ("RCCL gather" if backend == "nccl" else "gloo gather (rehearsal)"))
             if world > 1 else "single GPU",
-            "rays_per_frame": rays / frames,
+            "rays_walked_per_frame": walked / frames,
+            "rays_built_per_frame": rays / frames,
+            "mrays_per_s_built": rays / elapsed / 1e6,
         },
         "roofline": {
             "bound": "hbm",

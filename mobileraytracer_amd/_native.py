@@ -52,6 +52,7 @@ class MrtFrameStats(ctypes.Structure):
         ("levelTraceMs", ctypes.c_double * 16), ("levelShadowMs", ctypes.c_double * 16),
         ("maxNodeRecordsPerRay", ctypes.c_uint64),
         ("assistedSubtrees", ctypes.c_uint64), ("maxRayMicros", ctypes.c_uint64),
+        ("walkedRays", ctypes.c_uint64),
     ]
 
 

@@ -556,6 +556,7 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     v.key = fbits(o4.w);
     v.tc = tc;
     v.d = xyz(d4);
+    if (level > a.maxDepth) return v;  // the depth cap below, taken before the gathers
     // issue every table gather of this vertex at once: their latencies overlap
     const float pick0 = s.tables[sampleIndex(v.key, tc, purposeLightPick(0))].x;
     const float lr0 = s.tables[sampleIndex(v.key, tc, purposeLightR(0))].y;
@@ -828,7 +829,8 @@ __global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int
 }
 
 // ---------------------------------------------------------------------------------------
-template <int kShader>
+// kTex: a textured scene (the Kd replay below); untextured scenes run the lean instantiation
+template <int kShader, bool kTex>
 __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
     const int count = min(counters[cntRays(level)], lv.cap);
     for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
@@ -853,7 +855,7 @@ __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, i
         // writes the material again (exact while at most one material is textured: the subtree
         // records keep only its last write)
         float4 lD = make_float4(0.0F, 0.0F, 0.0F, -1.0F), lS = lD, lT = lD, own = lD;
-        if (s.textured != 0) {
+        if (kTex) {
             own = lv.kd[i];
             if (own.w >= 0.0F) Kd = xyz(own);
             if (vb.x >= 0) lD = nx.last[vb.x];
@@ -903,7 +905,7 @@ __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, i
             out = make_float4(rgb.x, rgb.y, rgb.z, hitLight ? 1.0F : 0.0F);
         }
         lv.res[i] = out;
-        if (s.textured != 0) lv.last[i] = lT.w >= 0.0F ? lT : (lS.w >= 0.0F ? lS : (lD.w >= 0.0F ? lD : own));
+        if (kTex) lv.last[i] = lT.w >= 0.0F ? lT : (lS.w >= 0.0F ? lS : (lD.w >= 0.0F ? lD : own));
     }
 }
 
@@ -946,7 +948,7 @@ __global__ __launch_bounds__(256) void k_dump_hits(Level lv, int n, int32_t* kin
     t[i] = h.x;
 }
 
-__global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats) {
+__global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats, int skippedLevel) {
     unsigned long long rays = 0, shadows = 0;
     for (int l = 1; l <= maxLevel; ++l) {
         rays += static_cast<unsigned long long>(counters[cntRays(l)]);
@@ -957,6 +959,7 @@ __global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats) 
     stats[kStatRays] += rays;
     stats[kStatShadowRays] += shadows;
     stats[kStatPrimary] += static_cast<unsigned long long>(counters[cntRays(1)]);
+    if (skippedLevel > 0) stats[kStatSkipped] += static_cast<unsigned long long>(counters[cntRays(skippedLevel)]);
     if (counters[kCntOverflow] != 0) stats[kStatOverflow] |= static_cast<unsigned long long>(counters[kCntOverflow]);
 }
 
@@ -1152,10 +1155,17 @@ void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, 
 
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                    const ShadeArgs& a, int grid, hipStream_t st) {
+    const bool tex = s.textured != 0;
     if (shader == kShaderPathTracer) {
-        hipLaunchKernelGGL(k_resolve<kShaderPathTracer>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+        if (tex)
+            hipLaunchKernelGGL((k_resolve<kShaderPathTracer, true>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+        else
+            hipLaunchKernelGGL((k_resolve<kShaderPathTracer, false>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
     } else if (shader == kShaderWhitted) {
-        hipLaunchKernelGGL(k_resolve<kShaderWhitted>, dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+        if (tex)
+            hipLaunchKernelGGL((k_resolve<kShaderWhitted, true>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+        else
+            hipLaunchKernelGGL((k_resolve<kShaderWhitted, false>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
     }  // single-level shaders: k_shade_simple wrote the final results
 }
 
@@ -1174,8 +1184,8 @@ void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float
     hipLaunchKernelGGL(k_dump_hits, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, lv, n, kind, index, t);
 }
 
-void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st) {
-    hipLaunchKernelGGL(k_tally, dim3(1), dim3(1), 0, st, counters, maxLevel, stats);
+void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel) {
+    hipLaunchKernelGGL(k_tally, dim3(1), dim3(1), 0, st, counters, maxLevel, stats, skippedLevel);
 }
 
 // ---------------------------------------------------------------------------------------

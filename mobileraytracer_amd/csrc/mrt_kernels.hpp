@@ -49,7 +49,8 @@ constexpr int kStatLevelShadows = 8 + kMaxLevels;     // + level - 1: shadow ray
 constexpr int kStatMaxNodesRay = 8 + 2 * kMaxLevels;  // counting builds: most node records of one ray
 constexpr int kStatAssist = kStatMaxNodesRay + 1;    // tail-assist variants: subtrees handed over
 constexpr int kStatMaxRayTicks = kStatAssist + 1;    // tail-assist variants: longest ray (100 MHz ticks)
-constexpr int kNumStats = kStatMaxRayTicks + 1;
+constexpr int kStatSkipped = kStatMaxRayTicks + 1;     // rays of a last level whose walk was skipped
+constexpr int kNumStats = kStatSkipped + 1;
 
 // One level of the wavefront (SoA queues).
 struct Level {
@@ -137,7 +138,7 @@ void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx
 void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, int32_t* packed, hipStream_t st);
 void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st);
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);
-void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st);
+void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel = 0);
 int traceResidentThreadsPerCU();
 // Ray reordering for traversal coherence: keys = direction octant | Morton code of the origin
 // in the scene box, radix-sorted with the ray index; `order` receives the visit order.

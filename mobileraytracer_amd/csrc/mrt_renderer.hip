@@ -147,6 +147,8 @@ struct mrt_renderer {
     hipEvent_t forkEvent = nullptr;
     int overlap = 1;                     // tuning key 3: shadow rays on their own stream
     int sortRays = 0;                    // tuning key 4: reorder rays before tracing (1 closest-hit, 2 shadow)
+    int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
+    bool walkSkipped = false;            // the last pass skipped that walk
 
     // state (Renderer.hpp:30-40)
     std::atomic<bool> stopFlag{false};
@@ -600,6 +602,14 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // buffers alternate by level); every shadow(L) -> resolve.
         hipStream_t sb = r->overlap == 1 ? pp.shadowStream : ps;
         const bool comboMode = r->overlap == 2 && s_comboCapable(r->ds.variant);
+        // The last level (depth RayDepthMax + 1) shades to zero whatever its rays hit: shade()
+        // returns at the depth cap (PathTracer.cpp:24-26, Whitted.cpp:15-17), so its
+        // closest-hit walk is dead work and is skipped.  Not for textured scenes (rayTrace
+        // writes the texel Kd before shade() returns, Shader.cpp:114-122) nor in the combined
+        // launch (which also carries the previous level's shadow rays).
+        const bool skipLast = r->skipLast != 0 && r->ds.textured == 0 && r->overlap != 2 &&
+                              (shader == kShaderWhitted || shader == kShaderPathTracer) && nLevels > r->maxDepth;
+        r->walkSkipped = skipLast;
         size_t sync = 0;
         hipEvent_t shadowDone[kMaxLevels] = {};
         if (sb != ps) {
@@ -623,7 +633,7 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             const bool combined =
                 r->overlap == 2 && launchCombo(r->ds, pp.levels[l], pp.levels[l - 1], pp.counters, l, pp.gstack, r->gdepth,
                                                pp.stats, counting, r->traceThreads, ps);
-            if (!combined)
+            if (!combined && !(skipLast && l == nLevels))
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, ps);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
             if (sb != ps && l >= 3) MRT_HIP(hipStreamWaitEvent(ps, shadowDone[l - 2], 0));
@@ -665,7 +675,7 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         aa.spp = spp;
         aa.sampleBase = sampleBase;
         launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, ps);
-        launchTally(pp.counters, nLevels, pp.stats, ps);
+        launchTally(pp.counters, nLevels, pp.stats, ps, skipLast ? nLevels : 0);
     }
     // join: st continues after every pipeline
     for (int pi = 1; pi < nPipes; ++pi) {
@@ -701,6 +711,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     if (hs[kStatOverflow] != 0) return false;
     fs->rays += hs[kStatRays];
     fs->shadowRays += hs[kStatShadowRays];
+    fs->walkedRays += hs[kStatRays] - hs[kStatSkipped];
     fs->primaryRays += hs[kStatPrimary];
     fs->nodeRecords += hs[kStatNodes];
     fs->triTests += hs[kStatTris];
@@ -728,7 +739,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
                 const size_t lvl = (e / 5) % static_cast<size_t>(r->nLevels);
                 fs->levelTraceMs[lvl] += ta;
                 fs->levelShadowMs[lvl] += tb;
-                fs->traceLaunches += 1;
+                if (!(r->walkSkipped && lvl + 1 == static_cast<size_t>(r->nLevels))) fs->traceLaunches += 1;
                 fs->shadowLaunches += 1;
             }
         }
@@ -781,6 +792,7 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs = pass;
                     fs.rays += prev.rays;
                     fs.shadowRays += prev.shadowRays;
+                    fs.walkedRays += prev.walkedRays;
                     fs.primaryRays += prev.primaryRays;
                     fs.nodeRecords += prev.nodeRecords;
                     fs.triTests += prev.triTests;
@@ -978,6 +990,10 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->streamMode = value;
         return 0;
     }
+    if (key == 7 && (value == 0 || value == 1)) {
+        r->skipLast = value;
+        return 0;
+    }
     if (key == 5 && value >= 1 && value <= 8) {
         return guarded([&] {
             MRT_HIP(hipDeviceSynchronize());
@@ -1058,6 +1074,10 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
     }
     if (key == 6) {
         *value = r->streamMode;
+        return 0;
+    }
+    if (key == 7) {
+        *value = r->skipLast;
         return 0;
     }
     gLastError = "unknown tuning key";

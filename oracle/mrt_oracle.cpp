@@ -21,7 +21,8 @@
 // Deliberate deviations from the reference, identical in the product:
 //   * sample tables use fixed seeds and every draw is a pure function of
 //     (pixel, sample, ray-tree vertex, purpose) instead of shared atomic cursors;
-//   * the OBJ fill is single-threaded in file order; textures are not sampled;
+//   * the OBJ fill is single-threaded in file order; a textured hit writes Kd into the render
+//     thread's own copy of the materials (the reference shares them between threads);
 //   * each pixel receives its samples in order (no tile-claim race, Renderer.cpp:190-193).
 #include <algorithm>
 #include <map>

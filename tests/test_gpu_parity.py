@@ -340,6 +340,36 @@ def test_shadow_stream_overlap_is_invariant():
             assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
 
 
+def test_last_level_walk_skip_is_invariant():
+    """The depth-capped last level shades to zero whatever its rays hit, so skipping its
+    closest-hit walk (tuning key 7, default on) changes no pixel and no ray count; the walked-ray
+    statistic drops by exactly that level's rays.  Textured scenes keep the walk (the texel write
+    before shade() returns is replayed), as does the combined launch (tuning key 3 = 2)."""
+    import mobileraytracer_amd as m
+    cases = ((make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5), True),
+             (make_cfg(128, 128, shader=1, scene="water", max_depth=3), True),
+             (make_cfg(64, 64, shader=2, spp=2, max_depth=2), True),
+             (make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3), False))
+    for cfg, skips in cases:
+        outs = []
+        with m.Renderer(cfg) as r:
+            assert r.get_tuning(7) == 1
+            for skip, overlap in ((1, 1), (0, 1), (1, 0), (1, 2)):
+                r.set_tuning(7, skip)
+                r.set_tuning(3, overlap)
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"]))
+                last = st["levelRays"][cfg.maxDepth]  # level maxDepth + 1
+                skipped = skips and skip == 1 and overlap != 2
+                assert st["walkedRays"] == st["rays"] - (last if skipped else 0)
+                if skips:
+                    assert last > 0
+        for bm, rays, shadows in outs[1:]:
+            assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
+
+
 def _render_shards(cfg_kw, world):
     """Render every shard separately into a device-packed buffer, gather, unpack on 'rank 0'."""
     import torch

@@ -25,12 +25,13 @@ def main():
     for rnd in range(3):
         for v in variants:
             parts = v.split(":")
-            parts += ["1", "0", "1", "0"][len(parts) - 1:]
+            parts += ["1", "0", "1", "0", "1"][len(parts) - 1:]
             r.set_tuning(1, int(parts[0]))
             r.set_tuning(3, int(parts[1]))
             r.set_tuning(4, int(parts[2]))
             r.set_tuning(5, int(parts[3]))
             r.set_tuning(6, int(parts[4]))
+            r.set_tuning(7, int(parts[5]))  # skip the last level's walk (default 1)
             r.render_frame_device(bm, pk, sh)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
