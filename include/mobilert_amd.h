@@ -119,9 +119,9 @@ int mrt_get_scene_info(const mrt_renderer *r, mrt_scene_info *info);
 int mrt_set_profiling(mrt_renderer *r, int32_t flags);
 int mrt_get_frame_stats(const mrt_renderer *r, mrt_frame_stats *stats);
 /* tuning knobs for A/B measurement (results are identical for every value):
- * key 1 = trace kernel organisation, 0..21 (mrt_kernels.hip kTraceCfg: 0 per-wave batches,
+ * key 1 = trace kernel organisation, 0..22 (mrt_kernels.hip kTraceCfg: 0 per-wave batches,
  *         others while-while walks with refill threshold / LDS stack / work-cursor / tail-assist /
- *         compressed-node options),
+ *         compressed-node / last-occluder options),
  * key 2 = near-first traversal with conservative t-culling (1) or the reference visit set (0),
  * key 3 = shadow rays on the same stream (0), their own stream (1), or combined with the next
  *         level's closest-hit launch (2),

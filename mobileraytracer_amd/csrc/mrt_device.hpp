@@ -42,6 +42,7 @@ struct DScene {
     const CNode* triCNodes;    // compressed copy of triNodes (same numbering; [triTop, ..) used)
     const float* leafBoxes;    // exact box of every triangle leaf, 8 floats at its first primitive
     int32_t compOk;            // triCNodes / leafBoxes are valid (else compressed variants fall back)
+    const float* occBoxes;     // exact box of each triangle's leaf, 8 floats per triangle (variant 22)
     // textures (map_Kd): scenes with a textured material only (`textured` != 0)
     const float4* triTex;      // 2 per triangle: (tA.xy, tB.xy), (tC.xy, -, -)
     const int4* texInfo;       // per texture: width, height, channels, first byte in texels

@@ -163,6 +163,7 @@ struct TraceCfgRow {
     int assist = 0;                             // tail assist: idle lanes take subtrees of walking ones
     int trim = 0;                               // grid trimmed to ~2 lanes per ray; drained cursors read first
     int comp = 0;                               // compressed nodes (CNode) below the LDS top
+    int occ = 0;                                // shadow rays test the lane's last occluder first
 };
 constexpr TraceCfgRow kTraceCfg[] = {
     {2, 1, kLdsStack, 1, 1, 0},   // 0  per-wave batches, if-if
@@ -187,6 +188,7 @@ constexpr TraceCfgRow kTraceCfg[] = {
     {2, 32, 8, 8, 1, 128, 256, 1, 0, 0, 1},  // 19 as 14, compressed nodes
     {2, 32, 8, 8, 1, 128, 256, 1, 1, 0, 1},  // 20 as 19 with tail assist
     {2, 32, 8, 8, 1, 128, 256, 1, 1, 1, 1},  // 21 as 20, trimmed grid
+    {2, 32, 8, 8, 1, 128, 256, 1, 0, 0, 0, 1},  // 22 as 14, last-occluder test for shadow rays
 };
 constexpr int kNumTraceVariants = sizeof(kTraceCfg) / sizeof(kTraceCfg[0]);
 static_assert(kNumTraceVariants == kTraceVariants, "mrt_kernels.hpp kTraceVariants");
@@ -204,6 +206,7 @@ struct TraceCfg {
     static constexpr bool kAssist = kTraceCfg[kVariant].assist != 0;
     static constexpr bool kTrim = kTraceCfg[kVariant].trim != 0;
     static constexpr bool kComp = kTraceCfg[kVariant].comp != 0;
+    static constexpr bool kOcc = kTraceCfg[kVariant].occ != 0;
     static_assert(!kComp || (kTraceCfg[kVariant].wide == 2 && kTraceCfg[kVariant].fastSlab != 0), "CNode walk: BVH2, finite slab");
     static_assert(kTop <= kTopNodesMax, "top nodes");
     static_assert(kThreads % 64 == 0 && kThreads <= 1024, "workgroup size");
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
     if (C::kTrim && blockSpare<C::kThreads>(count)) return;
     stageTop<C::kTop, C::kThreads>(s, ldsTop);
     if (kVariant > 0)
-        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp>(s, lv.rO, lv.rD, lv.hit, count, fetch,
+        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp, C::kOcc>(s, lv.rO, lv.rD, lv.hit, count, fetch,
                                                                                    st, &cnt, ldsTop, lv.order);
     while (kVariant == 0) {
         int base = 0;
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
     if (C::kTrim && blockSpare<C::kThreads>(count)) return;
     stageTop<C::kTop, C::kThreads>(s, ldsTop);
     if (kVariant > 0)
-        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp>(s, lv.sO, lv.sD, lv.sC, count, fetch,
+        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp, C::kOcc>(s, lv.sO, lv.sD, lv.sC, count, fetch,
                                                                                   st, &cnt, ldsTop, lv.shadowOrder);
     while (kVariant == 0) {
         int base = 0;
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
         const int count = min(counters[cntRays(level)], lv.cap);
         int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride
                                     : counters + kCntFetchTrace + level;
-        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp>(
+        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp, C::kOcc>(
             s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, lv.order);
     }
     if (level >= 2) {
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
         const int count = min(counters[cntShadows(pl)], prev.shadowCap);
         int* fetch = C::kShards > 1 ? counters + kCntFetchShards + (kMaxLevels + pl) * kMaxFetchShards * kFetchStride
                                     : counters + kCntFetchShadow + pl;
-        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp>(
+        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp, C::kOcc>(
             s, prev.sO, prev.sD, prev.sC, count, fetch, st, &cntS, ldsTop, prev.shadowOrder);
     }
     if (kCount) {
@@ -1021,7 +1024,8 @@ int persistentGrid(K kernel, int variant, int kind, int threads, int maxThreads)
         MRT_LAUNCH_ONE(KERNEL, KIND, 18)                                                                     \
         MRT_LAUNCH_ONE(KERNEL, KIND, 19)                                                                     \
         MRT_LAUNCH_ONE(KERNEL, KIND, 20)                                                                     \
-        default: MRT_LAUNCH_ONE(KERNEL, KIND, 21)                                                            \
+        MRT_LAUNCH_ONE(KERNEL, KIND, 21)                                                                    \
+        default: MRT_LAUNCH_ONE(KERNEL, KIND, 22)                                                            \
     }
 
 #define MRT_LAUNCH_COMBO_ONE(V)                                                                              \
@@ -1108,6 +1112,7 @@ bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* count
         MRT_LAUNCH_COMBO_ONE(19)
         MRT_LAUNCH_COMBO_ONE(20)
         MRT_LAUNCH_COMBO_ONE(21)
+        MRT_LAUNCH_COMBO_ONE(22)
         default:
             return false;  // variant 0 (per-wave batches): separate launches
     }

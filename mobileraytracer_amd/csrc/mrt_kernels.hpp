@@ -11,7 +11,7 @@ constexpr int kShaderDepthMap = 3;    // C_wrapper.cpp:175-179
 constexpr int kShaderDiffuse = 4;     // C_wrapper.cpp:181-186 (DiffuseMaterial)
 constexpr int kShaderNoShadows = 5;   // C_wrapper.cpp:188-193 (the switch's default: 0, 5, ...)
 constexpr int kMaxLevels = 16;           // max ray depth + 2
-constexpr int kTraceVariants = 22;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
+constexpr int kTraceVariants = 23;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
 constexpr int kDefaultTraceVariant = 14;
 constexpr int kAccNaive = 1;  // Shader::Accelerator (Shader.hpp:20-24)
 constexpr int kAccGrid = 2;

@@ -265,6 +265,28 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
         d.leafBoxes = r->sceneMem.upload(lb, st);
     }
     {
+        // the exact box of each triangle's leaf (its parent's record of it), for the shadow
+        // walk's last-occluder test (trace variant 22)
+        const size_t nt = sc.triangles.size();
+        std::vector<float> ob(std::max<size_t>(nt, 1) * 8, 0.0F);
+        auto fill = [&](int32_t lref, float x0, float y0, float z0, float x1, float y1, float z1) {
+            const int f = leafFirst(lref), n = leafCount(lref);
+            for (int k = f; k < f + n && k < static_cast<int>(nt); ++k) {
+                const float b[6] = {x0, y0, z0, x1, y1, z1};
+                std::copy(b, b + 6, ob.begin() + 8 * static_cast<size_t>(k));
+            }
+        };
+        if (nt > 0) {
+            const GRoot& rt = d.triRoot;
+            if (rt.ref < 0) fill(rt.ref, rt.bmin[0], rt.bmin[1], rt.bmin[2], rt.bmax[0], rt.bmax[1], rt.bmax[2]);
+            for (const GNode& n : g) {
+                if (n.refL < 0) fill(n.refL, n.lminx, n.lminy, n.lminz, n.lmaxx, n.lmaxy, n.lmaxz);
+                if (n.refR < 0) fill(n.refR, n.rminx, n.rminy, n.rminz, n.rmaxx, n.rmaxy, n.rmaxz);
+            }
+        }
+        d.occBoxes = r->sceneMem.upload(ob, st);
+    }
+    {
         std::vector<GNode4> g4;
         toDeviceBVH4(tn, sc.triangles.size(), &g4, &d.triRoot4);
         d.triNodes4 = r->sceneMem.upload(g4, st);

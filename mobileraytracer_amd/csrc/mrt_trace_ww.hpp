@@ -265,7 +265,7 @@ __device__ __forceinline__ int2 takeBottom(TStack& st) {
 // kComp: compressed nodes (innerStepC) for all-finite waves, and a leaf's triangles count only
 // once its exact box passes (lanes with finite 1/d; the others only ever take exact steps).
 template <bool kAny, bool kCount, int kWide, int kRefill, int kShards, int kTop, bool kFastSlab, bool kAssist = false,
-          bool kTrim = false, bool kComp = false>
+          bool kTrim = false, bool kComp = false, bool kOcc = false>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                                 TStack& st, TravCount* cnt, const GNode* ldsTop,
@@ -294,6 +294,14 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
     int nHelp = 0;       // kAs, owner: helpers still walking parts of this lane's ray
     bool occl = false;   // kAs && kAny: occlusion found (by this lane or a helper)
     uint32_t t0 = 0;     // kAs: fetch time of this lane's ray (100 MHz ticks)
+    // kOcc (shadow rays): the triangle that occluded this lane's previous shadow ray is tested
+    // first.  A hit with eps <= t < distance in a leaf whose exact box passes is one the walk
+    // would find (the reference reaches that leaf: every ancestor's box contains it and the
+    // finite-1/d slab test is monotone in the bounds), and any hit makes the answer "occluded"
+    // (BVH.hpp:350-351), so the walk is skipped; otherwise the ray walks as usual.
+    constexpr bool kO = kOcc && kAny && !kCount && !kAs;
+    const BufRes occBuf = bufferOf(kO ? static_cast<const void*>(s.occBoxes) : static_cast<const void*>(s.triNodes));
+    int lastOcc = -1;
     while (true) {
         if (kAs) {
             // ---- helpers whose walk is over: merge into the owner lane (same total order) ----
@@ -451,6 +459,18 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     }
                     bt = b.t;
                     bcode = b.code;
+                    if (kO && rayIdx >= 0 && lastOcc >= 0 && finiteInv(inv)) {
+                        const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(lastOcc));
+                        const uint32_t off = static_cast<uint32_t>(lastOcc) * 48u;
+                        float t, u, v;
+                        if (code != src &&
+                            triTest(bload3(triBuf, off), bload3(triBuf, off + 16u), bload3(triBuf, off + 32u), o, d, &t,
+                                    &u, &v) &&
+                            !(t < kEpsilon) && !(t >= bt) && leafReachable(occBuf, lastOcc, o, inv)) {
+                            out[rayIdx].w = 1.0F;
+                            rayIdx = -1;
+                        }
+                    }
                     if (rayIdx >= 0) {
                         float te;
                         const GRoot& r = kWide == 4 ? s.triRoot4 : s.triRoot;
@@ -563,6 +583,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 if (kC && reach < 0) reach = leafReachable(leafBuf, first, o, inv) ? 1 : 0;
                 if (kC && reach == 0) break;  // the reference never tests this leaf's triangles
                 if (kAny) {
+                    if (kO) lastOcc = j;
                     hit = true;
                     break;
                 }

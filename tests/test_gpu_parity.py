@@ -284,7 +284,7 @@ def test_trace_kernel_variants_are_identical():
                 make_cfg(128, 128, shader=2, scene="water", spp=2), make_cfg(64, 64, shader=1)):
         outs = []
         with m.Renderer(cfg) as r:
-            for v in range(22):  # every kTraceCfg row
+            for v in range(23):  # every kTraceCfg row
                 r.set_tuning(1, v)
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
                 r.render_frame(bm)
