@@ -834,7 +834,8 @@ __global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int
 // ---------------------------------------------------------------------------------------
 // kTex: a textured scene (the Kd replay below); untextured scenes run the lean instantiation
 template <int kShader, bool kTex>
-__global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
+__global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a,
+                                                 int deadChildren) {
     const int count = min(counters[cntRays(level)], lv.cap);
     for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
          i += static_cast<int>(gridDim.x * blockDim.x)) {
@@ -850,6 +851,10 @@ __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, i
         if (vb.x >= nx.cap) vb.x = -1;
         if (vb.y >= nx.cap) vb.y = -1;
         if (vb.z >= nx.cap) vb.z = -1;
+        // children at the depth cap: radiance 0, no light hit.  Whitted adds Ks * 0 / Kt * 0 and
+        // PathTracer Kd * 0 (finite materials) to sums that start at +0, which leaves them as
+        // they are, so an absent child gives the same bits
+        if (deadChildren != 0) vb = make_int4(-1, -1, -1, 0);
         const int nShadow = va.w >> 3;
         const float4* m = s.mats + 4 * va.x;
         v3 Kd = xyz(m[1]);
@@ -1159,18 +1164,19 @@ void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, 
 }
 
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
-                   const ShadeArgs& a, int grid, hipStream_t st) {
+                   const ShadeArgs& a, int grid, hipStream_t st, bool deadChildren) {
+    const int dead = deadChildren ? 1 : 0;
     const bool tex = s.textured != 0;
     if (shader == kShaderPathTracer) {
         if (tex)
-            hipLaunchKernelGGL((k_resolve<kShaderPathTracer, true>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+            hipLaunchKernelGGL((k_resolve<kShaderPathTracer, true>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a, dead);
         else
-            hipLaunchKernelGGL((k_resolve<kShaderPathTracer, false>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+            hipLaunchKernelGGL((k_resolve<kShaderPathTracer, false>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a, dead);
     } else if (shader == kShaderWhitted) {
         if (tex)
-            hipLaunchKernelGGL((k_resolve<kShaderWhitted, true>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+            hipLaunchKernelGGL((k_resolve<kShaderWhitted, true>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a, dead);
         else
-            hipLaunchKernelGGL((k_resolve<kShaderWhitted, false>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a);
+            hipLaunchKernelGGL((k_resolve<kShaderWhitted, false>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a, dead);
     }  // single-level shaders: k_shade_simple wrote the final results
 }
 

@@ -133,8 +133,10 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
                   unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st);
+// deadChildren: level + 1 is the depth-capped last level, whose results are all zero; its
+// records are then not read (a zero child adds exactly nothing, section 3 of DESIGN.md)
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
-                   const ShadeArgs& a, int grid, hipStream_t st);
+                   const ShadeArgs& a, int grid, hipStream_t st, bool deadChildren = false);
 void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, int32_t* packed, hipStream_t st);
 void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st);
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);

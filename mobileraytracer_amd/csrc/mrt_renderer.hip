@@ -632,6 +632,9 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         const bool skipLast = r->skipLast != 0 && r->ds.textured == 0 && r->overlap != 2 &&
                               (shader == kShaderWhitted || shader == kShaderPathTracer) && nLevels > r->maxDepth;
         r->walkSkipped = skipLast;
+        // ... and with it the level's shading (every record terminal, radiance 0) and resolve:
+        // the parents' resolve treats the capped children as absent, which gives the same bits
+        const bool skipLastShade = skipLast && nLevels >= 2 && r->ds.textured == 0;
         size_t sync = 0;
         hipEvent_t shadowDone[kMaxLevels] = {};
         if (sb != ps) {
@@ -659,7 +662,8 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, ps);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
             if (sb != ps && l >= 3) MRT_HIP(hipStreamWaitEvent(ps, shadowDone[l - 2], 0));
-            launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
+            if (!(skipLastShade && l == nLevels))
+                launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
             if (sb != ps) {
                 const hipEvent_t shaded = syncEvent(pp, sync++);
@@ -686,8 +690,9 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             }
         }
         if (sb != ps) MRT_HIP(hipStreamWaitEvent(ps, shadowDone[nLevels], 0));
-        for (int l = nLevels; l >= 1; --l) {
-            launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
+        for (int l = skipLastShade ? nLevels - 1 : nLevels; l >= 1; --l) {
+            launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps,
+                          skipLastShade && l == nLevels - 1);
         }
         AccumArgs aa{};
         aa.map = map;
