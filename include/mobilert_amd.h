@@ -95,8 +95,6 @@ typedef struct mrt_frame_stats {
     double levelTraceMs[16];      /* profiling: closest-hit trace time per depth */
     double levelShadowMs[16];     /* profiling: any-hit trace time per depth */
     uint64_t maxNodeRecordsPerRay; /* counting pass only: most node records one ray fetched */
-    uint64_t assistedSubtrees;     /* tail-assist trace variants: subtrees handed to idle lanes */
-    uint64_t maxRayMicros;         /* tail-assist trace variants: longest fetch-to-result time of one ray */
     uint64_t walkedRays;           /* closest-hit rays traversed: `rays` minus the depth-capped last
                                       level's, whose walk is skipped (tuning key 7) */
 } mrt_frame_stats;
@@ -119,15 +117,10 @@ int mrt_get_scene_info(const mrt_renderer *r, mrt_scene_info *info);
 int mrt_set_profiling(mrt_renderer *r, int32_t flags);
 int mrt_get_frame_stats(const mrt_renderer *r, mrt_frame_stats *stats);
 /* tuning knobs for A/B measurement (results are identical for every value):
- * key 1 = trace kernel organisation, 0..22 (mrt_kernels.hip kTraceCfg: 0 per-wave batches,
- *         others while-while walks with refill threshold / LDS stack / work-cursor / tail-assist /
- *         compressed-node / last-occluder options),
+ * key 1 = trace walk: 0 per-wave 64-ray batches with the plain DFS of BVH.hpp:327-384,
+ *         1 persistent while-while walk (default),
  * key 2 = near-first traversal with conservative t-culling (1) or the reference visit set (0),
- * key 3 = shadow rays on the same stream (0), their own stream (1), or combined with the next
- *         level's closest-hit launch (2),
- * key 4 = reorder rays before traversal (bit 0 closest-hit, bit 1 shadow),
- * key 5 = concurrent chunk pipelines, 1..8,
- * key 6 = streaming mode: every level of a pass in one persistent launch (1),
+ * key 3 = shadow rays on the same stream (0) or their own stream (1, default),
  * key 7 = skip the closest-hit walk of the depth-capped last level (1, default) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);

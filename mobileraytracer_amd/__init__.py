@@ -114,7 +114,7 @@ class Renderer:
         _native.check(self._lib.mrt_set_profiling(self._h, int(timing) | (2 * int(counting))))
 
     def set_tuning(self, key: int, value: int) -> None:
-        """A/B knobs (identical results): 1 = trace kernel variant (0..15), 2 = t-culling,
+        """A/B knobs (identical results): 1 = trace walk (0 reference, 1 default), 2 = t-culling,
         3 = shadow rays on their own stream."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 

@@ -51,7 +51,6 @@ class MrtFrameStats(ctypes.Structure):
         ("levelRays", ctypes.c_uint64 * 16), ("levelShadowRays", ctypes.c_uint64 * 16),
         ("levelTraceMs", ctypes.c_double * 16), ("levelShadowMs", ctypes.c_double * 16),
         ("maxNodeRecordsPerRay", ctypes.c_uint64),
-        ("assistedSubtrees", ctypes.c_uint64), ("maxRayMicros", ctypes.c_uint64),
         ("walkedRays", ctypes.c_uint64),
     ]
 

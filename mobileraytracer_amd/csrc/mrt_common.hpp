@@ -162,38 +162,6 @@ struct alignas(16) GNode {
 };
 static_assert(sizeof(GNode) == 64, "GNode must be 64 bytes");
 
-// Compressed BVH2 inner node (32 bytes = 2 loads; same numbering as GNode, built from it by
-// toDeviceCBVH).  Both children's boxes sit on a per-axis grid anchored at the node's own box
-// minimum (exact) with a power-of-two step, 8 bits per bound, rounded outwards with the kernel's
-// arithmetic (fma(step, u, origin) rounds once, as origin + step * u does on the host), so every
-// dequantised box contains the exact one.  Child references are implicit in the depth-first
-// pre-order numbering: an inner left child is node + 1; an inner right child is node + 1 when
-// the left is a leaf, else `ref`; a leaf's first primitive is `ref` (left) or `ref` + the left
-// leaf's count (right of a leaf), or `ref` (right of an inner left).
-struct alignas(16) CNode {
-    float ox, oy, oz;   // grid origin
-    uint32_t expMeta;   // bytes 0-2: biased exponents of the x/y/z steps (step 2^(e-127); 0: step 0)
-                        // byte 3: 1 left is a leaf, 2 right is a leaf, (countL-1) << 2, (countR-1) << 4
-    uint32_t q[3];      // bytes: L lo xyz, L hi xyz, R lo xyz, R hi xyz
-    int32_t ref;
-};
-static_assert(sizeof(CNode) == 32, "CNode must be 32 bytes");
-
-// 4-wide node collapsed from the reference BVH2 (one 128-byte record): component-major child
-// boxes so one float4 holds the same bound of all four children.  A collapsed child is reached
-// when its own box passes; its skipped BVH2 ancestors' boxes contain it (min/max are exact), and
-// the slab predicate is monotone in the bounds, so every ancestor test also passes - except in
-// the NaN-degenerate case (ray origin exactly on a bound with a zero direction component), the
-// divergence SURVEY.md Appendix A.7 allows and DESIGN.md documents.
-struct alignas(16) GNode4 {
-    float minx[4], miny[4], minz[4];
-    float maxx[4], maxy[4], maxz[4];
-    int32_t ref[4];    // inner node index, leaf ref, or kRefEmpty
-    int32_t pad[4];
-};
-static_assert(sizeof(GNode4) == 128, "GNode4 must be 128 bytes");
-constexpr int32_t kRefEmpty = 0x7FFFFFFF;
-
 // root box + root reference of one BVH (the reference tests the root box first,
 // BVH.hpp:340-342)
 struct GRoot {

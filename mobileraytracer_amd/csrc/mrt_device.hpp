@@ -16,15 +16,13 @@
 namespace mrt {
 
 constexpr int kBlock = 256;         // threads per workgroup for every trace kernel
-constexpr int kLdsStack = 16;       // max per-thread short stack in LDS (entries of 8 bytes)
-constexpr int kLdsStackMin = 8;     // smallest LDS stack a kernel variant uses (sizes the spill area)
+constexpr int kLdsStackMin = 8;     // per-thread stack entries (8 bytes) in LDS; deeper ones spill
 constexpr float kCullMargin = 0x1p-10f;
 
 struct DScene {
     const float4* triGeom;     // 3 per triangle (BVH order): A, AB, AC  (xyz)
     const float4* triShade;    // 3 per triangle: nA (w = material index bits), nB, nC
     const GNode* triNodes;
-    const GNode4* triNodes4;   // the same BVH collapsed to 4-wide nodes
     const float4* planes;      // 2 per plane: normal (w = material bits), point
     const GNode* planeNodes;
     const float4* spheres;     // 2 per sphere: center (w = sqRadius), (x = material bits)
@@ -33,16 +31,13 @@ struct DScene {
     const float4* mats;        // 4 per material: Le (w = ior), Kd, Ks, Kt
     const float2* tables;  // 2^20 x {shader (Shader.cpp:23), sampler (StaticHaltonSeq.cpp)}
                            // shuffled Halton values
-    GRoot triRoot, triRoot4, planeRoot, sphereRoot;
+    GRoot triRoot, planeRoot, sphereRoot;
     int32_t nLights;
     int32_t nMats;
     int32_t cull;              // 1: near-first + conservative t-culling, 0: reference visit set
-    int32_t variant;           // trace kernel organisation (mrt_kernels.hip kTraceCfg)
+    int32_t variant;           // trace walk: 0 per-wave reference walk, 1 persistent while-while
     int32_t triTop;            // triNodes[0, triTop) are the breadth-first top of the tree
-    const CNode* triCNodes;    // compressed copy of triNodes (same numbering; [triTop, ..) used)
-    const float* leafBoxes;    // exact box of every triangle leaf, 8 floats at its first primitive
-    int32_t compOk;            // triCNodes / leafBoxes are valid (else compressed variants fall back)
-    const float* occBoxes;     // exact box of each triangle's leaf, 8 floats per triangle (variant 22)
+    int32_t matsFinite;        // every material's Kd / Ks / Kt component is finite
     // textures (map_Kd): scenes with a textured material only (`textured` != 0)
     const float4* triTex;      // 2 per triangle: (tA.xy, tB.xy), (tC.xy, -, -)
     const int4* texInfo;       // per texture: width, height, channels, first byte in texels

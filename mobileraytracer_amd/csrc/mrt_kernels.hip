@@ -19,8 +19,6 @@
 #include "mrt_kernels.hpp"
 #include "mrt_trace_ww.hpp"
 
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <utility>
 
@@ -151,118 +149,40 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
 }
 
 // ---------------------------------------------------------------------------------------
-// Trace-kernel variants (identical results; tools/perf_sweep.py A/Bs them).  Columns:
-// BVH width, refill threshold (idle lanes before a wave fetches new rays; 1 = per lane),
-// LDS stack entries, work cursors (8 = one per XCD group of workgroups), min waves per SIMD.
-//   0 per-wave 64-ray batches, if-if walk (BVH2); the rest are while-while walks.
-struct TraceCfgRow {
-    int wide, refill, stack, shards, minWaves;  // shards <= kMaxFetchShards
-    int top;                                    // BVH2 top nodes staged in LDS (<= kTopNodesMax)
-    int threads = kBlock;                       // per workgroup (the LDS top is shared by them)
-    int fastSlab = 0;                           // IEEE min/max slab test when every 1/d is finite
-    int assist = 0;                             // tail assist: idle lanes take subtrees of walking ones
-    int trim = 0;                               // grid trimmed to ~2 lanes per ray; drained cursors read first
-    int comp = 0;                               // compressed nodes (CNode) below the LDS top
-    int occ = 0;                                // shadow rays test the lane's last occluder first
-};
-constexpr TraceCfgRow kTraceCfg[] = {
-    {2, 1, kLdsStack, 1, 1, 0},   // 0  per-wave batches, if-if
-    {2, 1, kLdsStack, 1, 1, 0},   // 1  while-while, per-lane refill
-    {4, 1, kLdsStack, 1, 1, 0},   // 2  as 1, 4-wide BVH
-    {2, 32, 8, 8, 1, 0, 64, 1},   // 3  as 14 without the LDS top, one wave per workgroup
-    {2, 32, 8, 8, 1, 0, 128, 1},  // 4  as 3, two waves per workgroup
-    {2, 32, 8, 8, 1, 64, 128, 1}, // 5  as 4 with the top 64 nodes in LDS
-    {2, 32, 8, 8, 1, 128, 128, 1},// 6  as 4 with the top 128 nodes in LDS
-    {2, 32, kLdsStack, 8, 1, 0},  // 7
-    {2, 32, 8, 8, 1, 0},          // 8
-    {2, 16, 8, 8, 1, 0, 64, 1},   // 9  as 3, refill at 16 idle lanes
-    {2, 32, 8, 8, 8, 0},          // 10 as 8, compiled for 8 waves per SIMD
-    {2, 32, 8, 32, 1, 0},         // 11 as 8, 32 cursors
-    {2, 32, 8, 8, 1, 64},         // 12 as 8, top 64 nodes in LDS
-    {2, 32, 8, 8, 1, 128},        // 13 as 8, top 128 nodes in LDS
-    {2, 32, 8, 8, 1, 128, 256, 1},  // 14 as 13, IEEE min/max slab test for finite 1/d (default)
-    {2, 32, 8, 8, 1, 128, 512},     // 15 as 13, 512-thread workgroups
-    {2, 32, 8, 8, 1, 128, 256, 1, 1},     // 16 as 14 with tail assist
-    {2, 32, 8, 8, 1, 128, 256, 1, 1, 1},  // 17 as 16, trimmed grid
-    {2, 32, 8, 8, 1, 128, 256, 1, 0, 1},  // 18 as 14, trimmed grid
-    {2, 32, 8, 8, 1, 128, 256, 1, 0, 0, 1},  // 19 as 14, compressed nodes
-    {2, 32, 8, 8, 1, 128, 256, 1, 1, 0, 1},  // 20 as 19 with tail assist
-    {2, 32, 8, 8, 1, 128, 256, 1, 1, 1, 1},  // 21 as 20, trimmed grid
-    {2, 32, 8, 8, 1, 128, 256, 1, 0, 0, 0, 1},  // 22 as 14, last-occluder test for shadow rays
-};
-constexpr int kNumTraceVariants = sizeof(kTraceCfg) / sizeof(kTraceCfg[0]);
-static_assert(kNumTraceVariants == kTraceVariants, "mrt_kernels.hpp kTraceVariants");
+// Trace kernels.  Two walks with identical results (tested):
+//   variant 0: per-wave 64-ray batches, if-if walk (closestHit / anyHit of mrt_device.hpp) -
+//              the plain restatement of BVH.hpp:327-384, kept as the in-kernel reference;
+//   variant 1: the persistent while-while walk of mrt_trace_ww.hpp (default).
+constexpr int kWalkThreads = 256;
 
-template <int kVariant>
-struct TraceCfg {
-    static constexpr int kWide = kTraceCfg[kVariant].wide;
-    static constexpr int kRefill = kTraceCfg[kVariant].refill;
-    static constexpr int kStack = kTraceCfg[kVariant].stack;
-    static constexpr int kShards = kTraceCfg[kVariant].shards;
-    static constexpr int kMinWaves = kTraceCfg[kVariant].minWaves;
-    static constexpr int kTop = kTraceCfg[kVariant].wide == 2 ? kTraceCfg[kVariant].top : 0;
-    static constexpr int kThreads = kTraceCfg[kVariant].threads;
-    static constexpr bool kFastSlab = kTraceCfg[kVariant].fastSlab != 0;
-    static constexpr bool kAssist = kTraceCfg[kVariant].assist != 0;
-    static constexpr bool kTrim = kTraceCfg[kVariant].trim != 0;
-    static constexpr bool kComp = kTraceCfg[kVariant].comp != 0;
-    static constexpr bool kOcc = kTraceCfg[kVariant].occ != 0;
-    static_assert(!kComp || (kTraceCfg[kVariant].wide == 2 && kTraceCfg[kVariant].fastSlab != 0), "CNode walk: BVH2, finite slab");
-    static_assert(kTop <= kTopNodesMax, "top nodes");
-    static_assert(kThreads % 64 == 0 && kThreads <= 1024, "workgroup size");
-};
-
-// Trimmed grid (kTrim): a level of `count` rays needs ~2 lanes per ray (the spare lanes assist
-// the slowest walks); the other workgroups of the persistent grid leave at once instead of
-// each paying for the LDS top and a round of cursor atomics.
-template <int kThreads>
-__device__ __forceinline__ bool blockSpare(int count) {
-    const long long need = (2LL * count + kThreads - 1) / kThreads;
-    return static_cast<long long>(blockIdx.x) >= max(need, 8LL);
-}
-
-// Tail-assist variants: handed-over subtrees (sum) and the longest ray (max) of the launch.
-__device__ __forceinline__ void assistStats(const TravCount& c, unsigned long long* stats) {
-    unsigned long long a = c.assists;
-    uint32_t m = c.ticksMax;
+template <bool kCount>
+__device__ __forceinline__ void reduceCounts(const TravCount& cnt, unsigned long long* stats, int nodesStat,
+                                             int trisStat) {
+    unsigned long long n = cnt.nodes, t = cnt.tris;
     for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_down(a, off, 64);
-        m = max(m, static_cast<uint32_t>(__shfl_down(static_cast<int>(m), off, 64)));
+        n += __shfl_down(n, off, 64);
+        t += __shfl_down(t, off, 64);
     }
     if (laneId() == 0) {
-        if (a != 0) atomicAdd(stats + kStatAssist, a);
-        atomicMax(stats + kStatMaxRayTicks, static_cast<unsigned long long>(m));
+        atomicAdd(stats + nodesStat, n);
+        atomicAdd(stats + trisStat, t);
     }
-}
-
-// Copies the BVH2 top into LDS (all threads; ends with a barrier).
-template <int kTop, int kThreads>
-__device__ __forceinline__ void stageTop(const DScene& s, GNode* ldsTop) {
-    if (kTop == 0) return;
-    const int n = min(kTop, s.triTop) * static_cast<int>(sizeof(GNode) / sizeof(float4));
-    const float4* src = reinterpret_cast<const float4*>(s.triNodes);
-    float4* dst = reinterpret_cast<float4*>(ldsTop);
-    for (int i = static_cast<int>(threadIdx.x); i < n; i += kThreads) dst[i] = src[i];
-    __syncthreads();
 }
 
 template <bool kCount, int kVariant>
-__global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::kMinWaves) void k_trace(DScene s, Level lv, int* counters, int level, int2* gstack,
-                                                  int gdepth, unsigned long long* stats) {
-    using C = TraceCfg<kVariant>;
-    __shared__ int2 ldsStack[C::kStack * C::kThreads];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * C::kThreads + threadIdx.x) * gdepth, 0,
-              C::kStack, C::kThreads};
+__global__ __launch_bounds__(kWalkThreads, 1) void k_trace(DScene s, Level lv, int* counters, int level,
+                                                            int2* gstack, int gdepth, unsigned long long* stats) {
+    __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
+              kWalkStack, kWalkThreads};
     const int count = min(counters[cntRays(level)], lv.cap);
-    int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride
-                                : counters + kCntFetchTrace + level;
+    int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
-    __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
-    if (C::kTrim && blockSpare<C::kThreads>(count)) return;
-    stageTop<C::kTop, C::kThreads>(s, ldsTop);
-    if (kVariant > 0)
-        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp, C::kOcc>(s, lv.rO, lv.rD, lv.hit, count, fetch,
-                                                                                   st, &cnt, ldsTop, lv.order);
+    if (kVariant == 1) {
+        __shared__ GNode ldsTop[kWalkTop];
+        stageTop<kWalkThreads>(s, ldsTop);
+        traceWhileWhile<false, kCount>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop);
+    }
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -276,39 +196,26 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
             lv.hit[i] = make_float4(b.t, b.u, b.v, bitsf(b.code));
         }
     }
-    if (C::kAssist && !kCount) assistStats(cnt, stats);
     if (kCount) {
-        unsigned long long n = cnt.nodes, t = cnt.tris;
-        for (int off = 32; off > 0; off >>= 1) {
-            n += __shfl_down(n, off, 64);
-            t += __shfl_down(t, off, 64);
-        }
-        if (laneId() == 0) {
-            atomicAdd(stats + kStatNodes, n);
-            atomicAdd(stats + kStatTris, t);
-        }
+        reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris);
         atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
     }
 }
 
 template <bool kCount, int kVariant>
-__global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::kMinWaves) void k_shadow(DScene s, Level lv, int* counters, int level, int2* gstack,
-                                                   int gdepth, unsigned long long* stats) {
-    using C = TraceCfg<kVariant>;
-    __shared__ int2 ldsStack[C::kStack * C::kThreads];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * C::kThreads + threadIdx.x) * gdepth, 0,
-              C::kStack, C::kThreads};
+__global__ __launch_bounds__(kWalkThreads, 1) void k_shadow(DScene s, Level lv, int* counters, int level,
+                                                             int2* gstack, int gdepth, unsigned long long* stats) {
+    __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
+              kWalkStack, kWalkThreads};
     const int count = min(counters[cntShadows(level)], lv.shadowCap);
-    int* fetch = C::kShards > 1
-                     ? counters + kCntFetchShards + (kMaxLevels + level) * kMaxFetchShards * kFetchStride
-                     : counters + kCntFetchShadow + level;
+    int* fetch = counters + kCntFetchShards + (kMaxLevels + level) * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
-    __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
-    if (C::kTrim && blockSpare<C::kThreads>(count)) return;
-    stageTop<C::kTop, C::kThreads>(s, ldsTop);
-    if (kVariant > 0)
-        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp, C::kOcc>(s, lv.sO, lv.sD, lv.sC, count, fetch,
-                                                                                  st, &cnt, ldsTop, lv.shadowOrder);
+    if (kVariant == 1) {
+        __shared__ GNode ldsTop[kWalkTop];
+        stageTop<kWalkThreads>(s, ldsTop);
+        traceWhileWhile<true, kCount>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop);
+    }
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
@@ -322,65 +229,7 @@ __global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::k
             lv.sC[i].w = occ ? 1.0F : 0.0F;
         }
     }
-    if (C::kAssist && !kCount) assistStats(cnt, stats);
-    if (kCount) {
-        unsigned long long n = cnt.nodes, t = cnt.tris;
-        for (int off = 32; off > 0; off >>= 1) {
-            n += __shfl_down(n, off, 64);
-            t += __shfl_down(t, off, 64);
-        }
-        if (laneId() == 0) {
-            atomicAdd(stats + kStatNodesShadow, n);
-            atomicAdd(stats + kStatTrisShadow, t);
-        }
-    }
-}
-
-// Closest-hit rays of `level` and then, in the same launch, the shadow rays of level - 1:
-// one persistent drain per level instead of two (tuning key 3 = 2).  Workgroups switch to
-// the shadow queue as the closest-hit queue runs dry, so the shadow work fills the tail.
-template <bool kCount, int kVariant>
-__global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, TraceCfg<kVariant>::kMinWaves) void k_combo(
-    DScene s, Level lv, Level prev, int* counters, int level, int2* gstack, int gdepth, unsigned long long* stats) {
-    using C = TraceCfg<kVariant>;
-    static_assert(kVariant > 0, "while-while variants only");
-    __shared__ int2 ldsStack[C::kStack * C::kThreads];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * C::kThreads + threadIdx.x) * gdepth, 0,
-              C::kStack, C::kThreads};
-    __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
-    stageTop<C::kTop, C::kThreads>(s, ldsTop);
-    TravCount cnt{0u, 0u}, cntS{0u, 0u};
-    {
-        const int count = min(counters[cntRays(level)], lv.cap);
-        int* fetch = C::kShards > 1 ? counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride
-                                    : counters + kCntFetchTrace + level;
-        traceWhileWhile<false, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp, C::kOcc>(
-            s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, lv.order);
-    }
-    if (level >= 2) {
-        const int pl = level - 1;
-        const int count = min(counters[cntShadows(pl)], prev.shadowCap);
-        int* fetch = C::kShards > 1 ? counters + kCntFetchShards + (kMaxLevels + pl) * kMaxFetchShards * kFetchStride
-                                    : counters + kCntFetchShadow + pl;
-        traceWhileWhile<true, kCount, C::kWide, C::kRefill, C::kShards, C::kTop, C::kFastSlab, C::kAssist, C::kTrim, C::kComp, C::kOcc>(
-            s, prev.sO, prev.sD, prev.sC, count, fetch, st, &cntS, ldsTop, prev.shadowOrder);
-    }
-    if (kCount) {
-        unsigned long long n = cnt.nodes, t = cnt.tris, ns = cntS.nodes, ts = cntS.tris;
-        for (int off = 32; off > 0; off >>= 1) {
-            n += __shfl_down(n, off, 64);
-            t += __shfl_down(t, off, 64);
-            ns += __shfl_down(ns, off, 64);
-            ts += __shfl_down(ts, off, 64);
-        }
-        if (laneId() == 0) {
-            atomicAdd(stats + kStatNodes, n);
-            atomicAdd(stats + kStatTris, t);
-            atomicAdd(stats + kStatNodesShadow, ns);
-            atomicAdd(stats + kStatTrisShadow, ts);
-        }
-        atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
-    }
+    if (kCount) reduceCounts<kCount>(cnt, stats, kStatNodesShadow, kStatTrisShadow);
 }
 
 // Closest hit (kAny false: lv.rO / rD -> lv.hit) or shadow test (true: lv.sO / sD -> lv.sC.w)
@@ -612,37 +461,14 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     return v;
 }
 
-// Payload stores: plain, or (kPublish) `sc1` buffer stores for rays that other waves of the
-// same launch will read (the hand-off protocol of the microarchitecture guide: sc1 stores,
-// the storing wave's vmcnt(0), then the ready flag).
-template <bool kPublish>
-__device__ __forceinline__ void storeF4(float4* base, int j, float4 v) {
-    if (kPublish) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
-                                               __builtin_amdgcn_make_buffer_rsrc(base, static_cast<short>(0), 0x7FFFFFFF,
-                                                                                 0x00020000),
-                                               static_cast<uint32_t>(j) * 16u, 0, 16);
-    } else {
-        base[j] = v;
-    }
-}
-template <bool kPublish>
-__device__ __forceinline__ void storeU32(uint32_t* base, int j, uint32_t v) {
-    if (kPublish) {
-        __builtin_amdgcn_raw_buffer_store_b32(v, __builtin_amdgcn_make_buffer_rsrc(base, static_cast<short>(0), 0x7FFFFFFF,
-                                                                                  0x00020000),
-                                              static_cast<uint32_t>(j) * 4u, 0, 16);
-    } else {
-        base[j] = v;
-    }
-}
-
 // Writes vertex i's shadow rays (level lv, from shadowBase) and children (level nx, from
 // childBase) and its record.  Slots past a queue's capacity set the overflow flag (the frame is
-// then redone in smaller passes).
-template <bool kPublish>
+// then redone in smaller passes).  deadNext: level + 1 is the depth-capped last level, whose
+// rays are counted (the reference constructs them) but never traced, shaded or read, so their
+// payloads are not written and their directions not computed.
 __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, int i, const Level& lv, const Level& nx,
-                                          int shadowBase, int childBase, int* counters, const ShadeArgs& a) {
+                                          int shadowBase, int childBase, int* counters, const ShadeArgs& a,
+                                          bool deadNext) {
     if (v.terminal) {
         lv.res[i] = v.leaf;
         lv.vtx[i] = make_int4(-1, 0, 0, 0);
@@ -664,11 +490,9 @@ __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, 
             const int j = shadowBase + written;
             ++written;
             if (j < lv.shadowCap) {
-                storeF4<kPublish>(lv.sO, j, make_float4(v.g.P.x, v.g.P.y, v.g.P.z, bitsf(v.g.src)));
-                storeF4<kPublish>(lv.sD, j, make_float4(ld.x, ld.y, ld.z, dist));
-                // sc1 too when published: the shadow walk, maybe on another XCD, later writes the
-                // occlusion flag into this line, and a dirty copy here must not overwrite it
-                storeF4<kPublish>(lv.sC, j, make_float4(lc.x, lc.y, lc.z, 0.0F));
+                lv.sO[j] = make_float4(v.g.P.x, v.g.P.y, v.g.P.z, bitsf(v.g.src));
+                lv.sD[j] = make_float4(ld.x, ld.y, ld.z, dist);
+                lv.sC[j] = make_float4(lc.x, lc.y, lc.z, 0.0F);
             } else {
                 atomicOr(counters + kCntOverflow, 1);
             }
@@ -676,26 +500,29 @@ __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, 
     }
     // child rays: diffuse (PathTracer.cpp:90-91), specular (:118-120), transmission (:129-131),
     // stored consecutively from childBase
-    int c = childBase;
-    auto emit = [&](v3 dir, uint32_t slot) {
-        const int j = c++;
-        if (j >= nx.cap) {
-            atomicOr(counters + kCntOverflow, 1);
-            return;
-        }
-        storeF4<kPublish>(nx.rO, j, make_float4(v.g.P.x, v.g.P.y, v.g.P.z, bitsf(v.key)));
-        storeF4<kPublish>(nx.rD, j, make_float4(dir.x, dir.y, dir.z, bitsf(v.g.src)));
-        storeU32<kPublish>(nx.tree, j, v.tc * 4u + slot);
-    };
-    if (v.wantD) emit(cosineHemisphere(v.g.N, v.hemi1, v.hemi2), 1u);
-    if (v.wantS) emit(reflect(v.d, v.g.N), 2u);
-    if (v.wantT) emit(refract(v.d, v.g.N, 1.0F / v.ior), 3u);
+    if (!deadNext) {
+        int c = childBase;
+        auto emit = [&](v3 dir, uint32_t slot) {
+            const int j = c++;
+            if (j >= nx.cap) {
+                atomicOr(counters + kCntOverflow, 1);
+                return;
+            }
+            nx.rO[j] = make_float4(v.g.P.x, v.g.P.y, v.g.P.z, bitsf(v.key));
+            nx.rD[j] = make_float4(dir.x, dir.y, dir.z, bitsf(v.g.src));
+            nx.tree[j] = v.tc * 4u + slot;
+        };
+        if (v.wantD) emit(cosineHemisphere(v.g.N, v.hemi1, v.hemi2), 1u);
+        if (v.wantS) emit(reflect(v.d, v.g.N), 2u);
+        if (v.wantT) emit(refract(v.d, v.g.N, 1.0F / v.ior), 3u);
+    }
     const int mask = (v.wantD ? 1 : 0) | (v.wantS ? 2 : 0) | (v.wantT ? 4 : 0);
     lv.vtx[i] = make_int4(v.mat, shadowBase, childBase, (v.nShadow << 3) | mask);
 }
 
 template <int kShader>
-__global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a) {
+__global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a,
+                                                  int deadNext) {
     const int count = min(counters[cntRays(level)], lv.cap);
     // {rays of level+1, shadow rays of level}: one 64-bit allocation per block and iteration
     auto* pair = reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1));
@@ -720,42 +547,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
         int childBase, shadowBase;
         blockAllocPair(pair, active ? v.nChild : 0, active ? v.nShadow : 0, &childBase, &shadowBase, allocLds, parity);
         parity ^= 1;
-        if (active) shadeEmit<false>(s, v, i, lv, nx, shadowBase, childBase, counters, a);
-    }
-}
-
-}  // namespace mrt
-#include "mrt_stream.hpp"
-namespace mrt {
-
-constexpr int kStreamMinWaves = 5;  // caps registers: the shading code would otherwise take 144 VGPRs
-
-template <int kShader, int kVariant>
-__global__ __launch_bounds__(TraceCfg<kVariant>::kThreads, kStreamMinWaves) void k_stream(
-    DScene s, StreamArgs A, int* counters, int2* gstack, int gdepth) {
-    using C = TraceCfg<kVariant>;
-    static_assert(C::kWide == 2, "streaming mode walks the BVH2");
-    __shared__ int2 ldsStack[C::kStack * C::kThreads];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * C::kThreads + threadIdx.x) * gdepth, 0,
-              C::kStack, C::kThreads};
-    __shared__ GNode ldsTop[C::kTop > 0 ? C::kTop : 1];
-    stageTop<C::kTop, C::kThreads>(s, ldsTop);
-    streamLoop<kShader, C::kWide, C::kRefill, C::kTop, C::kFastSlab>(s, A, counters, st, ldsTop);
-}
-
-// level counts for resolve / tally from the streaming counters; overflow and error flags
-__global__ void k_stream_finish(int* counters, int nLevels, StreamArgs A) {
-    const int l = static_cast<int>(threadIdx.x);
-    if (l < 1 || l > nLevels) return;
-    const int rays = l == 1 ? counters[cntRays(1)] : *streamCnt(counters, l, 0);
-    const int shadows = *streamCnt(counters, l, 2);
-    if (l > 1) counters[cntRays(l)] = min(rays, A.lv[l].cap);
-    counters[cntShadows(l)] = min(shadows, A.lv[l].shadowCap);
-    if (rays > A.lv[l].cap || shadows > A.lv[l].shadowCap) atomicOr(counters + kCntOverflow, 1);
-    if (l == 1) {
-        const int err = counters[kCntStream + (kMaxLevels * 4 + 1) * kFetchStride];
-        const int left = counters[kCntStream + kMaxLevels * 4 * kFetchStride];
-        if (err != 0 || left != 0) atomicOr(counters + kCntOverflow, 2);
+        if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, deadNext != 0);
     }
 }
 
@@ -978,151 +770,40 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
     hipLaunchKernelGGL(k_raygen, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, a, lv, counters);
 }
 
-// Persistent grid: the variant's own occupancy x CUs workgroups, capped by the thread count
-// the spill stacks were sized for.
+// Persistent grid: the kernel's own occupancy x CUs workgroups, capped by the thread count the
+// spill stacks were sized for.
 template <typename K>
-int persistentGrid(K kernel, int variant, int kind, int threads, int maxThreads) {
-    static int occ[5][kTraceVariants] = {};  // kind: 0 closest, 1 shadow, 2 combined, 3/4 streaming
+int persistentGrid(K kernel, int slot, int maxThreads) {
+    static int occ[8] = {};
     static int cus = 0;
-    const int cap = std::max(1, maxThreads / threads);
+    const int cap = std::max(1, maxThreads / kWalkThreads);
     if (cus == 0) {
         hipDeviceProp_t prop;
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return cap;
         cus = prop.multiProcessorCount;
     }
-    int& o = occ[kind][variant];
-    if (o == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, threads, 0) != hipSuccess) o = 0;
+    int& o = occ[slot];
+    if (o == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, kWalkThreads, 0) != hipSuccess) o = 0;
     return o > 0 ? std::min(cap, o * cus) : cap;
 }
 
-#define MRT_LAUNCH_ONE(KERNEL, KIND, V)                                                                     \
-    case V: {                                                                                                \
-        constexpr int kT = TraceCfg<V>::kThreads;                                                            \
-        const int g = persistentGrid(KERNEL<false, V>, V, KIND, kT, maxThreads);                            \
-        if (countStats)                                                                                      \
-            hipLaunchKernelGGL((KERNEL<true, V>), dim3(g), dim3(kT), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-        else                                                                                                 \
-            hipLaunchKernelGGL((KERNEL<false, V>), dim3(g), dim3(kT), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-        break;                                                                                               \
-    }
-#define MRT_LAUNCH_TRACE(KERNEL, KIND)                                                                        \
-    switch (s.variant) {                                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 0)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 1)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 2)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 3)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 4)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 5)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 6)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 7)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 8)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 9)                                                                      \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 10)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 11)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 12)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 13)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 14)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 15)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 16)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 17)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 18)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 19)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 20)                                                                     \
-        MRT_LAUNCH_ONE(KERNEL, KIND, 21)                                                                    \
-        default: MRT_LAUNCH_ONE(KERNEL, KIND, 22)                                                            \
-    }
-
-#define MRT_LAUNCH_COMBO_ONE(V)                                                                              \
-    case V: {                                                                                                \
-        constexpr int kT = TraceCfg<V>::kThreads;                                                            \
-        const int g = persistentGrid(k_combo<false, V>, V, 2, kT, maxThreads);                              \
-        if (countStats)                                                                                      \
-            hipLaunchKernelGGL((k_combo<true, V>), dim3(g), dim3(kT), 0, st, s, lv, prev, counters, level, gstack, gdepth, stats); \
-        else                                                                                                 \
-            hipLaunchKernelGGL((k_combo<false, V>), dim3(g), dim3(kT), 0, st, s, lv, prev, counters, level, gstack, gdepth, stats); \
-        break;                                                                                               \
-    }
-
-template <int kShader, int V>
-void launchStreamV(const DScene& s, const StreamArgs& A, int* counters, int2* gstack, int gdepth, int maxThreads,
-                   hipStream_t st) {
-    constexpr int kT = TraceCfg<V>::kThreads;
-    const int g = persistentGrid(k_stream<kShader, V>, V, kShader == kShaderWhitted ? 3 : 4, kT, maxThreads);
-    hipLaunchKernelGGL((k_stream<kShader, V>), dim3(g), dim3(kT), 0, st, s, A, counters, gstack, gdepth);
-}
-
-bool launchStream(int shader, const DScene& s, const Level* lv, int nLevels, uint32_t epoch, const ShadeArgs& a,
-                  int* counters, int2* gstack, int gdepth, int maxThreads, hipStream_t st) {
-    if (shader != kShaderWhitted && shader != kShaderPathTracer) return false;
-    if (s.textured != 0) return false;  // the Kd replay of textured scenes needs the level-by-level resolve
-    if (s.accel != kAccBVH && s.accel != kAccGrid) return false;
-    if (s.variant != 14 && s.variant != 13 && s.variant != 8) return false;
-    StreamArgs A{};
-    for (int l = 0; l < kMaxLevels; ++l) A.lv[l] = lv[l];
-    A.nLevels = nLevels;
-    A.epoch = epoch;
-    A.sa = a;
-    const bool w = shader == kShaderWhitted;
-    switch (s.variant) {
-        case 8:
-            w ? launchStreamV<kShaderWhitted, 8>(s, A, counters, gstack, gdepth, maxThreads, st)
-              : launchStreamV<kShaderPathTracer, 8>(s, A, counters, gstack, gdepth, maxThreads, st);
-            break;
-        case 13:
-            w ? launchStreamV<kShaderWhitted, 13>(s, A, counters, gstack, gdepth, maxThreads, st)
-              : launchStreamV<kShaderPathTracer, 13>(s, A, counters, gstack, gdepth, maxThreads, st);
-            break;
-        default:
-            w ? launchStreamV<kShaderWhitted, 14>(s, A, counters, gstack, gdepth, maxThreads, st)
-              : launchStreamV<kShaderPathTracer, 14>(s, A, counters, gstack, gdepth, maxThreads, st);
-            break;
-    }
-    return true;
-}
-
-void launchStreamFinish(int* counters, int nLevels, const Level* lv, hipStream_t st) {
-    StreamArgs A{};
-    for (int l = 0; l < kMaxLevels; ++l) A.lv[l] = lv[l];
-    A.nLevels = nLevels;
-    hipLaunchKernelGGL(k_stream_finish, dim3(1), dim3(64), 0, st, counters, nLevels, A);
-}
-
-bool traceVariantCompressed(int variant) {
-    return variant >= 0 && variant < kNumTraceVariants && kTraceCfg[variant].comp != 0;
-}
-
-bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,
-                 int gdepth, unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
-    if (s.accel != kAccBVH && s.accel != kAccGrid) return false;
-    switch (s.variant) {
-        MRT_LAUNCH_COMBO_ONE(1)
-        MRT_LAUNCH_COMBO_ONE(2)
-        MRT_LAUNCH_COMBO_ONE(3)
-        MRT_LAUNCH_COMBO_ONE(4)
-        MRT_LAUNCH_COMBO_ONE(5)
-        MRT_LAUNCH_COMBO_ONE(6)
-        MRT_LAUNCH_COMBO_ONE(7)
-        MRT_LAUNCH_COMBO_ONE(8)
-        MRT_LAUNCH_COMBO_ONE(9)
-        MRT_LAUNCH_COMBO_ONE(10)
-        MRT_LAUNCH_COMBO_ONE(11)
-        MRT_LAUNCH_COMBO_ONE(12)
-        MRT_LAUNCH_COMBO_ONE(13)
-        MRT_LAUNCH_COMBO_ONE(14)
-        MRT_LAUNCH_COMBO_ONE(15)
-        MRT_LAUNCH_COMBO_ONE(16)
-        MRT_LAUNCH_COMBO_ONE(17)
-        MRT_LAUNCH_COMBO_ONE(18)
-        MRT_LAUNCH_COMBO_ONE(19)
-        MRT_LAUNCH_COMBO_ONE(20)
-        MRT_LAUNCH_COMBO_ONE(21)
-        MRT_LAUNCH_COMBO_ONE(22)
-        default:
-            return false;  // variant 0 (per-wave batches): separate launches
-    }
-    return true;
-}
+#define MRT_LAUNCH_WALK(KERNEL, SLOT)                                                                           \
+    do {                                                                                                       \
+        if (s.variant == 0) {                                                                                  \
+            const int g = persistentGrid(KERNEL<false, 0>, SLOT, maxThreads);                                  \
+            if (countStats)                                                                                    \
+                hipLaunchKernelGGL((KERNEL<true, 0>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+            else                                                                                               \
+                hipLaunchKernelGGL((KERNEL<false, 0>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        } else {                                                                                               \
+            const int g = persistentGrid(KERNEL<false, 1>, SLOT + 1, maxThreads);                              \
+            if (countStats)                                                                                    \
+                hipLaunchKernelGGL((KERNEL<true, 1>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+            else                                                                                               \
+                hipLaunchKernelGGL((KERNEL<false, 1>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        }                                                                                                      \
+    } while (0)
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
@@ -1130,7 +811,7 @@ void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int
         hipLaunchKernelGGL((k_trace_other<false>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }
-    MRT_LAUNCH_TRACE(k_trace, 0);
+    MRT_LAUNCH_WALK(k_trace, 0);
 }
 
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
@@ -1139,17 +820,18 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
         hipLaunchKernelGGL((k_trace_other<true>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }
-    MRT_LAUNCH_TRACE(k_shadow, 1);
+    MRT_LAUNCH_WALK(k_shadow, 2);
 }
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
-                 const ShadeArgs& a, int grid, hipStream_t st) {
+                 const ShadeArgs& a, int grid, hipStream_t st, bool deadNext) {
+    const int dead = deadNext ? 1 : 0;
     switch (shader) {
         case kShaderWhitted:
-            hipLaunchKernelGGL(k_shade<kShaderWhitted>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a);
+            hipLaunchKernelGGL(k_shade<kShaderWhitted>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a, dead);
             break;
         case kShaderPathTracer:
-            hipLaunchKernelGGL(k_shade<kShaderPathTracer>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a);
+            hipLaunchKernelGGL(k_shade<kShaderPathTracer>, dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a, dead);
             break;
         case kShaderDepthMap:
             hipLaunchKernelGGL(k_shade_simple<kShaderDepthMap>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, a);
@@ -1199,74 +881,17 @@ void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStre
     hipLaunchKernelGGL(k_tally, dim3(1), dim3(1), 0, st, counters, maxLevel, stats, skippedLevel);
 }
 
-// ---------------------------------------------------------------------------------------
-// ray reordering (tuning key 4, off by default).  Measured on C4: closest-hit traversal of
-// levels 2-6 drops 10 % (9.5 -> 8.5 ms) with the full 30-bit key, but the radix sort of each
-// level costs ~0.9 ms, more than it saves; octant-only or coarse keys save under 0.4 ms.
-// Keying by the origin's primitive (BVH order) instead of the Morton code gains the same;
-// with only its top 10 bits (a counting sort's budget) the gain falls to 0.65 ms.
-__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 9 bits -> every third bit
-    v &= 0x1FFu;
-    v = (v | (v << 16)) & 0x030000FFu;
-    v = (v | (v << 8)) & 0x0300F00Fu;
-    v = (v | (v << 4)) & 0x030C30C3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-
-__global__ __launch_bounds__(256) void k_sort_keys(const float4* rO, const float4* rD, const int* countPtr, int cap,
-                                                   GRoot box, uint32_t* keys, int* vals) {
-    const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
-    if (i >= cap) return;
-    const int count = min(*countPtr, cap);
-    uint32_t key = 0xFFFFFFFFu;
-    if (i < count) {
-        const float4 o = rO[i];
-        const float4 d = rD[i];
-        const uint32_t oct = (d.x < 0.0F ? 1u : 0u) | (d.y < 0.0F ? 2u : 0u) | (d.z < 0.0F ? 4u : 0u);
-        auto q = [](float x, float lo, float hi) {
-            const float f = (x - lo) / fmaxf(hi - lo, 1e-30F);
-            return static_cast<uint32_t>(fminf(fmaxf(f, 0.0F), 0.999999F) * 512.0F);
-        };
-        const uint32_t m = spread3(q(o.x, box.bmin[0], box.bmax[0])) | (spread3(q(o.y, box.bmin[1], box.bmax[1])) << 1) |
-                           (spread3(q(o.z, box.bmin[2], box.bmax[2])) << 2);
-        key = (oct << 27) | m;
-    }
-    keys[i] = key;
-    vals[i] = i;
-}
-
-size_t sortRaysTempBytes(int cap) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
-                                             static_cast<uint32_t*>(nullptr), static_cast<const int*>(nullptr),
-                                             static_cast<int*>(nullptr), cap, 0, 30);
-    return bytes;
-}
-
-void sortRays(const float4* rO, const float4* rD, const int* count, int cap, const GRoot& box, uint32_t* keys,
-              uint32_t* keysAlt, int* vals, int* order, void* temp, size_t tempBytes, hipStream_t st) {
-    hipLaunchKernelGGL(k_sort_keys, dim3((cap + 255) / 256), dim3(256), 0, st, rO, rD, count, cap, box, keys, vals);
-    size_t bytes = tempBytes;
-    (void)hipcub::DeviceRadixSort::SortPairs(temp, bytes, keys, keysAlt, vals, order, cap, 0, 30, st);
-}
-
-template <int... V>
-int maxResidentThreads(std::integer_sequence<int, V...>) {
-    int best = kBlock;
-    const void* kernels[] = {reinterpret_cast<const void*>(k_trace<false, V>)...};
-    const int threads[] = {TraceCfg<V>::kThreads...};
-    for (size_t i = 0; i < sizeof...(V); ++i) {
+int traceResidentThreadsPerCU() {
+    // the spill stacks are sized for the walk with the most resident threads
+    int best = kWalkThreads;
+    const void* kernels[] = {reinterpret_cast<const void*>(k_trace<false, 0>), reinterpret_cast<const void*>(k_trace<false, 1>),
+                             reinterpret_cast<const void*>(k_shadow<false, 0>), reinterpret_cast<const void*>(k_shadow<false, 1>)};
+    for (const void* k : kernels) {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernels[i], threads[i], 0) == hipSuccess)
-            best = std::max(best, n * threads[i]);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWalkThreads, 0) == hipSuccess)
+            best = std::max(best, n * kWalkThreads);
     }
     return best;
-}
-
-int traceResidentThreadsPerCU() {
-    // the spill stacks are sized for the variant with the most resident threads
-    return maxResidentThreads(std::make_integer_sequence<int, kTraceVariants>{});
 }
 
 }  // namespace mrt

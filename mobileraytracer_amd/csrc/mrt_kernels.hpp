@@ -11,27 +11,21 @@ constexpr int kShaderDepthMap = 3;    // C_wrapper.cpp:175-179
 constexpr int kShaderDiffuse = 4;     // C_wrapper.cpp:181-186 (DiffuseMaterial)
 constexpr int kShaderNoShadows = 5;   // C_wrapper.cpp:188-193 (the switch's default: 0, 5, ...)
 constexpr int kMaxLevels = 16;           // max ray depth + 2
-constexpr int kTraceVariants = 23;       // trace-kernel organisations (mrt_kernels.hip kTraceCfg)
-constexpr int kDefaultTraceVariant = 14;
+constexpr int kTraceVariants = 2;        // 0: per-wave reference walk, 1: persistent while-while walk
+constexpr int kDefaultTraceVariant = 1;
 constexpr int kAccNaive = 1;  // Shader::Accelerator (Shader.hpp:20-24)
 constexpr int kAccGrid = 2;
 constexpr int kAccBVH = 3;
-constexpr int kExactTraceVariant = 14;    // stands in for compressed variants when a scene has no CNodes
-constexpr int kTopNodesMax = 128;        // BVH2 nodes numbered breadth-first (LDS-staged by some variants)
+constexpr int kTopNodesMax = 128;        // BVH2 nodes numbered breadth-first (staged in LDS by the walk)
 
 // Device counters (ints).  Pair l = {rays of level l+1, shadow rays of level l} sits on two
 // adjacent ints so k_shade allocates both with one 64-bit atomic per block.
 constexpr int kCntPairs = 0;                          // 2 * (kMaxLevels + 1) ints
-constexpr int kCntFetchTrace = 64;                    // kMaxLevels single work cursors
-constexpr int kCntFetchShadow = kCntFetchTrace + kMaxLevels;
-constexpr int kCntOverflow = kCntFetchShadow + kMaxLevels;
-constexpr int kMaxFetchShards = 32;                   // sharded work cursors per level
+constexpr int kCntOverflow = 64;
+constexpr int kMaxFetchShards = 8;                    // work cursors per level (one per XCD group)
 constexpr int kFetchStride = 32;                      // ints between cursors (a 128-byte line each)
 constexpr int kCntFetchShards = 128;                  // 2 kinds x kMaxLevels x kMaxFetchShards lines
-constexpr int kCntStream = kCntFetchShards + 2 * kMaxLevels * kMaxFetchShards * kFetchStride;
-// streaming mode: per level 4 lines (ray alloc, ray claim, shadow alloc, shadow claim), then
-// `pending` and the error flag
-constexpr int kNumCounters = kCntStream + (kMaxLevels * 4 + 2) * kFetchStride;
+constexpr int kNumCounters = kCntFetchShards + 2 * kMaxLevels * kMaxFetchShards * kFetchStride;
 MRT_HD constexpr int cntRays(int level) { return kCntPairs + 2 * (level - 1); }
 MRT_HD constexpr int cntShadows(int level) { return kCntPairs + 2 * level + 1; }
 
@@ -47,9 +41,7 @@ constexpr int kStatTrisShadow = 7;  // any-hit kernel: triangle tests (counting 
 constexpr int kStatLevelRays = 8;                     // + level - 1: rays of each level
 constexpr int kStatLevelShadows = 8 + kMaxLevels;     // + level - 1: shadow rays of each level
 constexpr int kStatMaxNodesRay = 8 + 2 * kMaxLevels;  // counting builds: most node records of one ray
-constexpr int kStatAssist = kStatMaxNodesRay + 1;    // tail-assist variants: subtrees handed over
-constexpr int kStatMaxRayTicks = kStatAssist + 1;    // tail-assist variants: longest ray (100 MHz ticks)
-constexpr int kStatSkipped = kStatMaxRayTicks + 1;     // rays of a last level whose walk was skipped
+constexpr int kStatSkipped = kStatMaxNodesRay + 1;   // rays of a last level whose walk was skipped
 constexpr int kNumStats = kStatSkipped + 1;
 
 // One level of the wavefront (SoA queues).
@@ -65,10 +57,6 @@ struct Level {
     float4* sO;      // shadow ray origin, w = source primitive bits
     float4* sD;      // shadow ray direction, w = distance to the light
     float4* sC;      // light contribution Le*cos, w = occluded flag
-    uint32_t* ready;         // streaming mode: per ray slot, = epoch once its payload is stored
-    uint32_t* sReady;        // the same for the shadow ray slots
-    const int* order;        // trace visit order of the rays (null: queue order)
-    const int* shadowOrder;  // the same for the shadow rays
     // textured scenes: the texel this vertex's hit wrote into its material's Kd (xyz, w = the
     // material index, -1 none), and the last such write in the vertex's subtree (Shader.cpp:112-120)
     float4* kd;
@@ -118,21 +106,11 @@ struct AccumArgs {
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
-// streaming mode: every level of the pass in one persistent launch (mrt_stream.hpp); returns
-// false for shaders / variants without that form.  lv[0..kMaxLevels), epoch as StreamArgs.
-bool launchStream(int shader, const DScene& s, const Level* lv, int nLevels, uint32_t epoch, const ShadeArgs& a,
-                  int* counters, int2* gstack, int gdepth, int maxThreads, hipStream_t st);
-void launchStreamFinish(int* counters, int nLevels, const Level* lv, hipStream_t st);
-// closest-hit rays of `level` then shadow rays of level - 1 in one launch; false if the trace
-// variant has no such form (the caller then launches them separately)
-// kTraceCfg row `variant` walks compressed nodes (needs DScene::compOk)
-bool traceVariantCompressed(int variant);
-bool launchCombo(const DScene& s, const Level& lv, const Level& prev, int* counters, int level, int2* gstack,
-                 int gdepth, unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
+// deadNext: level + 1 is the depth-capped last level (its rays are counted, never written)
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
-                 const ShadeArgs& a, int grid, hipStream_t st);
+                 const ShadeArgs& a, int grid, hipStream_t st, bool deadNext = false);
 // deadChildren: level + 1 is the depth-capped last level, whose results are all zero; its
 // records are then not read (a zero child adds exactly nothing, section 3 of DESIGN.md)
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
@@ -141,11 +119,6 @@ void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, in
 void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st);
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);
 void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel = 0);
-int traceResidentThreadsPerCU();
-// Ray reordering for traversal coherence: keys = direction octant | Morton code of the origin
-// in the scene box, radix-sorted with the ray index; `order` receives the visit order.
-size_t sortRaysTempBytes(int cap);
-void sortRays(const float4* rO, const float4* rD, const int* count, int cap, const GRoot& box, uint32_t* keys,
-              uint32_t* keysAlt, int* vals, int* order, void* temp, size_t tempBytes, hipStream_t st);  // max over trace variants of resident threads per CU
+int traceResidentThreadsPerCU();  // max over the trace walks of resident threads per CU
 
 }  // namespace mrt

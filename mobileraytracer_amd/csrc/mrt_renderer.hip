@@ -96,7 +96,7 @@ struct mrt_renderer {
     mrt::GCamera cam{};
     mrt::DScene ds{};
     std::vector<int32_t> triOrder, planeOrder, sphereOrder;
-    int64_t nTri = 0, nLights = 0, nPlanes = 0, nSpheres = 0, nMats = 0, nTriNodes = 0, nTriNodes4 = 0;
+    int64_t nTri = 0, nLights = 0, nPlanes = 0, nSpheres = 0, nMats = 0, nTriNodes = 0;
     int triDepth = 0, maxBvhDepth = 0;
     int stackNeed = 0;  // worst-case traversal stack entries over all node layouts
 
@@ -108,35 +108,18 @@ struct mrt_renderer {
 
     // queues
     DeviceMem sceneMem, queueMem, frameMem;  // frameMem: bitmaps, kept when the queues are resized
-    struct SortBufs {
-        uint32_t* keys = nullptr;
-        uint32_t* keysAlt = nullptr;
-        int* vals = nullptr;
-        int* order = nullptr;
-        void* temp = nullptr;
-        size_t tempBytes = 0;
-        int cap = 0;
-    };
-    // A pipeline renders chunks of pixel slots on its own pair of streams with its own queues.
-    // Chunks of different pipelines run concurrently, so one chunk's level-to-level drains
-    // (every level waits for its slowest ray) are filled by another chunk's work.
+    // The wavefront queues of one chunk of pixel slots, and the two streams it runs on.
     struct Pipe {
         mrt::Level levels[mrt::kMaxLevels]{};
         int* counters = nullptr;
         unsigned long long* stats = nullptr;
         int2* gstack = nullptr;        // spill stacks of the closest-hit kernel ...
         int2* gstackShadow = nullptr;  // ... and of the any-hit kernel (the two can run together)
-        SortBufs sortRay, sortShadow;
-        hipStream_t stream = nullptr;        // raygen, closest-hit, shade, resolve, accumulate
         hipStream_t shadowStream = nullptr;  // any-hit launches, overlapped with the next level
         std::vector<hipEvent_t> syncPool;    // ordering events between the streams
         std::vector<hipEvent_t> evPool;      // profiling: 5 timing events per level and chunk
         size_t evCount = 0;
-    };
-    std::vector<Pipe> pipes;
-    int nPipes = 1;                      // tuning key 5 (more pipelines measured slower)
-    int streamMode = 0;                  // tuning key 6: every level of a pass in one launch
-    uint32_t epoch = 0;                  // streaming mode: ready-flag value of the current pass
+    } pipe;
     int chunkSlots = 0;
     int gdepth = 0;
     int traceThreads = 0, workGrid = 0;  // traceThreads: resident trace threads, whole device
@@ -144,9 +127,7 @@ struct mrt_renderer {
     int32_t* dBackup = nullptr;  // progressive mode: the running average before the current pass
     size_t backupN = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t forkEvent = nullptr;
     int overlap = 1;                     // tuning key 3: shadow rays on their own stream
-    int sortRays = 0;                    // tuning key 4: reorder rays before tracing (1 closest-hit, 2 shadow)
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
     bool walkSkipped = false;            // the last pass skipped that walk
 
@@ -158,13 +139,9 @@ struct mrt_renderer {
     mrt_frame_stats last{};
 
     ~mrt_renderer() {
-        for (Pipe& p : pipes) {
-            for (hipEvent_t e : p.evPool) (void)hipEventDestroy(e);
-            for (hipEvent_t e : p.syncPool) (void)hipEventDestroy(e);
-            if (p.stream != nullptr) (void)hipStreamDestroy(p.stream);
-            if (p.shadowStream != nullptr) (void)hipStreamDestroy(p.shadowStream);
-        }
-        if (forkEvent != nullptr) (void)hipEventDestroy(forkEvent);
+        for (hipEvent_t e : pipe.evPool) (void)hipEventDestroy(e);
+        for (hipEvent_t e : pipe.syncPool) (void)hipEventDestroy(e);
+        if (pipe.shadowStream != nullptr) (void)hipStreamDestroy(pipe.shadowStream);
         if (stream != nullptr) (void)hipStreamDestroy(stream);
     }
 };
@@ -253,60 +230,8 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
 
     std::vector<GNode> g;
     DScene& d = r->ds;
-    // node layout below the LDS top: 0 depth-first pre-order, 1 random (diagnostic), 2 line pairs
-    const char* nl = std::getenv("MRT_NODE_LAYOUT");
-    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop, nl != nullptr ? std::atoi(nl) : 0);
+    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop);
     d.triNodes = r->sceneMem.upload(g, st);
-    {
-        std::vector<CNode> cn;
-        std::vector<float> lb;
-        d.compOk = toDeviceCBVH(g, d.triTop, d.triRoot, sc.triangles.size(), &cn, &lb) ? 1 : 0;
-        d.triCNodes = r->sceneMem.upload(cn, st);
-        d.leafBoxes = r->sceneMem.upload(lb, st);
-    }
-    {
-        // the exact box of each triangle's leaf (its parent's record of it), for the shadow
-        // walk's last-occluder test (trace variant 22)
-        const size_t nt = sc.triangles.size();
-        std::vector<float> ob(std::max<size_t>(nt, 1) * 8, 0.0F);
-        auto fill = [&](int32_t lref, float x0, float y0, float z0, float x1, float y1, float z1) {
-            const int f = leafFirst(lref), n = leafCount(lref);
-            for (int k = f; k < f + n && k < static_cast<int>(nt); ++k) {
-                const float b[6] = {x0, y0, z0, x1, y1, z1};
-                std::copy(b, b + 6, ob.begin() + 8 * static_cast<size_t>(k));
-            }
-        };
-        if (nt > 0) {
-            const GRoot& rt = d.triRoot;
-            if (rt.ref < 0) fill(rt.ref, rt.bmin[0], rt.bmin[1], rt.bmin[2], rt.bmax[0], rt.bmax[1], rt.bmax[2]);
-            for (const GNode& n : g) {
-                if (n.refL < 0) fill(n.refL, n.lminx, n.lminy, n.lminz, n.lmaxx, n.lmaxy, n.lmaxz);
-                if (n.refR < 0) fill(n.refR, n.rminx, n.rminy, n.rminz, n.rmaxx, n.rmaxy, n.rmaxz);
-            }
-        }
-        d.occBoxes = r->sceneMem.upload(ob, st);
-    }
-    {
-        std::vector<GNode4> g4;
-        toDeviceBVH4(tn, sc.triangles.size(), &g4, &d.triRoot4);
-        d.triNodes4 = r->sceneMem.upload(g4, st);
-        r->nTriNodes4 = static_cast<int64_t>(g4.size());
-        // depth of the 4-wide tree: a 4-wide walk pushes up to 3 entries per level
-        int depth4 = 0;
-        if (!g4.empty()) {
-            std::vector<std::pair<int, int>> stk{{0, 1}};
-            while (!stk.empty()) {
-                const auto [i, dd] = stk.back();
-                stk.pop_back();
-                depth4 = std::max(depth4, dd);
-                for (int k = 0; k < 4; ++k) {
-                    const int c = g4[static_cast<size_t>(i)].ref[k];
-                    if (c >= 0 && c != kRefEmpty) stk.push_back({c, dd + 1});
-                }
-            }
-        }
-        r->stackNeed = std::max(r->stackNeed, 3 * depth4 + 2);
-    }
     toDeviceBVH(pn, sc.planes.size(), &g, &d.planeRoot);
     d.planeNodes = r->sceneMem.upload(g, st);
     toDeviceBVH(sn, sc.spheres.size(), &g, &d.sphereRoot);
@@ -397,9 +322,14 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.nLights = static_cast<int32_t>(sc.lights.size());
     d.nMats = static_cast<int32_t>(sc.materials.size());
     d.cull = r->cfg.cull;
-    const char* tv = std::getenv("MRT_TRACE_VARIANT");
-    d.variant = tv != nullptr ? std::atoi(tv) : kDefaultTraceVariant;
-    if (traceVariantCompressed(d.variant) && d.compOk == 0) d.variant = kExactTraceVariant;
+    d.variant = kDefaultTraceVariant;
+    // the depth-capped last level's children count as absent in the resolve only while no
+    // material coefficient is infinite or NaN (inf * 0 would be NaN in the reference)
+    d.matsFinite = 1;
+    for (const HMaterial& m : sc.materials) {
+        for (const v3 c : {m.Kd, m.Ks, m.Kt})
+            if (!std::isfinite(c.x) || !std::isfinite(c.y) || !std::isfinite(c.z)) d.matsFinite = 0;
+    }
 
     // the two sample tables interleaved: one vertex's draws (consecutive indices, both
     // tables) share one or two cache lines
@@ -425,97 +355,45 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     const size_t capN = n1 * static_cast<size_t>(growth);
     const int nLevels = r->nLevels;
     r->gdepth = std::max(1, r->stackNeed - kLdsStackMin);
-    const size_t nChunks = (static_cast<size_t>(r->nSlots) + chunkSlots - 1) / static_cast<size_t>(chunkSlots);
-    const size_t nPipes = std::max<size_t>(1, std::min<size_t>(static_cast<size_t>(r->nPipes), nChunks));
-    while (r->pipes.size() < nPipes) {
-        r->pipes.emplace_back();
-        if (r->pipes.size() > 1) MRT_HIP(hipStreamCreateWithFlags(&r->pipes.back().stream, hipStreamNonBlocking));
-        MRT_HIP(hipStreamCreateWithFlags(&r->pipes.back().shadowStream, hipStreamNonBlocking));
+    mrt_renderer::Pipe& pp = r->pipe;
+    if (pp.shadowStream == nullptr) MRT_HIP(hipStreamCreateWithFlags(&pp.shadowStream, hipStreamNonBlocking));
+    // Ray / hit / payload buffers of levels L and L+2 are never live together (level L's rays are
+    // dead once k_shade(L) has read them; its vertex and result records stay until the resolve),
+    // but one set per level keeps the shadow stream's overlap free of reuse hazards.
+    for (int l = 1; l <= nLevels + 1 && l < kMaxLevels; ++l) {
+        Level& lv = pp.levels[l];
+        const size_t cap = (l == 1) ? n1 : capN;
+        const bool real = l <= nLevels;
+        lv = Level{};
+        lv.cap = real ? static_cast<int>(cap) : 0;
+        lv.shadowCap = real ? static_cast<int>(cap * spl) : 0;
+        const size_t rays = real ? cap : 0;  // level nLevels + 1: no rays (its parents are terminal)
+        lv.rO = r->queueMem.alloc<float4>(rays);
+        lv.rD = r->queueMem.alloc<float4>(rays);
+        lv.tree = r->queueMem.alloc<uint32_t>(rays);
+        lv.hit = r->queueMem.alloc<float4>(rays);
+        if (real) {
+            lv.sO = r->queueMem.alloc<float4>(cap * spl);
+            lv.sD = r->queueMem.alloc<float4>(cap * spl);
+            lv.vtx = r->queueMem.alloc<int4>(cap);
+            lv.res = r->queueMem.alloc<float4>(cap);
+            lv.sC = r->queueMem.alloc<float4>(cap * spl);
+        }
+        const bool tex = real && r->ds.textured != 0;
+        lv.kd = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
+        lv.last = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
     }
-    for (size_t pi = 0; pi < r->pipes.size(); ++pi) {
-        mrt_renderer::Pipe& pp = r->pipes[pi];
-        if (pi >= nPipes) {  // idle pipeline: no queues
-            for (Level& lv : pp.levels) lv = Level{};
-            pp.counters = nullptr;
-            continue;
-        }
-        // ray / hit / shadow buffers: one set per level (the streaming mode keeps every level
-        // live at once; the level-by-level mode could alternate two sets)
-        const int nBuf = std::min(nLevels + 1, kMaxLevels - 1);
-        std::vector<float4*> rO(nBuf + 1), rD(nBuf + 1), hit(nBuf + 1), sO(nBuf + 1), sD(nBuf + 1);
-        std::vector<uint32_t*> tree(nBuf + 1), ready(nBuf + 1), sReady(nBuf + 1);
-        for (int k = 1; k <= nBuf; ++k) {
-            const size_t cap = (k == 1) ? n1 : capN;
-            rO[k] = r->queueMem.alloc<float4>(cap);
-            rD[k] = r->queueMem.alloc<float4>(cap);
-            tree[k] = r->queueMem.alloc<uint32_t>(cap);
-            hit[k] = r->queueMem.alloc<float4>(cap);
-            ready[k] = r->queueMem.alloc<uint32_t>(cap);
-            MRT_HIP(hipMemset(ready[k], 0, cap * sizeof(uint32_t)));
-            if (k <= nLevels) {
-                sO[k] = r->queueMem.alloc<float4>(cap * spl);
-                sD[k] = r->queueMem.alloc<float4>(cap * spl);
-                sReady[k] = r->queueMem.alloc<uint32_t>(cap * spl);
-                MRT_HIP(hipMemset(sReady[k], 0, cap * spl * sizeof(uint32_t)));
-            } else {
-                sO[k] = sD[k] = nullptr;
-                sReady[k] = nullptr;
-            }
-        }
-        for (int l = 1; l <= nLevels + 1 && l < kMaxLevels; ++l) {
-            Level& lv = pp.levels[l];
-            const size_t cap = (l == 1) ? n1 : capN;
-            const bool real = l <= nLevels;
-            lv.cap = real ? static_cast<int>(cap) : 0;
-            lv.shadowCap = real ? static_cast<int>(cap * spl) : 0;
-            lv.rO = rO[l];
-            lv.rD = rD[l];
-            lv.tree = tree[l];
-            lv.hit = hit[l];
-            lv.sO = sO[l];
-            lv.sD = sD[l];
-            lv.ready = ready[l];
-            lv.sReady = sReady[l];
-            lv.order = nullptr;
-            lv.shadowOrder = nullptr;
-            if (real) {
-                lv.vtx = r->queueMem.alloc<int4>(cap);
-                lv.res = r->queueMem.alloc<float4>(cap);
-                lv.sC = r->queueMem.alloc<float4>(cap * spl);
-            } else {
-                lv.vtx = nullptr;
-                lv.res = nullptr;
-                lv.sC = nullptr;
-            }
-            const bool tex = real && r->ds.textured != 0;
-            lv.kd = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
-            lv.last = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
-        }
-        auto sortBufs = [&](mrt_renderer::SortBufs* b, size_t cap) {
-            b->cap = static_cast<int>(cap);
-            b->keys = r->queueMem.alloc<uint32_t>(cap);
-            b->keysAlt = r->queueMem.alloc<uint32_t>(cap);
-            b->vals = r->queueMem.alloc<int>(cap);
-            b->order = r->queueMem.alloc<int>(cap);
-            b->tempBytes = sortRaysTempBytes(b->cap);
-            b->temp = r->queueMem.alloc<uint8_t>(b->tempBytes);
-        };
-        sortBufs(&pp.sortRay, capN);
-        sortBufs(&pp.sortShadow, capN * spl);
-        pp.counters = r->queueMem.alloc<int>(kNumCounters);
-        pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats);
-        pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
-        pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
-    }
+    pp.counters = r->queueMem.alloc<int>(kNumCounters);
+    pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats);
+    pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
+    pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
 }
 
-// Chunk size for a target pipeline count: every pipeline gets work, within the path budget.
-int chunkFor(const mrt_renderer* r, int nPipes) {
+// Chunk size: every slot of the shard in one pass, within the path budget.
+int chunkFor(const mrt_renderer* r) {
     const size_t spp = static_cast<size_t>(std::max(1, r->cfg.samplesPixel));
     const size_t maxPaths = r->cfg.maxPathsPerPass > 0 ? static_cast<size_t>(r->cfg.maxPathsPerPass) : (size_t{1} << 24);
-    const size_t nSlots = static_cast<size_t>(r->nSlots);
-    const size_t perPipe = (nSlots + static_cast<size_t>(nPipes) - 1) / static_cast<size_t>(std::max(1, nPipes));
-    return static_cast<int>(std::max<size_t>(1, std::min(perPipe, maxPaths / spp)));
+    return static_cast<int>(std::max<size_t>(1, std::min(static_cast<size_t>(r->nSlots), maxPaths / spp)));
 }
 
 hipEvent_t syncEvent(mrt_renderer::Pipe& p, size_t i) {
@@ -538,16 +416,7 @@ hipEvent_t poolEvent(mrt_renderer::Pipe& p) {
 }
 
 // One pass over this shard's pixel slots: samples [sampleBase, sampleBase + spp).
-// Returns false if the queues overflowed (caller grows them and re-renders).
-bool s_comboCapable(int variant) { return variant > 0; }  // k_combo exists for while-while variants
-
-int activePipes(const mrt_renderer* r) {
-    int n = 0;
-    while (n < static_cast<int>(r->pipes.size()) && r->pipes[static_cast<size_t>(n)].counters != nullptr) ++n;
-    return n;
-}
-
-bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp) {
+void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp) {
     using namespace mrt;
     const int shader = r->shader;
     const bool timing = (r->profileFlags & 1) != 0;
@@ -555,28 +424,30 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     ShadeArgs sa{r->maxDepth, std::max(1, r->cfg.samplesLight), {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z}};
     const int nLevels = r->nLevels;
     const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
-    // fork: every pipeline starts after the work already queued on st
-    // Pipeline 0 runs on the caller's stream st (each extra stream costs a hardware queue:
-    // GPU_MAX_HW_QUEUES is 4, and two streams sharing one serialise); pipelines 1.. fork
-    // from st and join back.
-    const int nPipes = activePipes(r);
-    auto mainStream = [&](int pi) { return pi == 0 ? st : r->pipes[static_cast<size_t>(pi)].stream; };
-    if (nPipes > 1) {
-        if (r->forkEvent == nullptr) MRT_HIP(hipEventCreateWithFlags(&r->forkEvent, hipEventDisableTiming));
-        MRT_HIP(hipEventRecord(r->forkEvent, st));
-    }
-    for (int pi = 0; pi < nPipes; ++pi) {
-        mrt_renderer::Pipe& pp = r->pipes[static_cast<size_t>(pi)];
-        if (pi > 0) MRT_HIP(hipStreamWaitEvent(pp.stream, r->forkEvent, 0));
-        MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * kNumStats, mainStream(pi)));
-        pp.evCount = 0;
-    }
-    int chunk = 0;
-    for (int slot0 = 0; slot0 < r->nSlots && !r->stopFlag.load(); slot0 += r->chunkSlots, ++chunk) {
-        mrt_renderer::Pipe& pp = r->pipes[static_cast<size_t>(chunk % nPipes)];
-        const hipStream_t ps = mainStream(chunk % nPipes);
+    mrt_renderer::Pipe& pp = r->pipe;
+    MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * kNumStats, st));
+    pp.evCount = 0;
+    // Any-hit (shadow) rays of level L run on a second stream, overlapped with the closest-hit
+    // trace and shading of level L+1: the persistent kernels' drain phases fill each other.
+    // Orders: shade(L) -> shadow(L); shadow(L) -> shade(L+2) (shade(L+2) rewrites level L+2's
+    // shadow queue only, but the walk kernels share nothing else, so the order is for the spill
+    // stacks' sake: one per kernel kind); every shadow(L) -> resolve.
+    hipStream_t sb = r->overlap == 1 ? pp.shadowStream : st;
+    // The last level (depth RayDepthMax + 1) shades to zero whatever its rays hit: shade()
+    // returns at the depth cap (PathTracer.cpp:24-26, Whitted.cpp:15-17), so its closest-hit
+    // walk is dead work and is skipped.  Not for textured scenes (rayTrace writes the texel Kd
+    // before shade() returns, Shader.cpp:114-122).
+    const bool skipLast = r->skipLast != 0 && r->ds.textured == 0 &&
+                          (shader == kShaderWhitted || shader == kShaderPathTracer) && nLevels > r->maxDepth;
+    r->walkSkipped = skipLast;
+    // ... and with it the level's shading (every record terminal, radiance 0) and resolve: the
+    // parents' resolve treats the capped children as absent, which gives the same bits while
+    // every material is finite (Ks * 0 and Kd * 0 added to sums that start at +0), and the
+    // parents write no payload for them (only their count)
+    const bool skipLastShade = skipLast && nLevels >= 2 && r->ds.matsFinite != 0;
+    for (int slot0 = 0; slot0 < r->nSlots && !r->stopFlag.load(); slot0 += r->chunkSlots) {
         const int nChunk = std::min(r->chunkSlots, r->nSlots - slot0);
-        MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, ps));
+        MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
         RaygenArgs ra{};
         ra.cam = r->cam;
         ra.map = map;
@@ -588,110 +459,44 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.spp = spp;
         ra.sppTotal = r->cfg.samplesPixel;
         ra.sampleBase = sampleBase;
-        launchRaygen(ra, pp.levels[1], pp.counters, ps);
-        if (r->streamMode != 0 && !counting) {
-            // streaming mode: `pending` starts at the camera-ray count; the flags of a new pass
-            // compare against a fresh epoch (no clearing between passes)
-            const uint32_t epoch = ++r->epoch;
-            int* pendingPtr = pp.counters + kCntStream + kMaxLevels * 4 * kFetchStride;
-            MRT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(pendingPtr), ra.nPaths, 1, ps));
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
-            const bool ok = launchStream(shader, r->ds, pp.levels, nLevels, epoch, sa, pp.counters, pp.gstack, r->gdepth,
-                                         r->traceThreads, ps);
-            if (ok) {
-                if (timing) {
-                    for (int k = 0; k < 4; ++k) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
-                }
-                launchStreamFinish(pp.counters, nLevels, pp.levels, ps);
-                for (int l = nLevels; l >= 1; --l)
-                    launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
-                AccumArgs aa{};
-                aa.map = map;
-                aa.width = r->cfg.width;
-                aa.slotBase = slot0;
-                aa.nSlots = nChunk;
-                aa.spp = spp;
-                aa.sampleBase = sampleBase;
-                launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, ps);
-                launchTally(pp.counters, nLevels, pp.stats, ps);
-                continue;
-            }
-            if (timing) pp.evCount -= 1;  // not launched: fall back to the level-by-level form
-        }
-        // Any-hit (shadow) rays of level L run on a second stream, overlapped with the
-        // closest-hit trace and shading of level L+1: the persistent kernels' drain phases fill
-        // each other.  Orders: shade(L) -> shadow(L); shadow(L) -> shade(L+2) (the shadow ray
-        // buffers alternate by level); every shadow(L) -> resolve.
-        hipStream_t sb = r->overlap == 1 ? pp.shadowStream : ps;
-        const bool comboMode = r->overlap == 2 && s_comboCapable(r->ds.variant);
-        // The last level (depth RayDepthMax + 1) shades to zero whatever its rays hit: shade()
-        // returns at the depth cap (PathTracer.cpp:24-26, Whitted.cpp:15-17), so its
-        // closest-hit walk is dead work and is skipped.  Not for textured scenes (rayTrace
-        // writes the texel Kd before shade() returns, Shader.cpp:114-122) nor in the combined
-        // launch (which also carries the previous level's shadow rays).
-        const bool skipLast = r->skipLast != 0 && r->ds.textured == 0 && r->overlap != 2 &&
-                              (shader == kShaderWhitted || shader == kShaderPathTracer) && nLevels > r->maxDepth;
-        r->walkSkipped = skipLast;
-        // ... and with it the level's shading (every record terminal, radiance 0) and resolve:
-        // the parents' resolve treats the capped children as absent, which gives the same bits
-        const bool skipLastShade = skipLast && nLevels >= 2 && r->ds.textured == 0;
+        launchRaygen(ra, pp.levels[1], pp.counters, st);
         size_t sync = 0;
         hipEvent_t shadowDone[kMaxLevels] = {};
-        if (sb != ps) {
+        if (sb != st) {
             const hipEvent_t start = syncEvent(pp, sync++);
-            MRT_HIP(hipEventRecord(start, ps));
+            MRT_HIP(hipEventRecord(start, st));
             MRT_HIP(hipStreamWaitEvent(sb, start, 0));
         }
         for (int l = 1; l <= nLevels; ++l) {
-            Level& lv = pp.levels[l];
-            lv.order = nullptr;
-            lv.shadowOrder = nullptr;
-            if ((r->sortRays & 1) != 0 && l >= 2) {
-                const auto& b = pp.sortRay;
-                sortRays(lv.rO, lv.rD, pp.counters + cntRays(l), std::min(lv.cap, b.cap), r->ds.triRoot, b.keys,
-                         b.keysAlt, b.vals, b.order, b.temp, b.tempBytes, ps);
-                lv.order = b.order;
-            }
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
-            // overlap 2: this level's closest-hit rays and the previous level's shadow rays in
-            // one launch (the previous level's shadow launch below was skipped)
-            const bool combined =
-                r->overlap == 2 && launchCombo(r->ds, pp.levels[l], pp.levels[l - 1], pp.counters, l, pp.gstack, r->gdepth,
-                                               pp.stats, counting, r->traceThreads, ps);
-            if (!combined && !(skipLast && l == nLevels))
-                launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, ps);
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
-            if (sb != ps && l >= 3) MRT_HIP(hipStreamWaitEvent(ps, shadowDone[l - 2], 0));
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
+            if (!(skipLast && l == nLevels))
+                launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, st);
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
+            if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             if (!(skipLastShade && l == nLevels))
-                launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps);
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ps));
-            if (sb != ps) {
+                launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, st,
+                            skipLastShade && l + 1 == nLevels);
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
+            if (sb != st) {
                 const hipEvent_t shaded = syncEvent(pp, sync++);
-                MRT_HIP(hipEventRecord(shaded, ps));
+                MRT_HIP(hipEventRecord(shaded, st));
                 MRT_HIP(hipStreamWaitEvent(sb, shaded, 0));
             }
-            if (l < nLevels && (r->sortRays & 2) != 0) {
-                const auto& b = pp.sortShadow;
-                sortRays(lv.sO, lv.sD, pp.counters + cntShadows(l), std::min(lv.shadowCap, b.cap), r->ds.triRoot, b.keys,
-                         b.keysAlt, b.vals, b.order, b.temp, b.tempBytes, sb);
-                lv.shadowOrder = b.order;
-            }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
-            // the last level (depth > RayDepthMax) shades nothing: no shadow rays; in combined
-            // mode the next level's launch takes them
-            if (l < nLevels && !comboMode) {
+            // the last level (depth > RayDepthMax) shades nothing: no shadow rays
+            if (l < nLevels) {
                 launchShadow(r->ds, pp.levels[l], pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
                              r->traceThreads, sb);
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
-            if (sb != ps) {
+            if (sb != st) {
                 shadowDone[l] = syncEvent(pp, sync++);
                 MRT_HIP(hipEventRecord(shadowDone[l], sb));
             }
         }
-        if (sb != ps) MRT_HIP(hipStreamWaitEvent(ps, shadowDone[nLevels], 0));
+        if (sb != st) MRT_HIP(hipStreamWaitEvent(st, shadowDone[nLevels], 0));
         for (int l = skipLastShade ? nLevels - 1 : nLevels; l >= 1; --l) {
-            launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, ps,
+            launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, st,
                           skipLastShade && l == nLevels - 1);
         }
         AccumArgs aa{};
@@ -701,17 +506,9 @@ bool renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         aa.nSlots = nChunk;
         aa.spp = spp;
         aa.sampleBase = sampleBase;
-        launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, ps);
-        launchTally(pp.counters, nLevels, pp.stats, ps, skipLast ? nLevels : 0);
+        launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, st);
+        launchTally(pp.counters, nLevels, pp.stats, st, skipLast ? nLevels : 0);
     }
-    // join: st continues after every pipeline
-    for (int pi = 1; pi < nPipes; ++pi) {
-        mrt_renderer::Pipe& pp = r->pipes[static_cast<size_t>(pi)];
-        const hipEvent_t done = syncEvent(pp, 4 * kMaxLevels);
-        MRT_HIP(hipEventRecord(done, pp.stream));
-        MRT_HIP(hipStreamWaitEvent(st, done, 0));
-    }
-    return true;
 }
 
 // One pass (samples [sampleBase, sampleBase + spp)) with its statistics added to *fs.
@@ -721,20 +518,10 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     using namespace mrt;
     const auto t0 = std::chrono::steady_clock::now();
     renderPass(r, dBitmap, dPacked, st, sampleBase, spp);
-    const int nPipes = activePipes(r);
-    std::vector<unsigned long long> all(static_cast<size_t>(nPipes) * kNumStats);
-    for (int pi = 0; pi < nPipes; ++pi)
-        MRT_HIP(hipMemcpyAsync(all.data() + static_cast<size_t>(pi) * kNumStats, r->pipes[static_cast<size_t>(pi)].stats,
-                               sizeof(unsigned long long) * kNumStats, hipMemcpyDeviceToHost, st));
+    unsigned long long hs[kNumStats] = {};
+    MRT_HIP(hipMemcpyAsync(hs, r->pipe.stats, sizeof(unsigned long long) * kNumStats, hipMemcpyDeviceToHost, st));
     MRT_HIP(hipStreamSynchronize(st));
     const auto t1 = std::chrono::steady_clock::now();
-    unsigned long long hs[kNumStats] = {};
-    for (int pi = 0; pi < nPipes; ++pi) {
-        const unsigned long long* ps = all.data() + static_cast<size_t>(pi) * kNumStats;
-        for (int k = 0; k < kNumStats; ++k)
-            hs[k] = (k == kStatMaxNodesRay || k == kStatMaxRayTicks) ? std::max(hs[k], ps[k]) : hs[k] + ps[k];
-    }
-    if ((hs[kStatOverflow] & 2) != 0) throw std::runtime_error("streaming kernel: bounded wait exceeded or items left");
     if (hs[kStatOverflow] != 0) return false;
     fs->rays += hs[kStatRays];
     fs->shadowRays += hs[kStatShadowRays];
@@ -745,30 +532,27 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->shadowNodeRecords += hs[kStatNodesShadow];
     fs->shadowTriTests += hs[kStatTrisShadow];
     fs->maxNodeRecordsPerRay = std::max<uint64_t>(fs->maxNodeRecordsPerRay, hs[kStatMaxNodesRay]);
-    fs->assistedSubtrees += hs[kStatAssist];
-    fs->maxRayMicros = std::max<uint64_t>(fs->maxRayMicros, hs[kStatMaxRayTicks] / 100);
     for (int l = 0; l < kMaxLevels; ++l) {
         fs->levelRays[l] += hs[kStatLevelRays + l];
         fs->levelShadowRays[l] += hs[kStatLevelShadows + l];
     }
     fs->frameMs += std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (r->profileFlags & 1) {
-        for (int pi = 0; pi < nPipes; ++pi) {
-            const mrt_renderer::Pipe& pp = r->pipes[static_cast<size_t>(pi)];
-            for (size_t e = 0; e + 4 < pp.evCount; e += 5) {
-                float ta = 0.0F, tb = 0.0F, tc = 0.0F;
-                MRT_HIP(hipEventElapsedTime(&ta, pp.evPool[e], pp.evPool[e + 1]));
-                MRT_HIP(hipEventElapsedTime(&tc, pp.evPool[e + 1], pp.evPool[e + 2]));
-                MRT_HIP(hipEventElapsedTime(&tb, pp.evPool[e + 3], pp.evPool[e + 4]));
-                fs->traceMs += ta;
-                fs->shadeMs += tc;
-                fs->shadowMs += tb;
-                const size_t lvl = (e / 5) % static_cast<size_t>(r->nLevels);
-                fs->levelTraceMs[lvl] += ta;
-                fs->levelShadowMs[lvl] += tb;
-                if (!(r->walkSkipped && lvl + 1 == static_cast<size_t>(r->nLevels))) fs->traceLaunches += 1;
-                fs->shadowLaunches += 1;
-            }
+        const mrt_renderer::Pipe& pp = r->pipe;
+        for (size_t e = 0; e + 4 < pp.evCount; e += 5) {
+            float ta = 0.0F, tb = 0.0F, tc = 0.0F;
+            MRT_HIP(hipEventElapsedTime(&ta, pp.evPool[e], pp.evPool[e + 1]));
+            MRT_HIP(hipEventElapsedTime(&tc, pp.evPool[e + 1], pp.evPool[e + 2]));
+            MRT_HIP(hipEventElapsedTime(&tb, pp.evPool[e + 3], pp.evPool[e + 4]));
+            fs->traceMs += ta;
+            fs->shadeMs += tc;
+            fs->shadowMs += tb;
+            const size_t lvl = (e / 5) % static_cast<size_t>(r->nLevels);
+            fs->levelTraceMs[lvl] += ta;
+            fs->levelShadowMs[lvl] += tb;
+            const bool last = lvl + 1 == static_cast<size_t>(r->nLevels);
+            if (!(r->walkSkipped && last)) fs->traceLaunches += 1;
+            if (!last) fs->shadowLaunches += 1;  // the last level builds no shadow rays
         }
     }
     return true;
@@ -899,7 +683,7 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
     }
     uploadScene(r.get(), sc);
     buildUnits(r.get());
-    allocQueues(r.get(), chunkFor(r.get(), r->nPipes), 2);
+    allocQueues(r.get(), chunkFor(r.get()), 2);
     const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
     r->dBitmap = r->frameMem.alloc<int32_t>(npx);
     MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * npx, r->stream));
@@ -998,35 +782,20 @@ int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
 
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
     if (key == 1 && value >= 0 && value < mrt::kTraceVariants) {
-        r->ds.variant = (mrt::traceVariantCompressed(value) && r->ds.compOk == 0) ? mrt::kExactTraceVariant : value;
+        r->ds.variant = value;
         return 0;
     }
     if (key == 2 && (value == 0 || value == 1)) {
         r->ds.cull = value;
         return 0;
     }
-    if (key == 3 && value >= 0 && value <= 2) {
+    if (key == 3 && (value == 0 || value == 1)) {
         r->overlap = value;
-        return 0;
-    }
-    if (key == 4 && value >= 0 && value <= 3) {
-        r->sortRays = value;
-        return 0;
-    }
-    if (key == 6 && (value == 0 || value == 1)) {
-        r->streamMode = value;
         return 0;
     }
     if (key == 7 && (value == 0 || value == 1)) {
         r->skipLast = value;
         return 0;
-    }
-    if (key == 5 && value >= 1 && value <= 8) {
-        return guarded([&] {
-            MRT_HIP(hipDeviceSynchronize());
-            r->nPipes = value;
-            allocQueues(r, chunkFor(r, value), 2);
-        });
     }
     gLastError = "unknown tuning key/value";
     return -1;
@@ -1079,33 +848,12 @@ int64_t mrt_decode_texture(const char* path, int32_t* dims, uint8_t* texels) {
 }
 
 int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
-    if (key == 1) {
-        *value = r->ds.variant;
-        return 0;
-    }
-    if (key == 2) {
-        *value = r->ds.cull;
-        return 0;
-    }
-    if (key == 3) {
-        *value = r->overlap;
-        return 0;
-    }
-    if (key == 4) {
-        *value = r->sortRays;
-        return 0;
-    }
-    if (key == 5) {
-        *value = r->nPipes;
-        return 0;
-    }
-    if (key == 6) {
-        *value = r->streamMode;
-        return 0;
-    }
-    if (key == 7) {
-        *value = r->skipLast;
-        return 0;
+    switch (key) {
+        case 1: *value = r->ds.variant; return 0;
+        case 2: *value = r->ds.cull; return 0;
+        case 3: *value = r->overlap; return 0;
+        case 7: *value = r->skipLast; return 0;
+        default: break;
     }
     gLastError = "unknown tuning key";
     return -1;
@@ -1128,7 +876,7 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
         }
         const auto& units = r->unitsByRank[static_cast<size_t>(r->rankIndex)];
         const auto& prefix = r->prefixByRank[static_cast<size_t>(r->rankIndex)];
-        mrt_renderer::Pipe& pp = r->pipes[0];
+        mrt_renderer::Pipe& pp = r->pipe;
         const int cap = pp.levels[1].cap;
         int32_t* dk = static_cast<int32_t*>(nullptr);
         int32_t* di = nullptr;

@@ -872,7 +872,7 @@ template std::vector<HBVHNode> buildBVH<HSphere>(std::vector<HSphere>*, std::vec
 // so a parent and its left child usually share a 128-byte line.  Node numbering does not
 // affect results (boxes, child order and leaves are the reference's).
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
-                 int topCount, int* topPlaced, int layout) {
+                 int topCount, int* topPlaced) {
     out->clear();
     if (topPlaced != nullptr) *topPlaced = 0;
     const HBVHNode& r = nodes[0];
@@ -905,54 +905,18 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
         if (inner(l + 1)) bfs.push_back(l + 1);
     }
     if (topPlaced != nullptr) *topPlaced = static_cast<int>(order.size());
-    const size_t topEnd = order.size();
     auto place = [&](int32_t i) {
         newIdx[static_cast<size_t>(i)] = static_cast<int32_t>(order.size());
         order.push_back(i);
     };
     std::vector<int32_t> dfs{0};
-    if (layout == 2) {
-        // line pairs: a node at an even index and, right after it (same 128-byte line), its
-        // inner child with the larger box surface - the likelier next visit
-        auto area = [&](int32_t j) {
-            const v3 e = nodes[static_cast<size_t>(j)].box.mx - nodes[static_cast<size_t>(j)].box.mn;
-            return e.x * e.y + e.y * e.z + e.z * e.x;
-        };
-        while (!dfs.empty()) {
-            const int32_t i = dfs.back();
-            dfs.pop_back();
-            bool fresh = false;
-            if (newIdx[static_cast<size_t>(i)] < 0) {
-                if (order.size() % 2 != 0) order.push_back(-1);  // padding slot
-                place(i);
-                fresh = true;
-            }
-            const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
-            int32_t a = inner(l) ? l : -1, b = inner(l + 1) ? l + 1 : -1;
-            if (a >= 0 && b >= 0 && area(b) > area(a)) std::swap(a, b);
-            if (a < 0) std::swap(a, b);
-            if (fresh && a >= 0 && newIdx[static_cast<size_t>(a)] < 0) place(a);
-            if (b >= 0) dfs.push_back(b);
-            if (a >= 0) dfs.push_back(a);
-        }
-    } else {
-        while (!dfs.empty()) {
-            const int32_t i = dfs.back();
-            dfs.pop_back();
-            if (newIdx[static_cast<size_t>(i)] < 0) place(i);
-            const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
-            if (inner(l + 1)) dfs.push_back(l + 1);
-            if (inner(l)) dfs.push_back(l);
-        }
-        if (layout == 1) {  // diagnostic: the nodes below the top in a fixed random order
-            std::vector<int32_t> rest(order.begin() + static_cast<std::ptrdiff_t>(topEnd), order.end());
-            std::mt19937 rng(12345u);
-            std::shuffle(rest.begin(), rest.end(), rng);
-            for (size_t k = 0; k < rest.size(); ++k) {
-                order[topEnd + k] = rest[k];
-                newIdx[static_cast<size_t>(rest[k])] = static_cast<int32_t>(topEnd + k);
-            }
-        }
+    while (!dfs.empty()) {
+        const int32_t i = dfs.back();
+        dfs.pop_back();
+        if (newIdx[static_cast<size_t>(i)] < 0) place(i);
+        const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
+        if (inner(l + 1)) dfs.push_back(l + 1);
+        if (inner(l)) dfs.push_back(l);
     }
     auto ref = [&](int32_t j) {
         const HBVHNode& c = nodes[static_cast<size_t>(j)];
@@ -961,10 +925,6 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
     root->ref = 0;
     out->resize(order.size());
     for (size_t k = 0; k < order.size(); ++k) {
-        if (order[k] < 0) {  // padding
-            (*out)[k] = GNode{};
-            continue;
-        }
         const int32_t l = nodes[static_cast<size_t>(order[k])].indexOffset;
         const HBVHNode& L = nodes[static_cast<size_t>(l)];
         const HBVHNode& R = nodes[static_cast<size_t>(l + 1)];
@@ -985,181 +945,6 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
         g.refR = ref(l + 1);
         (*out)[k] = g;
     }
-}
-
-namespace {
-// One axis of a CNode: the smallest power-of-two step whose 8-bit grid holds the four bounds
-// (lo, hi, lo, hi) rounded outwards, checked with the kernel's own rounding.  Returns the
-// biased exponent (0: step 0, every bound equals the origin) or -1.
-int quantiseAxis(float origin, const float b[4], uint8_t u[4]) {
-    if (b[0] == origin && b[1] == origin && b[2] == origin && b[3] == origin) {
-        u[0] = u[1] = u[2] = u[3] = 0;
-        return 0;
-    }
-    auto deq = [origin](float step, long q) { return origin + step * static_cast<float>(q); };
-    const double ext = std::max(static_cast<double>(b[1]), static_cast<double>(b[3])) - static_cast<double>(origin);
-    int k = ext > 0.0 ? static_cast<int>(std::ceil(std::log2(ext / 255.0))) - 1 : -126;
-    for (k = std::max(k, -126); k <= 126; ++k) {
-        const float step = std::ldexp(1.0F, k);
-        bool ok = true;
-        for (int i = 0; i < 4 && ok; ++i) {
-            const bool lo = (i % 2) == 0;
-            const double r = (static_cast<double>(b[i]) - static_cast<double>(origin)) / static_cast<double>(step);
-            long q = lo ? static_cast<long>(std::floor(r)) : static_cast<long>(std::ceil(r));
-            q = std::min(255L, std::max(0L, q));
-            if (lo) {
-                while (q > 0 && deq(step, q) > b[i]) --q;
-                ok = deq(step, q) <= b[i];
-            } else {
-                while (q < 255 && deq(step, q) < b[i]) ++q;
-                ok = deq(step, q) >= b[i];
-            }
-            u[i] = static_cast<uint8_t>(q);
-        }
-        if (ok) return k + 127;
-    }
-    return -1;
-}
-
-int32_t collapse4(const std::vector<HBVHNode>& nodes, int32_t b2, std::vector<GNode4>* out) {
-    std::vector<int32_t> ch{nodes[static_cast<size_t>(b2)].indexOffset, nodes[static_cast<size_t>(b2)].indexOffset + 1};
-    while (ch.size() < 4) {
-        int best = -1;
-        float bestArea = -1.0F;
-        for (size_t k = 0; k < ch.size(); ++k) {
-            const HBVHNode& c = nodes[static_cast<size_t>(ch[k])];
-            if (c.numPrimitives > 0) continue;
-            const v3 l = c.box.mx - c.box.mn;
-            const float area = l.x * l.y + l.y * l.z + l.z * l.x;
-            if (area > bestArea) {
-                bestArea = area;
-                best = static_cast<int>(k);
-            }
-        }
-        if (best < 0) break;
-        const int32_t open = ch[static_cast<size_t>(best)];
-        const int32_t l = nodes[static_cast<size_t>(open)].indexOffset;
-        ch[static_cast<size_t>(best)] = l;
-        ch.insert(ch.begin() + best + 1, l + 1);
-    }
-    const int32_t me = static_cast<int32_t>(out->size());
-    out->push_back(GNode4{});
-    GNode4 g{};
-    for (int k = 0; k < 4; ++k) {
-        if (k >= static_cast<int>(ch.size())) {
-            g.minx[k] = g.miny[k] = g.minz[k] = 1.0F;
-            g.maxx[k] = g.maxy[k] = g.maxz[k] = -1.0F;
-            g.ref[k] = kRefEmpty;
-            continue;
-        }
-        const HBVHNode& c = nodes[static_cast<size_t>(ch[static_cast<size_t>(k)])];
-        g.minx[k] = c.box.mn.x;
-        g.miny[k] = c.box.mn.y;
-        g.minz[k] = c.box.mn.z;
-        g.maxx[k] = c.box.mx.x;
-        g.maxy[k] = c.box.mx.y;
-        g.maxz[k] = c.box.mx.z;
-        g.ref[k] = c.numPrimitives > 0 ? leafRef(c.indexOffset, c.numPrimitives)
-                                       : collapse4(nodes, ch[static_cast<size_t>(k)], out);
-    }
-    (*out)[static_cast<size_t>(me)] = g;
-    return me;
-}
-}  // namespace
-
-bool toDeviceCBVH(const std::vector<GNode>& g, int top, const GRoot& root, size_t numPrims, std::vector<CNode>* out,
-                  std::vector<float>* leafBoxes) {
-    out->assign(std::max<size_t>(g.size(), 1), CNode{});
-    leafBoxes->assign(std::max<size_t>(numPrims, 1) * 8, 0.0F);
-    auto putLeaf = [&](int32_t lref, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
-        const size_t f = static_cast<size_t>(leafFirst(lref));
-        if (f >= numPrims) return false;
-        float* b = leafBoxes->data() + 8 * f;
-        b[0] = mnx;
-        b[1] = mny;
-        b[2] = mnz;
-        b[3] = mxx;
-        b[4] = mxy;
-        b[5] = mxz;
-        return true;
-    };
-    if (numPrims == 0) return true;
-    if (root.ref < 0) return putLeaf(root.ref, root.bmin[0], root.bmin[1], root.bmin[2], root.bmax[0], root.bmax[1], root.bmax[2]);
-    for (size_t k = 0; k < g.size(); ++k) {
-        const GNode& n = g[k];
-        const bool lLeaf = n.refL < 0, rLeaf = n.refR < 0;
-        if (lLeaf && !putLeaf(n.refL, n.lminx, n.lminy, n.lminz, n.lmaxx, n.lmaxy, n.lmaxz)) return false;
-        if (rLeaf && !putLeaf(n.refR, n.rminx, n.rminy, n.rminz, n.rmaxx, n.rmaxy, n.rmaxz)) return false;
-        if (static_cast<int>(k) < top) continue;  // read from the exact LDS copy
-        const int32_t self = static_cast<int32_t>(k);
-        int32_t v;
-        if (!lLeaf && !rLeaf) {
-            if (n.refL != self + 1) return false;
-            v = n.refR;
-        } else if (!lLeaf) {
-            if (n.refL != self + 1) return false;
-            v = leafFirst(n.refR);
-        } else if (!rLeaf) {
-            if (n.refR != self + 1) return false;
-            v = leafFirst(n.refL);
-        } else {
-            if (leafFirst(n.refR) != leafFirst(n.refL) + leafCount(n.refL)) return false;
-            v = leafFirst(n.refL);
-        }
-        const int cL = lLeaf ? leafCount(n.refL) : 1, cR = rLeaf ? leafCount(n.refR) : 1;
-        if (cL < 1 || cL > 4 || cR < 1 || cR > 4) return false;
-        CNode c{};
-        c.ref = v;
-        c.expMeta = ((lLeaf ? 1u : 0u) | (rLeaf ? 2u : 0u) | (static_cast<uint32_t>(cL - 1) << 2) |
-                     (static_cast<uint32_t>(cR - 1) << 4))
-                    << 24;
-        const float lmn[3] = {n.lminx, n.lminy, n.lminz}, lmx[3] = {n.lmaxx, n.lmaxy, n.lmaxz};
-        const float rmn[3] = {n.rminx, n.rminy, n.rminz}, rmx[3] = {n.rmaxx, n.rmaxy, n.rmaxz};
-        float org[3];
-        uint8_t qb[12];
-        for (int a = 0; a < 3; ++a) {
-            org[a] = std::min(lmn[a], rmn[a]);
-            const float b[4] = {lmn[a], lmx[a], rmn[a], rmx[a]};
-            uint8_t u[4];
-            const int e = quantiseAxis(org[a], b, u);
-            if (e < 0) return false;
-            c.expMeta |= static_cast<uint32_t>(e) << (8 * a);
-            qb[a] = u[0];
-            qb[3 + a] = u[1];
-            qb[6 + a] = u[2];
-            qb[9 + a] = u[3];
-        }
-        c.ox = org[0];
-        c.oy = org[1];
-        c.oz = org[2];
-        for (int w = 0; w < 3; ++w)
-            c.q[w] = static_cast<uint32_t>(qb[4 * w]) | (static_cast<uint32_t>(qb[4 * w + 1]) << 8) |
-                     (static_cast<uint32_t>(qb[4 * w + 2]) << 16) | (static_cast<uint32_t>(qb[4 * w + 3]) << 24);
-        (*out)[k] = c;
-    }
-    return true;
-}
-
-void toDeviceBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode4>* out, GRoot* root) {
-    out->clear();
-    const HBVHNode& r = nodes[0];
-    root->bmin[0] = r.box.mn.x;
-    root->bmin[1] = r.box.mn.y;
-    root->bmin[2] = r.box.mn.z;
-    root->bmax[0] = r.box.mx.x;
-    root->bmax[1] = r.box.mx.y;
-    root->bmax[2] = r.box.mx.z;
-    root->count = static_cast<int32_t>(numPrims);
-    if (numPrims == 0) {
-        root->ref = 0;
-        return;
-    }
-    if (r.numPrimitives > 0) {
-        root->ref = leafRef(r.indexOffset, r.numPrimitives);
-        return;
-    }
-    out->reserve(nodes.size() / 2 + 1);
-    root->ref = collapse4(nodes, 0, out);
 }
 
 // ---- sample tables (Utils.cpp:43-53, Utils.hpp:209-218) ----------------------------------

@@ -133,16 +133,10 @@ bool aabbIntersect(const HAABB& b, v3 origin, v3 dir);  // AABB.cpp:34-54 (host 
 template <class T>
 std::vector<HBVHNode> buildBVH(std::vector<T>* prims, std::vector<int32_t>* order);
 
-// Converts reference nodes to the device child-box layout.
+// Converts reference nodes to the device child-box layout: the first topCount inner nodes
+// breadth-first (the trace kernel stages them in LDS), the rest depth-first pre-order.
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
-                 int topCount = 0, int* topPlaced = nullptr, int layout = 0);
-// Collapses the reference BVH2 into 4-wide nodes (greedy: open the largest-area inner child
-// until four children), depth-first order.  root->ref is BVH4 node 0 or a leaf ref.
-void toDeviceBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode4>* out, GRoot* root);
-// Compressed nodes (CNode) for g[top..) and the exact box of every leaf indexed by its first
-// primitive (8 floats each).  False if a node breaks the depth-first layout rules.
-bool toDeviceCBVH(const std::vector<GNode>& g, int top, const GRoot& root, size_t numPrims, std::vector<CNode>* out,
-                  std::vector<float>* leafBoxes);
+                 int topCount = 0, int* topPlaced = nullptr);
 
 // Utils.cpp:43-53 haltonSequence
 float haltonSequence(uint32_t index, uint32_t base);

@@ -276,16 +276,19 @@ def test_chunked_passes_and_cull_are_invariant():
     assert np.array_equal(a, b) and ra == rb
 
 
-def test_trace_kernel_variants_are_identical():
-    """Every trace-kernel organisation (per-wave batches / while-while + refill / 4-wide BVH)
-    returns the same hits, images and ray counts."""
+def test_trace_walks_are_identical():
+    """The per-wave reference walk (tuning key 1 = 0: 64-ray batches, plain DFS of
+    BVH.hpp:327-384) and the persistent while-while walk (1) return the same hits, images and
+    ray counts, with and without the conservative t-cull (key 2)."""
     import mobileraytracer_amd as m
     for cfg in (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
-                make_cfg(128, 128, shader=2, scene="water", spp=2), make_cfg(64, 64, shader=1)):
+                make_cfg(128, 128, shader=2, scene="water", spp=2), make_cfg(64, 64, shader=1),
+                make_cfg(128, 128, shader=1, sceneIndex=2)):
         outs = []
         with m.Renderer(cfg) as r:
-            for v in range(23):  # every kTraceCfg row
-                r.set_tuning(1, v)
+            for walk, cull in ((1, 1), (0, 1), (1, 0), (0, 0)):
+                r.set_tuning(1, walk)
+                r.set_tuning(2, cull)
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
                 r.render_frame(bm)
                 st = r.frame_stats()
@@ -295,43 +298,15 @@ def test_trace_kernel_variants_are_identical():
             assert all(np.array_equal(a, b) for a, b in zip(hits, outs[0][3]))
 
 
-def test_node_layouts_and_compressed_nodes_are_invariant(monkeypatch):
-    """Node numbering below the LDS top (depth-first, random, line pairs; MRT_NODE_LAYOUT) and
-    the compressed-node walk (variants 19-21, which need the depth-first numbering and fall back
-    to the exact walk otherwise) change nothing; assist variants report handed-over subtrees."""
-    import mobileraytracer_amd as m
-    cfg = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5)
-    outs = []
-    for layout in ("0", "1", "2"):
-        monkeypatch.setenv("MRT_NODE_LAYOUT", layout)
-        with m.Renderer(cfg) as r:
-            for v in (14, 19, 21):
-                r.set_tuning(1, v)
-                bm = np.zeros(cfg.width * cfg.height, np.int32)
-                r.render_frame(bm)
-                st = r.frame_stats()
-                outs.append((bm, st["rays"], st["shadowRays"]))
-                # compressed variants run only on the depth-first numbering
-                assert r.get_tuning(1) == (v if layout == "0" or v == 14 else 14)
-                if r.get_tuning(1) == 21:
-                    assert st["assistedSubtrees"] > 0 and st["maxRayMicros"] > 0
-    for bm, rays, shadows in outs[1:]:
-        assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
-
-
 def test_shadow_stream_overlap_is_invariant():
-    """Any-hit launches on their own stream (overlapping the next level), ray reordering before
-    traversal and concurrent chunk pipelines change nothing."""
+    """Any-hit launches on their own stream (overlapping the next level) change nothing."""
     import mobileraytracer_amd as m
     for cfg in (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
                 make_cfg(64, 64, shader=1)):
         outs = []
         with m.Renderer(cfg) as r:
-            for ov, srt, pipes in ((0, 0, 1), (1, 0, 1), (0, 3, 2), (1, 3, 3), (1, 1, 2), (1, 2, 1), (1, 0, 4),
-                                   (2, 0, 1), (2, 3, 2)):
+            for ov in (0, 1):
                 r.set_tuning(3, ov)
-                r.set_tuning(4, srt)  # ray reordering before traversal
-                r.set_tuning(5, pipes)  # concurrent chunk pipelines
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
                 r.render_frame(bm)
                 st = r.frame_stats()
@@ -344,7 +319,7 @@ def test_last_level_walk_skip_is_invariant():
     """The depth-capped last level shades to zero whatever its rays hit, so skipping its
     closest-hit walk (tuning key 7, default on) changes no pixel and no ray count; the walked-ray
     statistic drops by exactly that level's rays.  Textured scenes keep the walk (the texel write
-    before shade() returns is replayed), as does the combined launch (tuning key 3 = 2)."""
+    before shade() returns is replayed)."""
     import mobileraytracer_amd as m
     cases = ((make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5), True),
              (make_cfg(128, 128, shader=1, scene="water", max_depth=3), True),
@@ -354,7 +329,7 @@ def test_last_level_walk_skip_is_invariant():
         outs = []
         with m.Renderer(cfg) as r:
             assert r.get_tuning(7) == 1
-            for skip, overlap in ((1, 1), (0, 1), (1, 0), (1, 2)):
+            for skip, overlap in ((1, 1), (0, 1), (1, 0), (0, 0)):
                 r.set_tuning(7, skip)
                 r.set_tuning(3, overlap)
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
@@ -362,7 +337,7 @@ def test_last_level_walk_skip_is_invariant():
                 st = r.frame_stats()
                 outs.append((bm, st["rays"], st["shadowRays"]))
                 last = st["levelRays"][cfg.maxDepth]  # level maxDepth + 1
-                skipped = skips and skip == 1 and overlap != 2
+                skipped = skips and skip == 1
                 assert st["walkedRays"] == st["rays"] - (last if skipped else 0)
                 if skips:
                     assert last > 0

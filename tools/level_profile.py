@@ -16,8 +16,6 @@ def main():
     r = m.Renderer(cfg)
     if "VARIANT" in os.environ:
         r.set_tuning(1, int(os.environ["VARIANT"]))
-    if "SORT" in os.environ:
-        r.set_tuning(4, int(os.environ["SORT"]))
     d = torch.zeros(max(w * h, r.scene_info()["pixelSlotsMax"]), dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
     r.set_profiling(timing=True)

@@ -12,12 +12,8 @@ def frame_ms(n, w=1920, h=1080, spp=4, frames=10, rank=0):
     cfg = m.Config(width=w, height=h, shader=2, sceneIndex=-1, samplesPixel=spp, maxDepth=5, objFilePath=o,
                    mtlFilePath=l, camFilePath=c, rankIndex=rank, rankCount=n)
     with m.Renderer(cfg) as r:
-        if "PIPES" in os.environ:
-            r.set_tuning(5, int(os.environ["PIPES"]))
         if "OVERLAP" in os.environ:
             r.set_tuning(3, int(os.environ["OVERLAP"]))
-        if "STREAM" in os.environ:
-            r.set_tuning(6, int(os.environ["STREAM"]))
         if "VARIANT" in os.environ:
             r.set_tuning(1, int(os.environ["VARIANT"]))
         packed = torch.zeros(r.scene_info()["pixelSlotsMax"], dtype=torch.int32, device="cuda")
