@@ -56,7 +56,11 @@ typedef struct mrt_config {
     int32_t rankIndex;    /* screen-tile shard owned by this process */
     int32_t rankCount;    /* number of shards (GPUs); <= 0 -> 1 */
     int32_t device;       /* HIP device ordinal, -1 = current device */
-    int32_t cull;         /* 1 (default): near-first traversal + conservative t-culling */
+    int32_t cull;         /* near-first traversal with t-culling of the triangle BVH:
+                           * 0 none (the reference's visit set), 1 (default) fast: a box whose
+                           * entry exceeds best * (1 + 2^-10) is skipped, 2 certified: skipped
+                           * only on a rigorous bound of Moller-Trumbore's rounding (exact for
+                           * every input, slower).  See DESIGN.md section 3. */
     int32_t maxPathsPerPass; /* <= 0 -> automatic chunk size */
     int32_t progressive;  /* 1: one pass per sample; bitmap and mrt_get_sample() updated after
                            * each (Renderer.cpp:53-88).  0: all samples in flight at once.
@@ -119,7 +123,7 @@ int mrt_get_frame_stats(const mrt_renderer *r, mrt_frame_stats *stats);
 /* tuning knobs for A/B measurement (results are identical for every value):
  * key 1 = trace walk: 0 per-wave 64-ray batches with the plain DFS of BVH.hpp:327-384,
  *         1 persistent while-while walk (default),
- * key 2 = near-first traversal with conservative t-culling (1) or the reference visit set (0),
+ * key 2 = cull mode of walk 1: 0 none, 1 fast (default), 2 certified (mrt_config.cull),
  * key 3 = shadow rays on the same stream (0) or their own stream (1, default),
  * key 7 = skip the closest-hit walk of the depth-capped last level (1, default) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
@@ -138,6 +142,26 @@ int64_t mrt_triangle_bvh(const mrt_config *cfg, float *boxes, int32_t *offsets, 
  * width*height*channels (and fills dims[3] = width, height, channels) or -1; with non-NULL
  * texels copies the image, row-major, channels interleaved. */
 int64_t mrt_decode_texture(const char *path, int32_t *dims, uint8_t *texels);
+
+/* Host only: the renderer's sample tables (2^20 floats each; trig: 2^21, cos and sin of
+ * two_pi * shader[i] by the platform's libm, Shader.cpp:206-212).  NULL outputs are skipped. */
+int mrt_sample_tables(float *shader, float *sampler, float *trig);
+
+/* ---- test / diagnostic entry points (need a GPU; not on the render path) ----
+ * Device known-answer tests: the slab test the trace kernels inline (AABB.cpp:34-54) on n
+ * (box, ray) pairs: out[3i] = reference predicate, out[3i+1] = the IEEE min/max form used for
+ * waves whose 1/d is finite, out[3i+2] = whether 1/d is finite.  boxes: n x (min xyz, max xyz). */
+int mrt_kat_slab(const float *boxes, const float *orig, const float *dir, int32_t n, int32_t *out);
+/* Triangle::intersect (Triangle.cpp:63-109) as the kernels evaluate it: tris n x (A, B, C) xyz;
+ * hit[i] = 1 and t[i] on an accepted hit (eps <= t < RayLengthMax). */
+int mrt_kat_triangle(const float *tris, const float *orig, const float *dir, int32_t n, int32_t *hit, float *t);
+/* Arbitrary rays through the renderer's trace kernels (current walk and cull settings):
+ * any = 0: closest hit (Shader::rayTrace intersection part, Shader.cpp:86-111): kind / index
+ *          (input order, -1 on miss) / t per ray;
+ * any = 1: Shader::shadowTrace (Shader.cpp:132-158) with tmax dist[i]: kind[i] = occluded.
+ * src: NULL or n pairs (kind, input index) of the primitive each ray leaves (self-exclusion). */
+int mrt_trace_rays(mrt_renderer *r, const float *orig, const float *dir, const float *dist, const int32_t *src,
+                   int32_t n, int32_t any, int32_t *kind, int32_t *index, float *t);
 
 #ifdef __cplusplus
 }

@@ -142,6 +142,20 @@ class Renderer:
         _native.check(self._lib.mrt_primary_hits(self._h, _ptr(kind), _ptr(index), _ptr(t)))
         return kind, index, t
 
+    def trace_rays(self, orig, dirs, dist=None, src=None, any_hit=False):
+        """Arbitrary rays through the trace kernels (current walk / cull): closest hit
+        (kind, input index, t) per ray, or with any_hit the shadow test within dist
+        (kind = occluded).  src: None or (n, 2) int32 (kind, input index) source primitives."""
+        o = np.ascontiguousarray(orig, np.float32)
+        d = np.ascontiguousarray(dirs, np.float32)
+        n = len(o)
+        ds = np.ascontiguousarray(dist if dist is not None else np.zeros(n), np.float32)
+        sp = None if src is None else np.ascontiguousarray(src, np.int32)
+        k, i, t = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.float32)
+        _native.check(self._lib.mrt_trace_rays(self._h, _ptr(o), _ptr(d), _ptr(ds), None if sp is None else _ptr(sp),
+                                               n, int(any_hit), _ptr(k), _ptr(i), _ptr(t)))
+        return k, i, t
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._lib.mrt_destroy(self._h)
@@ -185,6 +199,34 @@ def decode_texture(path: str) -> np.ndarray:
     out = np.empty(int(n), np.uint8)
     lib.mrt_decode_texture(path.encode(), _ptr(dims), _ptr(out))
     return out.reshape(int(dims[1]), int(dims[0]), int(dims[2]))
+
+
+def sample_tables():
+    """Host only: (shader table, sampler table, trig (2^20 x cos, sin)) as the renderer builds them."""
+    a, b, t = np.empty(1 << 20, np.float32), np.empty(1 << 20, np.float32), np.empty(2 << 20, np.float32)
+    _native.check(_native.lib().mrt_sample_tables(_ptr(a), _ptr(b), _ptr(t)))
+    return a, b, t.reshape(-1, 2)
+
+
+def kat_slab(boxes, orig, dirs):
+    """The device slab test (AABB.cpp:34-54) on (box, ray) pairs: (reference predicate,
+    IEEE-min/max form, 1/d finite) per pair, int32 (n, 3)."""
+    b = np.ascontiguousarray(boxes, np.float32)
+    o = np.ascontiguousarray(orig, np.float32)
+    d = np.ascontiguousarray(dirs, np.float32)
+    out = np.empty((len(b), 3), np.int32)
+    _native.check(_native.lib().mrt_kat_slab(_ptr(b), _ptr(o), _ptr(d), len(b), _ptr(out)))
+    return out
+
+
+def kat_triangle(tris, orig, dirs):
+    """The device triangle test (Triangle.cpp:63-109) on (triangle A B C, ray) pairs: hit, t."""
+    tr = np.ascontiguousarray(tris, np.float32)
+    o = np.ascontiguousarray(orig, np.float32)
+    d = np.ascontiguousarray(dirs, np.float32)
+    hit, t = np.empty(len(tr), np.int32), np.empty(len(tr), np.float32)
+    _native.check(_native.lib().mrt_kat_triangle(_ptr(tr), _ptr(o), _ptr(d), len(tr), _ptr(hit), _ptr(t)))
+    return hit, t
 
 
 _active: List[Renderer] = []

@@ -158,9 +158,30 @@ struct alignas(16) GNode {
     float lminx, lminy, lminz, lmaxx;
     float lmaxy, lmaxz, rminx, rminy;
     float rminz, rmaxx, rmaxy, rmaxz;
-    int32_t refL, refR, pad0, pad1;
+    int32_t refL, refR;
+    uint32_t coneL, coneR;  // cull words of the children (kConeNever: never culled)
 };
 static_assert(sizeof(GNode) == 64, "GNode must be 64 bytes");
+
+// Cull word of a BVH2 child (GNode::coneL / coneR): what bounds the
+// Moller-Trumbore t of every triangle below the child.  bits 0-17: the normal-line axis a
+// (octahedral, 9 + 9 bits), bits 18-24: q = sin(psi) in 1/126 steps, rounded up, where every
+// triangle normal n satisfies |n.a| >= cos(psi) (127: no such bound), bits 25-31: K in
+// 2^(code/8) steps, rounded up, K >= |AB|_1 |AC|_1 / |AB x AC| of every triangle below (127: none).
+constexpr uint32_t kConeNever = 0xFFFFFFFFu;
+MRT_HD uint32_t coneQ(uint32_t w) { return (w >> 18) & 127u; }
+MRT_HD uint32_t coneK(uint32_t w) { return w >> 25; }
+MRT_HD v3 coneAxis(uint32_t w) {  // octahedral decode (not normalised: |a| in [1/sqrt(3), 1])
+    float x = static_cast<float>(w & 511u) * (2.0F / 511.0F) - 1.0F;
+    float y = static_cast<float>((w >> 9) & 511u) * (2.0F / 511.0F) - 1.0F;
+    const float z = 1.0F - fabsf(x) - fabsf(y);
+    if (z < 0.0F) {
+        const float ox = x;
+        x = (1.0F - fabsf(y)) * (ox >= 0.0F ? 1.0F : -1.0F);
+        y = (1.0F - fabsf(ox)) * (y >= 0.0F ? 1.0F : -1.0F);
+    }
+    return v3{x, y, z};
+}
 
 // root box + root reference of one BVH (the reference tests the root box first,
 // BVH.hpp:340-342)

@@ -7,8 +7,9 @@
 //     reference's "first visited wins on equal t" because its left-first DFS visits leaves in
 //     ascending BVH primitive index (BVH.hpp:252-268, 357-373) and kinds in the order
 //     planes, spheres, triangles, lights (Shader.cpp:104-111);
-//   * boxes are visited near-first and culled against the current best t with a relative
-//     margin (kCullMargin) that keeps every box that could hold an equal or rounding-adjacent t.
+//   * traverse<> visits exactly the reference's set of boxes (no t-culling): it serves the tiny
+//     plane / sphere BVHs and the per-wave reference walk; the persistent walk of
+//     mrt_trace_ww.hpp culls triangle boxes with a rigorous bound (cullKey).
 #pragma once
 
 #include "mrt_common.hpp"
@@ -17,7 +18,6 @@ namespace mrt {
 
 constexpr int kBlock = 256;         // threads per workgroup for every trace kernel
 constexpr int kLdsStackMin = 8;     // per-thread stack entries (8 bytes) in LDS; deeper ones spill
-constexpr float kCullMargin = 0x1p-10f;
 
 struct DScene {
     const float4* triGeom;     // 3 per triangle (BVH order): A, AB, AC  (xyz)
@@ -31,10 +31,11 @@ struct DScene {
     const float4* mats;        // 4 per material: Le (w = ior), Kd, Ks, Kt
     const float2* tables;  // 2^20 x {shader (Shader.cpp:23), sampler (StaticHaltonSeq.cpp)}
                            // shuffled Halton values
+    const float2* trig;    // 2^20 x {cos, sin} of 2 pi * shader entry (libm, fillHemisphereTrig)
     GRoot triRoot, planeRoot, sphereRoot;
     int32_t nLights;
     int32_t nMats;
-    int32_t cull;              // 1: near-first + conservative t-culling, 0: reference visit set
+    int32_t cull;              // walk 1's cull mode: 0 none, 1 fast, 2 certified (mrt_trace_ww.hpp)
     int32_t variant;           // trace walk: 0 per-wave reference walk, 1 persistent while-while
     int32_t triTop;            // triNodes[0, triTop) are the breadth-first top of the tree
     int32_t matsFinite;        // every material's Kd / Ks / Kt component is finite
@@ -89,6 +90,25 @@ __device__ __forceinline__ bool slabFinite(float mnx, float mny, float mnz, floa
     const float t1z = (mnz - o.z) * inv.z;
     const float t2z = (mxz - o.z) * inv.z;
     const float e = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fmaxf(fminf(t1z, t2z), 0.0F));
+    const float tMax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+    *tEntry = e;
+    return tMax >= e;
+}
+
+// slabFinite that also returns each axis's entry t (min of the two plane crossings): the
+// cull key inflates the box per axis (mrt_trace_ww.hpp cullKey).
+__device__ __forceinline__ bool slabFiniteAxes(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, v3 o,
+                                               v3 inv, float* tEntry, float* ex, float* ey, float* ez) {
+    const float t1x = (mnx - o.x) * inv.x;
+    const float t2x = (mxx - o.x) * inv.x;
+    const float t1y = (mny - o.y) * inv.y;
+    const float t2y = (mxy - o.y) * inv.y;
+    const float t1z = (mnz - o.z) * inv.z;
+    const float t2z = (mxz - o.z) * inv.z;
+    *ex = fminf(t1x, t2x);
+    *ey = fminf(t1y, t2y);
+    *ez = fminf(t1z, t2z);
+    const float e = fmaxf(fmaxf(*ex, *ey), fmaxf(*ez, 0.0F));
     const float tMax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
     *tEntry = e;
     return tMax >= e;
@@ -277,23 +297,11 @@ __device__ __forceinline__ bool traverse(const DScene& s, const GNode* nodes, co
             const int4 n3 = reinterpret_cast<const int4*>(np)[3];
             cnt->nodes += 2;
             float tl, tr;
-            bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
-            bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
-            if (s.cull) {
-                const float lim = b->t + b->t * kCullMargin;
-                hl = hl && !(tl > lim);
-                hr = hr && !(tr > lim);
-            }
-            if (hl && hr) {
-                int nearRef = n3.x, farRef = n3.y;
-                float farT = tr;
-                if (s.cull && tr < tl) {
-                    nearRef = n3.y;
-                    farRef = n3.x;
-                    farT = tl;
-                }
-                st.push(farRef, farT);
-                ref = nearRef;
+            const bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
+            const bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+            if (hl && hr) {  // BVH.hpp:357-373: left first, right pushed
+                st.push(n3.y, tr);
+                ref = n3.x;
                 continue;
             }
             if (hl) {
@@ -315,16 +323,8 @@ __device__ __forceinline__ bool traverse(const DScene& s, const GNode* nodes, co
                 return true;
             }
         }
-        // pop (skipping entries the current best has culled)
-        while (true) {
-            if (st.sp == base) return false;
-            const int2 e = st.pop();
-            const float et = __int_as_float(e.y);
-            if (!s.cull || !(et > b->t + b->t * kCullMargin)) {
-                ref = e.x;
-                break;
-            }
-        }
+        if (st.sp == base) return false;
+        ref = st.pop().x;
     }
 }
 

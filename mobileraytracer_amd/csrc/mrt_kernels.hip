@@ -169,7 +169,7 @@ __device__ __forceinline__ void reduceCounts(const TravCount& cnt, unsigned long
     }
 }
 
-template <bool kCount, int kVariant>
+template <bool kCount, int kVariant, int kCull>
 __global__ __launch_bounds__(kWalkThreads, 1) void k_trace(DScene s, Level lv, int* counters, int level,
                                                             int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kWalkThreads, 1) void k_trace(DScene s, Level lv, i
     if (kVariant == 1) {
         __shared__ GNode ldsTop[kWalkTop];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<false, kCount>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop);
+        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kWalkThreads, 1) void k_trace(DScene s, Level lv, i
     }
 }
 
-template <bool kCount, int kVariant>
+template <bool kCount, int kVariant, int kCull>
 __global__ __launch_bounds__(kWalkThreads, 1) void k_shadow(DScene s, Level lv, int* counters, int level,
                                                              int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kWalkThreads, 1) void k_shadow(DScene s, Level lv, 
     if (kVariant == 1) {
         __shared__ GNode ldsTop[kWalkTop];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<true, kCount>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop);
+        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -336,16 +336,14 @@ __device__ __forceinline__ float4 textureWrite(const DScene& s, float4 h) {
     return make_float4(c.x, c.y, c.z, static_cast<float>(mat));
 }
 
-// Shader::getCosineSampleHemisphere (Shader.cpp:188-216); cos/sin evaluated in double and
-// rounded, which agrees with glibc cosf/sinf except in rare last-ulp cases.
-__device__ __forceinline__ v3 cosineHemisphere(v3 n, float r1, float r2) {
-    const float phi = kTwoPi * r1;
+// Shader::getCosineSampleHemisphere (Shader.cpp:188-216).  cos(phi), sin(phi) with
+// phi = 2 pi r1 come from the per-entry table of the platform's cosf / sinf (DScene::trig), so
+// the bounce direction has the reference's bits.
+__device__ __forceinline__ v3 cosineHemisphere(v3 n, float cphi, float sphi, float r2) {
     const float cosTheta = sqrtf(r2);
     v3 u = fabsf(n.x) > 0.1F ? v3{0.0F, 1.0F, 0.0F} : v3{1.0F, 0.0F, 0.0F};
     u = normalize(cross(u, n));
     const v3 v = cross(n, u);
-    const float cphi = static_cast<float>(cos(static_cast<double>(phi)));
-    const float sphi = static_cast<float>(sin(static_cast<double>(phi)));
     const v3 dir = (u * (cphi * cosTheta) + v * (sphi * cosTheta)) + n * sqrtf(1.0F - r2);
     return normalize(dir);
 }
@@ -391,7 +389,7 @@ struct ShadeState {
     bool terminal, direct, wantD, wantS, wantT, ok0;
     float4 leaf;  // terminal: the vertex's final radiance (Le), w = hit-a-light flag
     v3 ld0, lc0;  // light sample 0 (kept in registers)
-    float dist0, hemi1, hemi2;
+    float dist0, hcos, hsin, hemi2;
     int nShadow, nChild;
 };
 
@@ -414,7 +412,9 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     const float lr0 = s.tables[sampleIndex(v.key, tc, purposeLightR(0))].y;
     const float lq0 = s.tables[sampleIndex(v.key, tc, purposeLightS(0))].y;
     const float rr = s.tables[sampleIndex(v.key, tc, kPRussian)].y;
-    v.hemi1 = s.tables[sampleIndex(v.key, tc, kPHemi1)].x;
+    const float2 hemi1 = s.trig[sampleIndex(v.key, tc, kPHemi1)];  // cos, sin of 2 pi r1
+    v.hcos = hemi1.x;
+    v.hsin = hemi1.y;
     v.hemi2 = s.tables[sampleIndex(v.key, tc, kPHemi2)].x;
     const uint32_t code = fbits(h.w);
     const uint32_t kind = primKind(code);
@@ -512,7 +512,7 @@ __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, 
             nx.rD[j] = make_float4(dir.x, dir.y, dir.z, bitsf(v.g.src));
             nx.tree[j] = v.tc * 4u + slot;
         };
-        if (v.wantD) emit(cosineHemisphere(v.g.N, v.hemi1, v.hemi2), 1u);
+        if (v.wantD) emit(cosineHemisphere(v.g.N, v.hcos, v.hsin, v.hemi2), 1u);
         if (v.wantS) emit(reflect(v.d, v.g.N), 2u);
         if (v.wantT) emit(refract(v.d, v.g.N, 1.0F / v.ior), 3u);
     }
@@ -764,6 +764,72 @@ __global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats, 
 }
 
 // ---------------------------------------------------------------------------------------
+// Device known-answer kernels: the SAME slab() / slabFinite() / triTest() the walks inline, on
+// the reference's unit-test vectors (TestAABB.cpp:111-130, TestTriangle.cpp:347-433).
+__global__ __launch_bounds__(64) void k_kat_slab(const float* boxes, const float* orig, const float* dir, int n,
+                                                 int32_t* out) {
+    const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const float* b = boxes + 6 * i;
+    const v3 o{orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]};
+    const v3 d{dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]};
+    const v3 inv{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
+    float te;
+    out[3 * i] = slab(b[0], b[1], b[2], b[3], b[4], b[5], o, inv, &te) ? 1 : 0;
+    out[3 * i + 1] = slabFinite(b[0], b[1], b[2], b[3], b[4], b[5], o, inv, &te) ? 1 : 0;
+    out[3 * i + 2] = finiteInv(inv) ? 1 : 0;  // slabFinite is used only for these rays
+}
+
+__global__ __launch_bounds__(64) void k_kat_triangle(const float* tris, const float* orig, const float* dir, int n,
+                                                     int32_t* hit, float* tOut) {
+    const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const float* p = tris + 9 * i;  // A, B, C (Triangle.cpp:14-26: AB = B - A, AC = C - A)
+    const float4 a4 = make_float4(p[0], p[1], p[2], 0.0F);
+    const float4 ab4 = make_float4(p[3] - p[0], p[4] - p[1], p[5] - p[2], 0.0F);
+    const float4 ac4 = make_float4(p[6] - p[0], p[7] - p[1], p[8] - p[2], 0.0F);
+    const v3 o{orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]};
+    const v3 d{dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]};
+    float t = 0.0F, u, v;
+    const bool h = triTest(a4, ab4, ac4, o, d, &t, &u, &v) && !(t < kEpsilon) && t < kRayLengthMax;
+    hit[i] = h ? 1 : 0;
+    tOut[i] = h ? t : 0.0F;
+}
+
+void launchKatSlab(const float* boxes, const float* orig, const float* dir, int n, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_kat_slab, dim3((n + 63) / 64), dim3(64), 0, st, boxes, orig, dir, n, out);
+}
+
+void launchKatTriangle(const float* tris, const float* orig, const float* dir, int n, int32_t* hit, float* t,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_kat_triangle, dim3((n + 63) / 64), dim3(64), 0, st, tris, orig, dir, n, hit, t);
+}
+
+// arbitrary rays into a level's queue (mrt_trace_rays): rO / rD or sO / sD / sC
+__global__ __launch_bounds__(256) void k_load_rays(Level lv, const float* orig, const float* dir, const float* dist,
+                                                   const uint32_t* src, int n, int any, int* counters) {
+    const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i == 0) counters[any ? cntShadows(1) : cntRays(1)] = n;
+    if (i >= n) return;
+    const uint32_t code = src != nullptr ? src[i] : kNoPrim;
+    if (any) {
+        lv.sO[i] = make_float4(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2], bitsf(code));
+        lv.sD[i] = make_float4(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2], dist[i]);
+        lv.sC[i] = make_float4(0.0F, 0.0F, 0.0F, -1.0F);
+    } else {
+        lv.rO[i] = make_float4(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2], 0.0F);
+        lv.rD[i] = make_float4(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2], bitsf(code));
+        lv.tree[i] = 1u;
+    }
+}
+
+void launchLoadRays(const Level& lv, const float* orig, const float* dir, const float* dist, const uint32_t* src, int n,
+                    bool any, int* counters, hipStream_t st) {
+    hipLaunchKernelGGL(k_load_rays, dim3(std::max(1, (n + 255) / 256)), dim3(256), 0, st, lv, orig, dir, dist, src, n,
+                       any ? 1 : 0, counters);
+}
+
+// ---------------------------------------------------------------------------------------
 // launch wrappers
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st) {
     const int blocks = (a.nPaths + 255) / 256;
@@ -774,7 +840,7 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
 // spill stacks were sized for.
 template <typename K>
 int persistentGrid(K kernel, int slot, int maxThreads) {
-    static int occ[8] = {};
+    static int occ[16] = {};
     static int cus = 0;
     const int cap = std::max(1, maxThreads / kWalkThreads);
     if (cus == 0) {
@@ -788,21 +854,21 @@ int persistentGrid(K kernel, int slot, int maxThreads) {
     return o > 0 ? std::min(cap, o * cus) : cap;
 }
 
+// variant 0 (reference walk, never culls) and variant 1 in each cull mode; slot: occupancy cache
+#define MRT_LAUNCH_ONE(KERNEL, V, C, SLOT)                                                                      \
+    do {                                                                                                       \
+        const int g = persistentGrid(KERNEL<false, V, C>, SLOT, maxThreads);                                   \
+        if (countStats)                                                                                        \
+            hipLaunchKernelGGL((KERNEL<true, V, C>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+        else                                                                                                   \
+            hipLaunchKernelGGL((KERNEL<false, V, C>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
+    } while (0)
 #define MRT_LAUNCH_WALK(KERNEL, SLOT)                                                                           \
     do {                                                                                                       \
-        if (s.variant == 0) {                                                                                  \
-            const int g = persistentGrid(KERNEL<false, 0>, SLOT, maxThreads);                                  \
-            if (countStats)                                                                                    \
-                hipLaunchKernelGGL((KERNEL<true, 0>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-            else                                                                                               \
-                hipLaunchKernelGGL((KERNEL<false, 0>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-        } else {                                                                                               \
-            const int g = persistentGrid(KERNEL<false, 1>, SLOT + 1, maxThreads);                              \
-            if (countStats)                                                                                    \
-                hipLaunchKernelGGL((KERNEL<true, 1>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-            else                                                                                               \
-                hipLaunchKernelGGL((KERNEL<false, 1>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
-        }                                                                                                      \
+        if (s.variant == 0) MRT_LAUNCH_ONE(KERNEL, 0, kCullNone, SLOT);                                        \
+        else if (s.cull == kCullFast) MRT_LAUNCH_ONE(KERNEL, 1, kCullFast, SLOT + 1);                          \
+        else if (s.cull == kCullCertified) MRT_LAUNCH_ONE(KERNEL, 1, kCullCertified, SLOT + 2);                \
+        else MRT_LAUNCH_ONE(KERNEL, 1, kCullNone, SLOT + 3);                                                   \
     } while (0)
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
@@ -820,7 +886,7 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
         hipLaunchKernelGGL((k_trace_other<true>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }
-    MRT_LAUNCH_WALK(k_shadow, 2);
+    MRT_LAUNCH_WALK(k_shadow, 4);
 }
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
@@ -884,8 +950,14 @@ void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStre
 int traceResidentThreadsPerCU() {
     // the spill stacks are sized for the walk with the most resident threads
     int best = kWalkThreads;
-    const void* kernels[] = {reinterpret_cast<const void*>(k_trace<false, 0>), reinterpret_cast<const void*>(k_trace<false, 1>),
-                             reinterpret_cast<const void*>(k_shadow<false, 0>), reinterpret_cast<const void*>(k_shadow<false, 1>)};
+    const void* kernels[] = {reinterpret_cast<const void*>(k_trace<false, 0, kCullNone>),
+                             reinterpret_cast<const void*>(k_trace<false, 1, kCullFast>),
+                             reinterpret_cast<const void*>(k_trace<false, 1, kCullCertified>),
+                             reinterpret_cast<const void*>(k_trace<false, 1, kCullNone>),
+                             reinterpret_cast<const void*>(k_shadow<false, 0, kCullNone>),
+                             reinterpret_cast<const void*>(k_shadow<false, 1, kCullFast>),
+                             reinterpret_cast<const void*>(k_shadow<false, 1, kCullCertified>),
+                             reinterpret_cast<const void*>(k_shadow<false, 1, kCullNone>)};
     for (const void* k : kernels) {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWalkThreads, 0) == hipSuccess)

@@ -119,6 +119,12 @@ void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, in
 void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st);
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);
 void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel = 0);
+// known-answer kernels (device slab / triangle tests) and arbitrary-ray loading for tests
+void launchKatSlab(const float* boxes, const float* orig, const float* dir, int n, int32_t* out, hipStream_t st);
+void launchKatTriangle(const float* tris, const float* orig, const float* dir, int n, int32_t* hit, float* t,
+                       hipStream_t st);
+void launchLoadRays(const Level& lv, const float* orig, const float* dir, const float* dist, const uint32_t* src, int n,
+                    bool any, int* counters, hipStream_t st);
 int traceResidentThreadsPerCU();  // max over the trace walks of resident threads per CU
 
 }  // namespace mrt

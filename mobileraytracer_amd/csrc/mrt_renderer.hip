@@ -230,7 +230,8 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
 
     std::vector<GNode> g;
     DScene& d = r->ds;
-    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop);
+    const std::vector<uint32_t> cones = triangleConeWords(tn, sc.triangles);
+    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop, &cones);
     d.triNodes = r->sceneMem.upload(g, st);
     toDeviceBVH(pn, sc.planes.size(), &g, &d.planeRoot);
     d.planeNodes = r->sceneMem.upload(g, st);
@@ -342,6 +343,9 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
         both[2 * k + 1] = samplerT[k];
     }
     d.tables = reinterpret_cast<const float2*>(r->sceneMem.upload(both, st));
+    std::vector<float> trig;
+    fillHemisphereTrig(shaderT, &trig);
+    d.trig = reinterpret_cast<const float2*>(r->sceneMem.upload(trig, st));
     MRT_HIP(hipStreamSynchronize(st));
 }
 
@@ -785,7 +789,7 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.variant = value;
         return 0;
     }
-    if (key == 2 && (value == 0 || value == 1)) {
+    if (key == 2 && value >= 0 && value <= 2) {
         r->ds.cull = value;
         return 0;
     }
@@ -845,6 +849,18 @@ int64_t mrt_decode_texture(const char* path, int32_t* dims, uint8_t* texels) {
         if (texels != nullptr) std::memcpy(texels, t.texels.data(), t.texels.size());
     });
     return rc == 0 ? n : -1;
+}
+
+int mrt_sample_tables(float* shader, float* sampler, float* trig) {
+    return guarded([&] {
+        std::vector<float> a, b, t;
+        mrt::fillHaltonTable(&a, mrt::kSeedShaderTable);
+        mrt::fillHaltonTable(&b, mrt::kSeedSamplerTable);
+        mrt::fillHemisphereTrig(a, &t);
+        if (shader != nullptr) std::memcpy(shader, a.data(), a.size() * sizeof(float));
+        if (sampler != nullptr) std::memcpy(sampler, b.data(), b.size() * sizeof(float));
+        if (trig != nullptr) std::memcpy(trig, t.data(), t.size() * sizeof(float));
+    });
 }
 
 int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
@@ -930,6 +946,120 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
         (void)hipFree(dk);
         (void)hipFree(di);
         (void)hipFree(dt);
+    });
+}
+
+}  // extern "C"
+
+// ---- test and diagnostic entry points ---------------------------------------------------
+namespace {
+// scoped device buffer for the diagnostic entry points (not on the render path)
+struct DevBuf {
+    void* p = nullptr;
+    explicit DevBuf(size_t bytes) { MRT_HIP(hipMalloc(&p, bytes == 0 ? 1 : bytes)); }
+    ~DevBuf() { (void)hipFree(p); }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+}  // namespace
+
+extern "C" {
+
+int mrt_kat_slab(const float* boxes, const float* orig, const float* dir, int32_t n, int32_t* out) {
+    return guarded([&] {
+        if (n <= 0) return;
+        const size_t N = static_cast<size_t>(n);
+        DevBuf b(N * 24), o(N * 12), d(N * 12), r(N * 12);
+        MRT_HIP(hipMemcpy(b.p, boxes, N * 24, hipMemcpyHostToDevice));
+        MRT_HIP(hipMemcpy(o.p, orig, N * 12, hipMemcpyHostToDevice));
+        MRT_HIP(hipMemcpy(d.p, dir, N * 12, hipMemcpyHostToDevice));
+        mrt::launchKatSlab(b.as<float>(), o.as<float>(), d.as<float>(), n, r.as<int32_t>(), nullptr);
+        MRT_HIP(hipMemcpy(out, r.p, N * 12, hipMemcpyDeviceToHost));
+    });
+}
+
+int mrt_kat_triangle(const float* tris, const float* orig, const float* dir, int32_t n, int32_t* hit, float* t) {
+    return guarded([&] {
+        if (n <= 0) return;
+        const size_t N = static_cast<size_t>(n);
+        DevBuf b(N * 36), o(N * 12), d(N * 12), h(N * 4), tt(N * 4);
+        MRT_HIP(hipMemcpy(b.p, tris, N * 36, hipMemcpyHostToDevice));
+        MRT_HIP(hipMemcpy(o.p, orig, N * 12, hipMemcpyHostToDevice));
+        MRT_HIP(hipMemcpy(d.p, dir, N * 12, hipMemcpyHostToDevice));
+        mrt::launchKatTriangle(b.as<float>(), o.as<float>(), d.as<float>(), n, h.as<int32_t>(), tt.as<float>(), nullptr);
+        MRT_HIP(hipMemcpy(hit, h.p, N * 4, hipMemcpyDeviceToHost));
+        MRT_HIP(hipMemcpy(t, tt.p, N * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+int mrt_trace_rays(mrt_renderer* r, const float* orig, const float* dir, const float* dist, const int32_t* src,
+                   int32_t n, int32_t any, int32_t* kind, int32_t* index, float* t) {
+    return guarded([&] {
+        using namespace mrt;
+        if (n <= 0) return;
+        hipStream_t st = r->stream;
+        mrt_renderer::Pipe& pp = r->pipe;
+        Level& lv = pp.levels[1];
+        const int cap = any ? lv.shadowCap : lv.cap;
+        // input-order primitive -> BVH-order code (self-exclusion source), and back for the output
+        auto inverse = [](const std::vector<int32_t>& order) {
+            std::vector<int32_t> inv(order.size());
+            for (size_t j = 0; j < order.size(); ++j) inv[static_cast<size_t>(order[j])] = static_cast<int32_t>(j);
+            return inv;
+        };
+        const std::vector<int32_t> triInv = inverse(r->triOrder), planeInv = inverse(r->planeOrder),
+                                   sphereInv = inverse(r->sphereOrder);
+        std::vector<uint32_t> codes(static_cast<size_t>(n), kNoPrim);
+        if (src != nullptr) {
+            for (int32_t i = 0; i < n; ++i) {
+                const int32_t k = src[2 * i], j = src[2 * i + 1];
+                if (k == kTriangle) codes[i] = encodePrim(kTriangle, static_cast<uint32_t>(triInv.at(static_cast<size_t>(j))));
+                if (k == kPlane) codes[i] = encodePrim(kPlane, static_cast<uint32_t>(planeInv.at(static_cast<size_t>(j))));
+                if (k == kSphere) codes[i] = encodePrim(kSphere, static_cast<uint32_t>(sphereInv.at(static_cast<size_t>(j))));
+                if (k == kLight) codes[i] = encodePrim(kLight, static_cast<uint32_t>(j));
+            }
+        }
+        const size_t C = static_cast<size_t>(std::min(cap, n));
+        DevBuf o(C * 12), d(C * 12), ds(C * 4), sc(C * 4);
+        std::vector<float4> out(C);
+        for (int32_t base = 0; base < n; base += static_cast<int32_t>(C)) {
+            const int m = std::min(static_cast<int>(C), n - base);
+            const size_t M = static_cast<size_t>(m);
+            MRT_HIP(hipMemcpyAsync(o.p, orig + 3 * static_cast<size_t>(base), M * 12, hipMemcpyHostToDevice, st));
+            MRT_HIP(hipMemcpyAsync(d.p, dir + 3 * static_cast<size_t>(base), M * 12, hipMemcpyHostToDevice, st));
+            if (any) MRT_HIP(hipMemcpyAsync(ds.p, dist + base, M * 4, hipMemcpyHostToDevice, st));
+            MRT_HIP(hipMemcpyAsync(sc.p, codes.data() + base, M * 4, hipMemcpyHostToDevice, st));
+            MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
+            launchLoadRays(lv, o.as<float>(), d.as<float>(), ds.as<float>(), sc.as<uint32_t>(), m, any != 0, pp.counters, st);
+            if (any) {
+                launchShadow(r->ds, lv, pp.counters, 1, pp.gstackShadow, r->gdepth, pp.stats, false, r->traceThreads, st);
+                MRT_HIP(hipMemcpyAsync(out.data(), lv.sC, M * 16, hipMemcpyDeviceToHost, st));
+            } else {
+                launchTrace(r->ds, lv, pp.counters, 1, pp.gstack, r->gdepth, pp.stats, false, r->traceThreads, st);
+                MRT_HIP(hipMemcpyAsync(out.data(), lv.hit, M * 16, hipMemcpyDeviceToHost, st));
+            }
+            MRT_HIP(hipStreamSynchronize(st));
+            for (int q = 0; q < m; ++q) {
+                const size_t i = static_cast<size_t>(base + q);
+                const float4 h = out[static_cast<size_t>(q)];
+                if (any) {
+                    kind[i] = h.w != 0.0F ? 1 : 0;
+                    index[i] = -1;
+                    t[i] = 0.0F;
+                    continue;
+                }
+                uint32_t code;
+                std::memcpy(&code, &h.w, 4);
+                int32_t k = static_cast<int32_t>(primKind(code)), idx = static_cast<int32_t>(primIndex(code));
+                if (k == kTriangle) idx = r->triOrder[static_cast<size_t>(idx)];
+                if (k == kPlane) idx = r->planeOrder[static_cast<size_t>(idx)];
+                if (k == kSphere) idx = r->sphereOrder[static_cast<size_t>(idx)];
+                if (k == kMiss) idx = -1;
+                kind[i] = k;
+                index[i] = idx;
+                t[i] = h.x;
+            }
+        }
     });
 }
 

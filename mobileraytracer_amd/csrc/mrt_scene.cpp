@@ -2,6 +2,7 @@
 #include "mrt_scene.hpp"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -872,7 +873,7 @@ template std::vector<HBVHNode> buildBVH<HSphere>(std::vector<HSphere>*, std::vec
 // so a parent and its left child usually share a 128-byte line.  Node numbering does not
 // affect results (boxes, child order and leaves are the reference's).
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
-                 int topCount, int* topPlaced) {
+                 int topCount, int* topPlaced, const std::vector<uint32_t>* cones) {
     out->clear();
     if (topPlaced != nullptr) *topPlaced = 0;
     const HBVHNode& r = nodes[0];
@@ -943,8 +944,116 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
         g.rmaxz = R.box.mx.z;
         g.refL = ref(l);
         g.refR = ref(l + 1);
+        g.coneL = cones != nullptr ? (*cones)[static_cast<size_t>(l)] : kConeNever;
+        g.coneR = cones != nullptr ? (*cones)[static_cast<size_t>(l + 1)] : kConeNever;
         (*out)[k] = g;
     }
+}
+
+namespace {
+// one node's cull word from its triangles [lo, hi) (BVH order)
+uint32_t coneWord(const std::vector<HTriangle>& tris, size_t lo, size_t hi) {
+    // K: conditioning of Moller-Trumbore's determinant (Triangle.cpp:67-70) for every triangle
+    double kMax = 1.0;
+    double m[3][3] = {};  // sum of n n^T over unit normals (sign-free: lines, not directions)
+    std::vector<std::array<double, 3>> ns;
+    ns.reserve(hi - lo);
+    for (size_t i = lo; i < hi; ++i) {
+        const HTriangle& t = tris[i];
+        const double ab[3] = {t.AB.x, t.AB.y, t.AB.z}, ac[3] = {t.AC.x, t.AC.y, t.AC.z};
+        const double n[3] = {ab[1] * ac[2] - ab[2] * ac[1], ab[2] * ac[0] - ab[0] * ac[2], ab[0] * ac[1] - ab[1] * ac[0]};
+        const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        const double l1 = (std::fabs(ab[0]) + std::fabs(ab[1]) + std::fabs(ab[2])) *
+                          (std::fabs(ac[0]) + std::fabs(ac[1]) + std::fabs(ac[2]));
+        if (!(len > 0.0) || !std::isfinite(l1)) return kConeNever;  // degenerate: no bound
+        kMax = std::max(kMax, l1 / len);
+        const std::array<double, 3> u{n[0] / len, n[1] / len, n[2] / len};
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) m[r][c] += u[static_cast<size_t>(r)] * u[static_cast<size_t>(c)];
+        ns.push_back(u);
+    }
+    const double kCode = std::ceil(8.0 * std::log2(kMax) + 1e-9);
+    if (ns.empty() || kCode > 126.0) return kConeNever;
+    // axis: dominant eigenvector of sum n n^T (power iteration from the largest column)
+    int col = 0;
+    for (int c = 1; c < 3; ++c)
+        if (m[c][c] > m[col][col]) col = c;
+    double a[3] = {m[0][col], m[1][col], m[2][col]};
+    for (int it = 0; it < 64; ++it) {
+        double b[3];
+        for (int r = 0; r < 3; ++r) b[r] = m[r][0] * a[0] + m[r][1] * a[1] + m[r][2] * a[2];
+        const double l = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
+        if (!(l > 0.0)) return kConeNever;
+        for (int r = 0; r < 3; ++r) a[r] = b[r] / l;
+    }
+    // octahedral encoding of a, then the cone around the DECODED axis (as the kernel sees it)
+    const double s1 = std::fabs(a[0]) + std::fabs(a[1]) + std::fabs(a[2]);
+    double ox = a[0] / s1, oy = a[1] / s1;
+    if (a[2] < 0.0) {
+        const double tx = ox;
+        ox = (1.0 - std::fabs(oy)) * (tx >= 0.0 ? 1.0 : -1.0);
+        oy = (1.0 - std::fabs(tx)) * (oy >= 0.0 ? 1.0 : -1.0);
+    }
+    const uint32_t qx = static_cast<uint32_t>(std::lround((ox + 1.0) * 0.5 * 511.0));
+    const uint32_t qy = static_cast<uint32_t>(std::lround((oy + 1.0) * 0.5 * 511.0));
+    const v3 dec = coneAxis(qx | (qy << 9));
+    const double dl = std::sqrt(double(dec.x) * dec.x + double(dec.y) * dec.y + double(dec.z) * dec.z);
+    const double ax[3] = {dec.x / dl, dec.y / dl, dec.z / dl};
+    double cosMin = 1.0;
+    for (const auto& u : ns) cosMin = std::min(cosMin, std::fabs(u[0] * ax[0] + u[1] * ax[1] + u[2] * ax[2]));
+    // psi = acos(cosMin) widened by 2e-3 rad (the kernel's float evaluation of the bound)
+    const double psi = std::acos(std::min(1.0, cosMin)) + 2e-3;
+    const double qCode = psi >= 1.5707963267948966 ? 127.0 : std::ceil(std::sin(psi) * 126.0 + 1e-9);
+    if (qCode > 126.0) return kConeNever;
+    return qx | (qy << 9) | (static_cast<uint32_t>(qCode) << 18) | (static_cast<uint32_t>(kCode) << 25);
+}
+}  // namespace
+
+std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris) {
+    std::vector<uint32_t> out(nodes.size(), kConeNever);
+    if (nodes.empty() || tris.empty()) return out;
+    // primitive range of every node: leaves hold [indexOffset, +numPrimitives); an inner node
+    // the union of its children's (contiguous in BVH order)
+    std::vector<std::array<int32_t, 2>> range(nodes.size(), {0, 0});
+    std::vector<std::pair<int32_t, bool>> st{{0, false}};
+    std::vector<char> seen(nodes.size(), 0);
+    while (!st.empty()) {
+        const auto [i, post] = st.back();
+        st.pop_back();
+        const HBVHNode& n = nodes[static_cast<size_t>(i)];
+        if (n.numPrimitives > 0 || nodes.size() == 1) {
+            range[static_cast<size_t>(i)] = {n.indexOffset, n.indexOffset + n.numPrimitives};
+            seen[static_cast<size_t>(i)] = 1;
+            continue;
+        }
+        if (post) {
+            const auto& l = range[static_cast<size_t>(n.indexOffset)];
+            const auto& r = range[static_cast<size_t>(n.indexOffset) + 1];
+            range[static_cast<size_t>(i)] = {std::min(l[0], r[0]), std::max(l[1], r[1])};
+            seen[static_cast<size_t>(i)] = 1;
+            continue;
+        }
+        st.push_back({i, true});
+        st.push_back({n.indexOffset, false});
+        st.push_back({n.indexOffset + 1, false});
+    }
+    const size_t nn = nodes.size();
+    const unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t i = next.fetch_add(64); i < nn; i = next.fetch_add(64)) {
+            for (size_t k = i; k < std::min(nn, i + 64); ++k) {
+                if (!seen[k]) continue;
+                const auto& r = range[k];
+                if (r[1] > r[0]) out[k] = coneWord(tris, static_cast<size_t>(r[0]), static_cast<size_t>(r[1]));
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < hw; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    return out;
 }
 
 // ---- sample tables (Utils.cpp:43-53, Utils.hpp:209-218) ----------------------------------
@@ -958,6 +1067,19 @@ float haltonSequence(uint32_t index, uint32_t base) {
         index = index / base;
     }
     return nextValue;
+}
+
+// one entry's cos / sin exactly as the reference evaluates them (std::cos / std::sin of a float:
+// libm cosf / sinf; kept out of line so the compiler cannot fold or vectorise the calls)
+__attribute__((noinline)) void hemisphereTrig(float r1, float* c, float* s) {
+    const float phi = kTwoPi * r1;
+    *c = std::cos(phi);
+    *s = std::sin(phi);
+}
+
+void fillHemisphereTrig(const std::vector<float>& shaderTable, std::vector<float>* out) {
+    out->resize(2 * shaderTable.size());
+    for (size_t i = 0; i < shaderTable.size(); ++i) hemisphereTrig(shaderTable[i], &(*out)[2 * i], &(*out)[2 * i + 1]);
 }
 
 void fillHaltonTable(std::vector<float>* table, uint32_t seed) {

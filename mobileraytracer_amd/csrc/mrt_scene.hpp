@@ -135,13 +135,21 @@ std::vector<HBVHNode> buildBVH(std::vector<T>* prims, std::vector<int32_t>* orde
 
 // Converts reference nodes to the device child-box layout: the first topCount inner nodes
 // breadth-first (the trace kernel stages them in LDS), the rest depth-first pre-order.
+// cones: the cull word of every reference node (triangleConeWords), or null (never culled).
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
-                 int topCount = 0, int* topPlaced = nullptr);
+                 int topCount = 0, int* topPlaced = nullptr, const std::vector<uint32_t>* cones = nullptr);
+// The cull word (mrt_common.hpp) of every node of a triangle BVH built by buildBVH over tris
+// (already in BVH order): the normal-line cone and the conditioning bound K of its triangles.
+std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris);
 
 // Utils.cpp:43-53 haltonSequence
 float haltonSequence(uint32_t index, uint32_t base);
 // Utils.hpp:209-218 with std::mt19937(seed) instead of random_device
 void fillHaltonTable(std::vector<float>* table, uint32_t seed);
+// Shader::getCosineSampleHemisphere (Shader.cpp:188-216) takes cos and sin of phi = 2 pi r1 with
+// r1 a shader-table entry, through the platform's libm (cosf / sinf).  They depend on the entry
+// alone, so the host evaluates them once per entry: out[2 i] = cos, out[2 i + 1] = sin.
+void fillHemisphereTrig(const std::vector<float>& shaderTable, std::vector<float>* out);
 constexpr uint32_t kSeedShaderTable = 0x4D525400u;   // Shader.cpp:23,37
 constexpr uint32_t kSeedSamplerTable = 0x4D525401u;  // StaticHaltonSeq.cpp:7-22
 

@@ -49,6 +49,9 @@ __device__ __forceinline__ float4 bload3(BufRes r, uint32_t off) {  // xyz; w un
 __device__ __forceinline__ int2 bload2i(BufRes r, uint32_t off) {
     return __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
+__device__ __forceinline__ int4 bload4i(BufRes r, uint32_t off) {
+    return __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 
 // number of set bits of a wave mask below this lane
 __device__ __forceinline__ int lanesBelowIn(uint64_t m) {
@@ -64,22 +67,67 @@ __device__ __forceinline__ int popCulled(TStack& st, float lim, bool cull) {
     return kRefDone;
 }
 
-// Culling, near-first order and the push of the far child.
-__device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float tr, int refL, int refR, float lim,
-                                              bool cull, TStack& st) {
+// ---- the conservative t-cull -------------------------------------
+// The reference tests every triangle whose ancestors' boxes the ray passes (BVH.hpp:327-384);
+// a box may be skipped only if no triangle inside can produce a hit the reference accepts with
+// t below the current best.  Moller-Trumbore's t is NOT bounded by the triangle's box: for a
+// grazing ray the determinant D = AB . (d x AC) is dominated by rounding and t_c = lambda t_plane
+// with lambda = D / D_c anywhere in (0, 1) (tests/cull_cases.py).  The rounding bounds of the
+// reference's own evaluation order give, for every accepted hit on a triangle T,
+//     |P_c - T| <= rho,  P_c = o + t_c d,
+//     rho = 4 gamma_7 |o - A|_1 |d|_1 K_T / (|d . n_T| - gamma_5 |d|_1 K_T),  K_T = |AB|_1 |AC|_1 / |AB x AC|,
+// so t_c >= the entry of the ray into the box inflated by rho.  Per child the host stores a
+// cone of normal lines (|n . a| >= cos psi for every triangle below) and K = max K_T
+// (mrt_common.hpp, cull words); the key below is that inflated entry with
+// |d . n| >= |d . a| cos psi - |d x a| sin psi and |o - A| <= |o - centre| + half diagonal.
+// No bound (a cone containing a line perpendicular to d, a degenerate triangle): key 0, never culled.
+__device__ __forceinline__ float cullKey(uint32_t w, float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                         float tmx, float tmy, float tmz, v3 o, v3 d, v3 inv) {
+    const uint32_t qc = coneQ(w), kc = coneK(w);
+    if (qc >= 127u || kc >= 127u) return 0.0F;
+    const v3 a0 = coneAxis(w);
+    const v3 a = a0 * (1.0F / sqrtf(dot(a0, a0)));
+    const float dn = sqrtf(dot(d, d));
+    const float c = fabsf(dot(d, a));
+    const float sn = length(cross(d, a)) * 1.000001F + 1e-7F * dn;  // |d x a|, rounded up
+    const float q = static_cast<float>(qc) * (1.0F / 126.0F);       // >= sin(psi)
+    const float cq = sqrtf(fmaxf(1.0F - q * q, 0.0F)) * 0.999999F;   // <= cos(psi)
+    const float smin = c * cq - sn * q;  // |d . n| >= this for every normal line in the cone
+    const float K = __builtin_amdgcn_exp2f(static_cast<float>(kc) * 0.125F) * 1.0001F;
+    const float dl1 = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    // |D_c| >= |N| (|d . n| - gamma_5 |d|_1 K): 2e-6 |d| covers the float evaluation of smin
+    const float den = smin - 2e-6F * dn - 0x1p-20F * K * dl1;
+    if (!(den > 0.0F)) return 0.0F;
+    const v3 ctr{0.5F * (mnx + mxx), 0.5F * (mny + mxy), 0.5F * (mnz + mxz)};
+    const float hd = 0.5F * length(v3{mxx - mnx, mxy - mny, mxz - mnz});
+    // |o - A| <= L; the absolute term covers the box's own rounding (Triangle.cpp:116-123 builds
+    // it from A + AB, A + AC in float) and the centre's
+    const float L = (length(o - ctr) + hd) * 1.0001F + 0x1p-20F * (fabsf(ctr.x) + fabsf(ctr.y) + fabsf(ctr.z) + hd);
+    // main term: 4 gamma_5 sqrt(3) < 2^-18; + 2^-20 L for the last products' rounding
+    const float rho = (0x1p-18F * K * dl1 * L / den + 0x1p-20F * L) * 1.001F;
+    // entry into the box inflated by rho, per axis, each term rounded down (2^-19 relative)
+    const float kx = tmx - fabsf(tmx) * 0x1p-19F - rho * fabsf(inv.x) * (1.0F + 0x1p-19F);
+    const float ky = tmy - fabsf(tmy) * 0x1p-19F - rho * fabsf(inv.y) * (1.0F + 0x1p-19F);
+    const float kz = tmz - fabsf(tmz) * 0x1p-19F - rho * fabsf(inv.z) * (1.0F + 0x1p-19F);
+    return fmaxf(fmaxf(kx, ky), kz);
+}
+
+// Culling against the keys, near-first order (by box entry) and the push of the far child.
+__device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float tr, float kl, float kr, int refL,
+                                              int refR, float lim, bool cull, TStack& st) {
     if (cull) {
-        hl = hl && !(tl > lim);
-        hr = hr && !(tr > lim);
+        hl = hl && !(kl > lim);
+        hr = hr && !(kr > lim);
     }
     if (hl && hr) {
         int nearRef = refL, farRef = refR;
-        float farT = tr;
+        float farK = kr;
         if (cull && tr < tl) {
             nearRef = refR;
             farRef = refL;
-            farT = tl;
+            farK = kl;
         }
-        st.push(farRef, farT);
+        st.push(farRef, farK);
         return nearRef;
     }
     if (hl) return refL;
@@ -87,37 +135,80 @@ __device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float 
     return popCulled(st, lim, cull);
 }
 
+// Cull modes (DScene::cull, mrt_set_tuning key 2):
+//   0  no culling: exactly the reference's visit set;
+//   1  fast: skip a box whose entry exceeds best * (1 + 2^-10).  Exact unless a triangle inside
+//      is hit at a grazing angle (|d . n| below ~1e-3) whose rounding moves Moller-Trumbore's t
+//      below the best hit (tests/cull_cases.py builds one); no such ray in any tested frame;
+//   2  certified: the keys of cullKey (a rigorous lower bound on every acceptable t below the
+//      box), exact for every input; slower (the bound needs each child's normal cone, and the
+//      cones of closed objects hold every direction).
+constexpr int kCullNone = 0, kCullFast = 1, kCullCertified = 2;
+constexpr float kCullMargin = 0x1p-10f;  // cull mode 1
+
+// the limit a key is compared with: a child / stack entry is skipped iff key > limit
+template <int kCull>
+__device__ __forceinline__ float cullLimit(float best) {
+    return kCull == kCullFast ? best + best * kCullMargin : best;
+}
+
 // One BVH2 inner-node visit: returns the next node (near child, or a popped entry).
 // Nodes [0, top) are read from the LDS copy ldsTop (the breadth-first top of the tree).
-// finite: wave-uniform, every active lane's 1/d is finite (slabFinite applies)
-__device__ __forceinline__ int innerStep(BufRes nodes, const GNode* ldsTop, int top, int ref, v3 o, v3 inv, float lim,
-                                         bool cull, TStack& st, TravCount* cnt, bool count, bool finite) {
+// finite: wave-uniform, every active lane's 1/d is finite (slabFinite applies; otherwise the
+// exact slab, and the certified mode does not cull)
+template <int kCull>
+__device__ __forceinline__ int innerStep(BufRes nodes, const GNode* ldsTop, int top, int ref, v3 o, v3 d, v3 inv,
+                                         float lim, TStack& st, TravCount* cnt, bool count, bool finite) {
+    constexpr bool cull = kCull != kCullNone;
     float4 n0, n1, n2;
-    int2 n3;
+    int4 n3;
     if (ref < top) {
         const float4* np = reinterpret_cast<const float4*>(ldsTop + ref);
         n0 = np[0];
         n1 = np[1];
         n2 = np[2];
-        n3 = reinterpret_cast<const int2*>(np)[6];
+        n3 = reinterpret_cast<const int4*>(np)[3];
     } else {
         const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(GNode));
         n0 = bload4(nodes, off);
         n1 = bload4(nodes, off + 16u);
         n2 = bload4(nodes, off + 32u);
-        n3 = bload2i(nodes, off + 48u);  // child refs (the rest is padding)
+        if (kCull == kCullCertified) {
+            n3 = bload4i(nodes, off + 48u);  // child refs and cull words
+        } else {
+            const int2 r = bload2i(nodes, off + 48u);  // child refs
+            n3 = make_int4(r.x, r.y, 0, 0);
+        }
     }
     if (count) cnt->nodes += 2;
-    float tl, tr;
+    float tl, tr, kl = 0.0F, kr = 0.0F;
     bool hl, hr;
-    if (finite) {
-        hl = slabFinite(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
-        hr = slabFinite(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+    if (kCull != kCullCertified) {
+        if (finite) {
+            hl = slabFinite(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
+            hr = slabFinite(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+        } else {
+            hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
+            hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
+        }
+        kl = tl;
+        kr = tr;
+    } else if (finite) {
+        float lx, ly, lz, rx, ry, rz;
+        hl = slabFiniteAxes(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl, &lx, &ly, &lz);
+        hr = slabFiniteAxes(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr, &rx, &ry, &rz);
+        // keys are needed for a child that may be culled now (entry beyond the best hit; a key
+        // never exceeds the entry) and for the far child, which goes on the stack
+        const bool rFar = !(tr < tl);
+        if (cull && hl && (tl > lim || (hr && !rFar)))
+            kl = cullKey(static_cast<uint32_t>(n3.z), n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, lx, ly, lz, o, d, inv);
+        if (cull && hr && (tr > lim || (hl && rFar)))
+            kr = cullKey(static_cast<uint32_t>(n3.w), n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, rx, ry, rz, o, d, inv);
     } else {
         hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
         hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
     }
-    return chooseChildren(hl, hr, tl, tr, n3.x, n3.y, lim, cull, st);
+    return chooseChildren(hl, hr, tl, tr, kl, kr, n3.x, n3.y, lim, cull, st);
 }
 
 // Copies the BVH2 top into LDS (all threads; ends with a barrier).
@@ -133,14 +224,14 @@ __device__ __forceinline__ void stageTop(const DScene& s, GNode* ldsTop) {
 // kAny = false: closest hit -> out[i] = (t, u, v, primitive code);
 // kAny = true:  shadow any-hit -> out[i].w = occluded flag.
 // fetch: kWalkShards cursors, kFetchStride ints apart.
-template <bool kAny, bool kCount>
+template <bool kAny, bool kCount, int kCull>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                                 TStack& st, TravCount* cnt, const GNode* ldsTop) {
     const int top = min(kWalkTop, s.triTop);
     const BufRes nodeBuf = bufferOf(s.triNodes);
     const BufRes triBuf = bufferOf(s.triGeom);
-    const bool cull = s.cull != 0;
+    constexpr bool cull = kCull != kCullNone;
     const int lane = static_cast<int>(threadIdx.x & 63u);
     int rayIdx = -1;
     bool exhausted = false;
@@ -266,9 +357,9 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         }
         // ---- inner nodes until every active lane holds a postponed leaf ----
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
-            const float curLim = bt + bt * kCullMargin;
+            const float curLim = cullLimit<kCull>(bt);
             const bool finite = __ballot(!finiteInv(inv)) == 0;
-            ref = innerStep(nodeBuf, ldsTop, top, ref, o, inv, curLim, cull, st, cnt, kCount, finite);
+            ref = innerStep<kCull>(nodeBuf, ldsTop, top, ref, o, d, inv, curLim, st, cnt, kCount, finite);
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
                 ref = popCulled(st, curLim, cull);
@@ -310,7 +401,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             leaf = 0;
             if (ref < 0) {  // the next node is a leaf too: test it now
                 leaf = ref;
-                ref = popCulled(st, bt + bt * kCullMargin, cull);
+                ref = popCulled(st, cullLimit<kCull>(bt), cull);
             }
         }
     }

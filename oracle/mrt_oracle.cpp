@@ -152,6 +152,14 @@ float haltonSequence(uint32_t index, uint32_t base) {  // Utils.cpp:43-53
     return nextValue;
 }
 
+// Shader.cpp:206-212: cos / sin of phi = two_pi * r1 through libm (std::cos / std::sin of a
+// float = cosf / sinf); out of line, so both calls stay plain libm calls
+__attribute__((noinline)) void hemisphereTrig(float r1, float* c, float* s) {
+    const float phi = kTwoPi * r1;
+    *c = std::cos(phi);
+    *s = std::sin(phi);
+}
+
 std::vector<float> haltonTable(uint32_t seed) {  // Utils.hpp:209-218, fixed seed
     std::vector<float> t(ArraySize);
     for (uint32_t i = 0; i < ArraySize; ++i) t[i] = haltonSequence(i, 2);
@@ -1128,13 +1136,14 @@ struct Engine {
     Vec3 cosineSampleHemisphere(const Vec3& normal, Ctx ctx, uint32_t tc) const {  // Shader.cpp:188-216
         const float uniformRandom1 = shaderTable[sampleIndex(ctx.key, tc, P_HEMI1)];
         const float uniformRandom2 = shaderTable[sampleIndex(ctx.key, tc, P_HEMI2)];
-        const float phi = kTwoPi * uniformRandom1;
+        float cosPhi, sinPhi;
+        hemisphereTrig(uniformRandom1, &cosPhi, &sinPhi);  // std::cos(phi), std::sin(phi), phi = 2 pi r1
         const float r2 = uniformRandom2;
         const float cosTheta = std::sqrt(r2);
         Vec3 u = std::abs(normal[0]) > 0.1F ? Vec3(0.0F, 1.0F, 0.0F) : Vec3(1.0F, 0.0F, 0.0F);
         u = normalize(cross(u, normal));
         const Vec3 v = cross(normal, u);
-        Vec3 direction = u * (std::cos(phi) * cosTheta) + v * (std::sin(phi) * cosTheta) + normal * std::sqrt(1.0F - r2);
+        Vec3 direction = u * (cosPhi * cosTheta) + v * (sinPhi * cosTheta) + normal * std::sqrt(1.0F - r2);
         return normalize(direction);
     }
 
@@ -1490,6 +1499,45 @@ void oracle_primary_hits(void* h, int32_t* kind, int32_t* index, float* t) {
     }
 }
 
+// Shader::rayTrace's intersection part (any = 0: kind / input index / t) or Shader::shadowTrace
+// (any = 1, tmax dist[i]: kind[i] = occluded) of arbitrary rays; src: NULL or (kind, input
+// index) pairs of the primitive each ray leaves (Ray::primitive_, self-exclusion)
+void oracle_trace_rays(void* h, const float* o, const float* d, const float* dist, const int32_t* src, int32_t n,
+                       int any, int32_t* kind, int32_t* index, float* t) {
+    auto* e = static_cast<oracle::Engine*>(h);
+    auto find = [&](int32_t k, int32_t j) -> const void* {
+        if (k == 3) {
+            for (const auto& p : e->triangles->primitives) if (p.inputIndex == j) return &p;
+        } else if (k == 1) {
+            for (const auto& p : e->planes->primitives) if (p.inputIndex == j) return &p;
+        } else if (k == 2) {
+            for (const auto& p : e->spheres->primitives) if (p.inputIndex == j) return &p;
+        } else if (k == 4) {
+            for (const auto& l : e->lights) if (l.index == j) return &l.triangle;
+        }
+        return nullptr;
+    };
+    for (int32_t i = 0; i < n; ++i) {
+        const oracle::Vec3 org(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
+        const oracle::Vec3 dir(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+        const void* prim = src != nullptr ? find(src[2 * i], src[2 * i + 1]) : nullptr;
+        if (any) {
+            const oracle::Ray ray(dir, org, 2, true, prim, nullptr);
+            kind[i] = e->shadowTrace(dist[i], ray) ? 1 : 0;
+            index[i] = -1;
+            t[i] = 0.0F;
+        } else {
+            const oracle::Ray ray(dir, org, 1, false, prim, nullptr);
+            oracle::Intersection it(ray);
+            it = e->closest(it);
+            const bool hit = it.length < oracle::RayLengthMax;
+            kind[i] = hit ? it.kind : 0;
+            index[i] = hit ? static_cast<int32_t>(it.index) : -1;
+            t[i] = it.length;
+        }
+    }
+}
+
 // reference-numbered BVH of the triangles: boxes (n x 6), indexOffset, numPrimitives, prim order
 int64_t oracle_triangle_bvh(void* h, float* boxes, int32_t* offsets, int32_t* counts, int32_t* order) {
     auto* e = static_cast<oracle::Engine*>(h);
@@ -1599,6 +1647,12 @@ int oracle_kat_camera(const char* path, float ratio, float* out) {
 }
 
 float oracle_halton(uint32_t index, uint32_t base) { return oracle::haltonSequence(index, base); }
+// cos / sin of 2 pi r1 for every entry of the shader table (seed 0x4D525400), as the oracle's
+// hemisphere sampler evaluates them: out[2i], out[2i + 1]
+void oracle_hemisphere_trig(float* out) {
+    const auto t = oracle::haltonTable(0x4D525400u);
+    for (size_t i = 0; i < t.size(); ++i) oracle::hemisphereTrig(t[i], out + 2 * i, out + 2 * i + 1);
+}
 void oracle_table(uint32_t seed, float* out) {
     const auto t = oracle::haltonTable(seed);
     std::memcpy(out, t.data(), t.size() * sizeof(float));

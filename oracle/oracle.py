@@ -46,6 +46,7 @@ def lib():
         L.oracle_render_tiles.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_int]
         L.oracle_counts.argtypes = [vp, vp]
         L.oracle_primary_hits.argtypes = [vp, vp, vp, vp]
+        L.oracle_trace_rays.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int, vp, vp, vp]
         L.oracle_triangle_bvh.restype = ctypes.c_int64
         L.oracle_triangle_bvh.argtypes = [vp, vp, vp, vp, vp]
         L.oracle_kat_triangle.argtypes = [f, f, f, f, f, ctypes.c_int, f]
@@ -58,6 +59,7 @@ def lib():
         L.oracle_halton.restype = ctypes.c_float
         L.oracle_halton.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_table.argtypes = [ctypes.c_uint32, vp]
+        L.oracle_hemisphere_trig.argtypes = [vp]
         L.oracle_path_key.restype = ctypes.c_uint32
         L.oracle_path_key.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_sample_index.restype = ctypes.c_uint32
@@ -216,6 +218,20 @@ class Oracle:
         lib().oracle_primary_hits(self._h, k.ctypes.data, i.ctypes.data, t.ctypes.data)
         return k, i, t
 
+    def trace_rays(self, orig, dirs, dist=None, src=None, any_hit=False):
+        """Closest hit (kind, input index, t) or, with any_hit, occlusion within dist of arbitrary
+        rays; src: (n, 2) int32 (kind, input index) of each ray's source primitive, or None."""
+        o = np.ascontiguousarray(orig, np.float32)
+        d = np.ascontiguousarray(dirs, np.float32)
+        n = len(o)
+        ds = np.ascontiguousarray(dist if dist is not None else np.zeros(n), np.float32)
+        sp = None if src is None else np.ascontiguousarray(src, np.int32)
+        k, i, t = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.float32)
+        lib().oracle_trace_rays(self._h, o.ctypes.data, d.ctypes.data, ds.ctypes.data,
+                                None if sp is None else sp.ctypes.data, n, int(any_hit),
+                                k.ctypes.data, i.ctypes.data, t.ctypes.data)
+        return k, i, t
+
     def triangle_bvh(self):
         n = lib().oracle_triangle_bvh(self._h, None, None, None, None)
         nt = self.counts()["triangles"]
@@ -283,6 +299,12 @@ def halton(index, base=2):
 def table(seed):
     out = np.empty(1 << 20, np.float32)
     lib().oracle_table(seed, out.ctypes.data)
+    return out
+
+
+def hemisphere_trig():
+    out = np.empty(2 << 20, np.float32)
+    lib().oracle_hemisphere_trig(out.ctypes.data)
     return out
 
 

@@ -1,0 +1,150 @@
+"""Full-frame parity at the benchmark configurations (C3, C4), every pixel.
+
+* C3 (Conference 1920x1080, 1 spp, Whitted): all 2,058,240 primary hit ids (kind, input index,
+  t bits) and the whole bitmap bit-exact against the oracle; rows 1072-1079 untouched.
+* C4 (1920x1080, 4 spp, PathTracer, depth 5): the whole bitmap bit-exact, the ray count equal.
+* Cull invariance at full size: no cull / fast cull / certified cull give the same bitmap, hits
+  and ray counts.
+* Random rays through the whole room: closest hits and shadow tests of 4M rays, every cull mode
+  against the reference walk, and a sample against the oracle.
+
+The scene is the Conference stand-in (mobileraytracer_amd/scenes.py: the real conference.obj is
+absent from the reference snapshot).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import SENTINEL, make_cfg, oracle_for
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16  # the GPU box's CPU share
+
+
+def oracle_full(oracle_mod, cfg):
+    o = oracle_for(oracle_mod, cfg)
+    bm = np.full(cfg.width * cfg.height, SENTINEL, np.int32)
+    _, rays = o.render(bm, threads=THREADS)
+    o.close()
+    return bm, rays
+
+
+@pytest.fixture(scope="module")
+def c3_gpu():
+    import mobileraytracer_amd as m
+    cfg = make_cfg(1920, 1080, shader=1, scene="conference")
+    out = {}
+    with m.Renderer(cfg) as r:
+        for cull in (1, 0, 2):
+            r.set_tuning(2, cull)
+            bm = np.full(1920 * 1080, SENTINEL, np.int32)
+            r.render_frame(bm)
+            out[cull] = (bm, r.frame_stats(), r.primary_hits())
+    return cfg, out
+
+
+def test_c3_primary_hits_full_frame(oracle_mod, c3_gpu):
+    cfg, out = c3_gpu
+    o = oracle_for(oracle_mod, cfg)
+    ok, oi, ot = o.primary_hits()
+    o.close()
+    k, i, t = out[1][2]
+    rendered = ok >= 0
+    assert rendered.sum() == 1920 * 1072
+    assert np.array_equal(k, ok) and np.array_equal(i, oi)
+    assert np.array_equal(t.view(np.int32), ot.view(np.int32))
+    assert (k[rendered] > 0).mean() > 0.99  # the room is closed: nearly every camera ray hits
+
+
+def test_c3_whitted_bitmap_full_frame(oracle_mod, c3_gpu):
+    cfg, out = c3_gpu
+    bm, st, _ = out[1]
+    ref, ref_rays = oracle_full(oracle_mod, cfg)
+    rows = bm.reshape(1080, 1920)
+    assert (rows[1072:] == SENTINEL).all()  # H / 16 = 67: rows 1072-1079 never rendered (Renderer.cpp:33-34)
+    assert (rows[:1072] != SENTINEL).all()
+    assert np.array_equal(bm, ref), int((bm != ref).sum())
+    assert st["rays"] + st["shadowRays"] == ref_rays
+
+
+def test_c3_cull_modes_identical_full_frame(c3_gpu):
+    _, out = c3_gpu
+    base_bm, base_st, base_hits = out[1]
+    for cull in (0, 2):
+        bm, st, hits = out[cull]
+        assert np.array_equal(bm, base_bm), cull
+        assert (st["rays"], st["shadowRays"]) == (base_st["rays"], base_st["shadowRays"])
+        assert all(np.array_equal(a, b) for a, b in zip(hits, base_hits))
+
+
+@pytest.fixture(scope="module")
+def c4_gpu():
+    import mobileraytracer_amd as m
+    cfg = make_cfg(1920, 1080, shader=2, scene="conference", spp=4, max_depth=5)
+    out = {}
+    with m.Renderer(cfg) as r:
+        for cull in (1, 0, 2):
+            r.set_tuning(2, cull)
+            bm = np.full(1920 * 1080, SENTINEL, np.int32)
+            r.render_frame(bm)
+            out[cull] = (bm, r.frame_stats())
+    return cfg, out
+
+
+def test_c4_pathtracer_full_frame(oracle_mod, c4_gpu):
+    cfg, out = c4_gpu
+    bm, st = out[1]
+    assert st["primaryRays"] == 4 * 1920 * 1072
+    ref, ref_rays = oracle_full(oracle_mod, cfg)
+    assert np.array_equal(bm, ref), int((bm != ref).sum())
+    assert st["rays"] + st["shadowRays"] == ref_rays
+
+
+def test_c4_cull_modes_identical_full_frame(c4_gpu):
+    _, out = c4_gpu
+    base_bm, base_st = out[1]
+    for cull in (0, 2):
+        bm, st = out[cull]
+        assert np.array_equal(bm, base_bm), (cull, int((bm != base_bm).sum()))
+        assert (st["rays"], st["shadowRays"]) == (base_st["rays"], base_st["shadowRays"])
+
+
+def random_rays(n, seed, box_min, box_max):
+    rng = np.random.default_rng(seed)
+    o = (box_min + rng.random((n, 3)) * (box_max - box_min)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    return o, d
+
+
+def test_random_rays_all_cull_modes(oracle_mod):
+    """4M rays from random points of the room in random directions, closest hit and a shadow test
+    to a random distance: walk 1 in every cull mode equals the reference walk (walk 0), and a
+    20,000-ray sample equals the oracle."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, shader=1, scene="conference")
+    with m.Renderer(cfg) as r:
+        boxes, _, _, _ = m.triangle_bvh(cfg)
+        lo, hi = boxes[0, :3], boxes[0, 3:]
+        o, d = random_rays(4_000_000, 7, lo, hi)
+        dist = np.random.default_rng(8).random(len(o)).astype(np.float32) * np.float32(np.linalg.norm(hi - lo))
+        res = {}
+        for walk, cull in ((0, 0), (1, 0), (1, 1), (1, 2)):
+            r.set_tuning(1, walk)
+            r.set_tuning(2, cull)
+            res[(walk, cull)] = (r.trace_rays(o, d), r.trace_rays(o, d, dist=dist, any_hit=True)[0])
+    ref_hits, ref_occ = res[(0, 0)]
+    assert (ref_hits[0] == 3).mean() > 0.5 and 0.05 < ref_occ.mean() < 0.95
+    for key, (hits, occ) in res.items():
+        assert all(np.array_equal(a, b) for a, b in zip(hits, ref_hits)), key
+        assert np.array_equal(occ, ref_occ), key
+    o_ = oracle_for(oracle_mod, cfg)
+    sel = np.arange(0, len(o), len(o) // 20000)
+    ok, oi, ot = o_.trace_rays(o[sel], d[sel])
+    occ = o_.trace_rays(o[sel], d[sel], dist=dist[sel], any_hit=True)[0]
+    o_.close()
+    assert np.array_equal(ok, ref_hits[0][sel]) and np.array_equal(oi, ref_hits[1][sel])
+    assert np.array_equal(ot.view(np.int32), ref_hits[2][sel].view(np.int32))
+    assert np.array_equal(occ, ref_occ[sel])

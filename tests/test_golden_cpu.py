@@ -135,3 +135,15 @@ def test_parallel_bvh_build_equals_reference_build(oracle_mod, scene):
     oboxes, ooff, ocnt, oorder = o.triangle_bvh()
     assert _bvh_walk(boxes, off, cnt) == _bvh_walk(oboxes, ooff, ocnt)
     assert np.array_equal(order, oorder)
+
+
+def test_hemisphere_trig_table_matches_oracle(oracle_mod):
+    """The renderer's host table of cos / sin(two_pi * r1) (Shader.cpp:206-212) equals, bit for
+    bit, the oracle's own libm evaluation of every shader-table entry; both tables equal too."""
+    import mobileraytracer_amd as m
+    a, b, t = m.sample_tables()
+    assert np.array_equal(a, oracle_mod.table(0x4D525400)) and np.array_equal(b, oracle_mod.table(0x4D525401))
+    ot = oracle_mod.hemisphere_trig().reshape(-1, 2)
+    assert np.array_equal(t.view(np.int32), ot.view(np.int32))
+    ph = np.float32(2 * np.pi) * a
+    assert np.abs(t[:, 0] - np.cos(ph.astype(np.float64))).max() < 1e-6

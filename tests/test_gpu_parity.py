@@ -2,12 +2,10 @@
 
 Bars (SURVEY.md section 8 / BASELINE.md):
   * primary-ray hit ids (kind, index, t): bit-exact, 100 % of pixels;
-  * Whitted images (no libm transcendentals on the path): bit-exact bitmaps and ray counts;
-  * PathTracer images: per-channel |delta| <= 2/255 on >= 99.9 % of pixels and mean |delta|
-    <= 0.25/255 (the only float difference is glibc cosf/sinf vs the GPU's double-rounded
-    cos/sin inside the cosine-hemisphere sampler, which can move a bounce direction by an ulp);
-  * full-size configs (1920x1080, 3840x2160): oracle spot tiles + size-independent properties
-    (determinism, shard invariance, chunk invariance, untouched rows).
+  * Whitted and PathTracer images: bit-exact bitmaps and ray counts (the PathTracer's only libm
+    calls, cos / sin of the hemisphere angle, come from a host table of the platform's cosf /
+    sinf, which the oracle shares: tests/test_golden_cpu.py);
+  * full frames (1920x1080): tests/test_full_frame.py; 3840x2160: shard invariance here.
 """
 import json
 import os
@@ -146,12 +144,8 @@ def test_other_scenes_and_shaders(oracle_mod, case):
     bm, rays, _ = gpu_render(cfg)
     ref, ref_rays = oracle_render(oracle_mod, cfg)
     once = coverage(cfg.width, cfg.height) == 1
-    if cfg.shader == 2:
-        assert_within_tolerance(bm, ref, once & (ref != SENTINEL))
-        assert abs(rays - ref_rays) <= 0.002 * ref_rays, (rays, ref_rays)
-    else:
-        assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
-        assert rays == ref_rays
+    assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
+    assert rays == ref_rays
     assert len(np.unique(bm)) > 1
 
 
@@ -170,12 +164,8 @@ def test_naive_and_missing_accelerator(oracle_mod, case):
     bm, rays, _ = gpu_render(cfg)
     ref, ref_rays = oracle_render(oracle_mod, cfg)
     once = coverage(cfg.width, cfg.height) == 1
-    if cfg.shader == 2:
-        assert_within_tolerance(bm, ref, once & (ref != SENTINEL))
-        assert abs(rays - ref_rays) <= 0.002 * ref_rays, (rays, ref_rays)
-    else:
-        assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
-        assert rays == ref_rays
+    assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
+    assert rays == ref_rays
     if cfg.accelerator == 1 and cfg.shader == 1:  # primary hit ids, bit-exact
         g = gpu_hits(cfg)
         o = oracle_for(oracle_mod, cfg)
@@ -210,7 +200,7 @@ def test_c1_matches_committed_fixture():
     assert rays == golden["cornell256_whitted"]["rays"]
 
 
-# ---- PathTracer: stated tolerance -----------------------------------------------------------------
+# ---- PathTracer: bit-exact (the hemisphere's cos / sin come from the host libm table) ----------
 @pytest.mark.parametrize("case", [
     dict(width=256, height=256, spp=4),
     dict(width=128, height=128, spp=4, scene="water"),            # branching ray tree (Kd + Ks)
@@ -219,74 +209,37 @@ def test_c1_matches_committed_fixture():
     dict(width=128, height=128, spp=4, sceneIndex=2),             # area lights + transmission sphere
     dict(width=128, height=128, spp=4, scene="teapot"),           # textured Kd read after the diffuse child
 ])
-def test_pathtracer_within_tolerance(oracle_mod, case):
+def test_pathtracer_bit_exact(oracle_mod, case):
     cfg = make_cfg(shader=2, **case)
     bm, rays, _ = gpu_render(cfg)
     ref, ref_rays = oracle_render(oracle_mod, cfg)
-    assert np.array_equal(bm == SENTINEL, ref == SENTINEL)
-    frac_ok, mean, exact = assert_within_tolerance(bm, ref)
-    assert abs(rays - ref_rays) <= 0.002 * ref_rays, (rays, ref_rays)
-    print(f"exact pixels {exact:.5f}, within 2/255 {frac_ok:.5f}, mean |d| {mean:.4f}, rays {rays} vs {ref_rays}")
+    once = coverage(cfg.width, cfg.height) == 1
+    assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
+    assert rays == ref_rays
 
 
-# ---- C3 / C4 / C5 at full size ------------------------------------------------------------------
-SPOT_TILES = (0, 7, 119, 136, 255)
+# ---- C3 / C4 full frames: tests/test_full_frame.py; C5 shards below ----------------------------
 
 
-def _spot_check(oracle_mod, cfg, bm, exact):
-    for t in SPOT_TILES:
-        ref, _ = oracle_render(oracle_mod, cfg, first_tile=t, num_tiles=1)
-        mask = ref != SENTINEL
-        assert mask.sum() == (cfg.width // 16) * (cfg.height // 16)
-        if exact:
-            assert np.array_equal(bm[mask], ref[mask]), t
-        else:
-            assert_within_tolerance(bm, ref, mask)
-
-
-def test_c3_conference_1080_whitted(oracle_mod):
-    cfg = make_cfg(1920, 1080, shader=1, scene="conference")
-    bm, rays, st = gpu_render(cfg)
-    rows = bm.reshape(1080, 1920)
-    assert (rows[1072:] == SENTINEL).all()  # H / 16 = 67: rows 1072-1079 are never rendered (Renderer.cpp:33-34)
-    assert (rows[:1072] != SENTINEL).all()
-    assert st["primaryRays"] == 1920 * 1072
-    _spot_check(oracle_mod, cfg, bm, exact=True)
-
-
-def test_c4_conference_1080_pathtracer(oracle_mod):
-    cfg = make_cfg(1920, 1080, shader=2, scene="conference", spp=4, max_depth=5)
-    bm, rays, st = gpu_render(cfg)
-    bm2, rays2, _ = gpu_render(cfg)
-    assert np.array_equal(bm, bm2) and rays == rays2  # deterministic
-    assert st["primaryRays"] == 4 * 1920 * 1072
-    _spot_check(oracle_mod, cfg, bm, exact=False)
-
-
-def test_chunked_passes_and_cull_are_invariant():
+def test_chunked_passes_are_invariant():
     base = make_cfg(1920, 1080, shader=2, scene="conference", spp=4, max_depth=5)
     bm, rays, _ = gpu_render(base)
     chunked = make_cfg(1920, 1080, shader=2, scene="conference", spp=4, max_depth=5, maxPathsPerPass=1 << 20)
     bm2, rays2, _ = gpu_render(chunked)
     assert np.array_equal(bm, bm2) and rays == rays2
-    small = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5)
-    nocull = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5, cull=0)
-    a, ra, _ = gpu_render(small)
-    b, rb, _ = gpu_render(nocull)
-    assert np.array_equal(a, b) and ra == rb
 
 
 def test_trace_walks_are_identical():
     """The per-wave reference walk (tuning key 1 = 0: 64-ray batches, plain DFS of
     BVH.hpp:327-384) and the persistent while-while walk (1) return the same hits, images and
-    ray counts, with and without the conservative t-cull (key 2)."""
+    ray counts in every cull mode (key 2: none, fast, certified)."""
     import mobileraytracer_amd as m
     for cfg in (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
                 make_cfg(128, 128, shader=2, scene="water", spp=2), make_cfg(64, 64, shader=1),
                 make_cfg(128, 128, shader=1, sceneIndex=2)):
         outs = []
         with m.Renderer(cfg) as r:
-            for walk, cull in ((1, 1), (0, 1), (1, 0), (0, 0)):
+            for walk, cull in ((1, 1), (0, 0), (1, 0), (1, 2)):
                 r.set_tuning(1, walk)
                 r.set_tuning(2, cull)
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
