@@ -6,14 +6,23 @@
 
 Workload (BASELINE.json metric, configs[3] = C4): the Conference scene at 1920x1080,
 4 samples per pixel, PathTracer, RayDepthMax 5 (camera ray + 4 bounces), samplesLight 1.
-A step is one Renderer::renderFrame (all 4 samples).  "Rays" counts every ray constructed
-(camera, shadow, diffuse, specular, transmission), as the reference's Ray id counter does
-(Ray.cpp:25-28; C_wrapper.cpp:247-256).  The frame buffer stays in device memory; the
-reference's host-bitmap copy is excluded (DESIGN.md gives the PCIe-inclusive rate).
+A step is one Renderer::renderFrame (all 4 samples).  `value` is WALKED Mrays/s: every ray
+whose BVH walk ran (camera, diffuse, specular and shadow rays; the depth-capped last level's
+rays are built and counted by the reference but shade to zero without a walk, DESIGN.md
+section 3).  The reference's own count, every Ray constructed (Ray.cpp:25-28,
+C_wrapper.cpp:247-256), is `config.mrays_per_s_built`.  The frame buffer stays in device
+memory; the reference's host-bitmap copy is excluded (DESIGN.md gives the PCIe-inclusive rate).
+The timed frames run with per-launch event timing OFF.
 
-Multi-GPU: one process per GPU; the frame's screen tiles are sharded (unit u -> rank u % N),
-each rank renders its shard into a packed buffer, one RCCL gather brings the shards to rank 0,
-which scatters them into the bitmap.  Total work is one frame whatever N is: scaling "strong".
+Per-kernel roofline: outside the timed region one counting frame (node / triangle fetches per
+ray, shaded vertices) and two frames with the shadow stream serialised and HIP events around
+every launch give each kernel's average launch duration; `achieved` = algorithmic bytes per
+launch / that duration.
+
+Multi-GPU: one process per GPU; the frame's pixel units (reference tile t cut into 8-row bands b)
+are sharded unit (t, b) -> rank (t + b) % N; each rank renders its shard into a packed buffer,
+one RCCL gather brings the shards to rank 0, which scatters them into the bitmap.  Total work
+is one frame whatever N is: scaling "strong".
 """
 import argparse
 import json
@@ -24,9 +33,12 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-BASELINE_METRIC = "Mrays/s + ms/frame, Conference OBJ 1920\u00d71080 4spp, 1/2/4/8 GPU"  # BASELINE.json "metric"
-PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-PEAK_L2_GBS = 34500.0  # aggregate L2 (8 x 4 MiB) read rate, same guide, section "L2 (per XCD)"
+BASELINE_METRIC = "Mrays/s + ms/frame, Conference OBJ 1920×1080 4spp, 1/2/4/8 GPU"  # BASELINE.json "metric"
+# /opt/skills/guides/MI355X_MICROARCH.md: HBM 8.0 TB/s peak; L2 34.5 TB/s aggregate, 36.9 TB/s
+# with the L1-reuse contribution: the most the vector-memory path delivers to the CUs, the
+# ceiling of a gather-bound kernel whose working set is cache-resident
+PEAK_HBM_GBS = 8000.0
+PEAK_VMEM_GBS = 36900.0
 
 
 def parse():
@@ -39,34 +51,107 @@ def parse():
     p.add_argument("--spp", type=int, default=4)
     p.add_argument("--max-depth", type=int, default=5)
     p.add_argument("--shader", type=int, default=2)
+    p.add_argument("--overlap", type=int, default=1, help="shadow rays on their own stream (timed frames)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-tiles", type=int, default=64, help="tiles of the frame timed on the CPU oracle")
     return p.parse_args()
 
 
+def effective_cores():
+    """Host threads this process may use: its CPU affinity, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, scene):
-    """The oracle (CPU restatement, AoS + recursion + std::thread tiles) on a bounded sample of
-    the same workload: every 4th reference tile (64 of 256) of the same frame."""
+    """The oracle (CPU restatement of the reference: AoS triangles, by-value hit records, the
+    reference's DFS, recursive shaders, std::thread tile loop) in timing-faithful mode (the
+    reference's shared atomic sampler cursors) over the WHOLE frame, on every core this
+    process may use."""
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = effective_cores()
     o = O.Oracle(args.width, args.height, args.shader, -1, args.spp, 1, args.max_depth,
                  obj=scene[0], mtl=scene[1], cam=scene[2])
-    tiles = list(range(0, o.num_tiles(), max(1, o.num_tiles() // args.cpu_tiles)))[: args.cpu_tiles]
+    o.set_faithful(True)
     t0 = time.perf_counter()
-    _, rays = o.render_tiles(tiles, threads=threads)
+    _, rays = o.render(threads=threads)
     dt = time.perf_counter() - t0
     o.close()
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{len(tiles)} of 256 reference tiles (every 4th) of the same frame, {rays} rays, {dt:.1f} s"}
+            "cpu_model": cpu_model(),
+            "sample": f"full frame (all 256 reference tiles, {args.spp} spp), {rays} rays built, {dt:.1f} s; "
+                      "timing-faithful draws (shared atomic sampler cursors)",
+            "rays_counted": "built (every Ray constructed, Ray.cpp:25-28)"}
 
 
-def pmc_traffic_per_launch():
-    """HBM bytes per k_trace launch from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(HERE, "profiles", "pmc_trace_kernel.json")
+def pmc_traffic():
+    """Bytes beyond L2 per launch for each kernel from the committed rocprofv3 PMC summary
+    (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), if present."""
+    path = os.path.join(HERE, "profiles", "r02_pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return {}
     with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        return json.load(f).get("bytes_beyond_l2_per_launch", {})
+
+
+def kernel_roofline(r, step):
+    """Per-kernel algorithmic bytes and serialised launch durations (outside the timed region)."""
+    r.set_profiling(counting=True)
+    step()
+    c = r.frame_stats()
+    r.set_tuning(3, 0)  # shadow rays on the render stream: every launch timed alone
+    r.set_profiling(timing=True)
+    tr_ms = sh_ms = sd_ms = 0.0
+    tr_n = sh_n = sd_n = 0
+    for _ in range(2):
+        step()
+        t = r.frame_stats()
+        tr_ms += t["traceMs"]; sh_ms += t["shadowMs"]; sd_ms += t["shadeMs"]
+        tr_n += t["traceLaunches"]; sh_n += t["shadowLaunches"]; sd_n += t["shadeLaunches"]
+    r.set_profiling()
+    r.set_tuning(3, 1)
+    walked, shadows, shaded = c["walkedRays"], c["shadowRays"], c["shadedVertices"]
+    # k_trace: per ray 32 (ray read: origin, direction) + 16 (hit write) + 32 per node record + 36 per
+    # triangle test; k_shadow: 32 (ray read) + 4 (flag write) + the same gathers
+    trace_b = 48.0 * walked + 32.0 * c["nodeRecords"] + 36.0 * c["triTests"]
+    shadow_b = 36.0 * shadows + 32.0 * c["shadowNodeRecords"] + 36.0 * c["shadowTriTests"]
+    # k_shade (DESIGN.md section 3): per vertex 52 read (origin, direction, hit, tree code) + 16
+    # written (vertex or result record); per shaded hit 48 (normals, material id) + 64 (material)
+    # + 64 (light) + 48 (six table draws); per shadow ray 48 written; per child ray 36 written
+    levels = c["levelRays"]
+    shaded_rays = sum(levels[:r.config.maxDepth])  # levels 1..maxDepth (the last is not shaded)
+    children = sum(levels[1:r.config.maxDepth + 1])
+    shade_b = 68.0 * shaded_rays + 224.0 * shaded + 48.0 * shadows + 36.0 * children
+    fr = max(1, 2)
+
+    def entry(name, frame_bytes, ms, launches):
+        launches_pf = launches / fr
+        per_launch = frame_bytes / max(1.0, launches_pf)
+        avg_ms = ms / max(1, launches)
+        ach = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        return {"algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches_per_frame": launches_pf,
+                "achieved": ach, "peak": PEAK_VMEM_GBS, "unit": "GB/s", "frac": ach / PEAK_VMEM_GBS}
+
+    per_ray = {"nodes": c["nodeRecords"] / max(1, walked), "tris": c["triTests"] / max(1, walked),
+               "shadow_nodes": c["shadowNodeRecords"] / max(1, shadows),
+               "shadow_tris": c["shadowTriTests"] / max(1, shadows), "shaded_vertices": shaded}
+    return {"k_trace": entry("k_trace", trace_b, tr_ms, tr_n), "k_shadow": entry("k_shadow", shadow_b, sh_ms, sh_n),
+            "k_shade": entry("k_shade", shade_b, sd_ms, sd_n)}, per_ray
 
 
 def main():
@@ -98,6 +183,7 @@ def main():
                    mtlFilePath=scene[1], camFilePath=scene[2], rankIndex=rank, rankCount=world,
                    device=torch.cuda.current_device())
     r = m.Renderer(cfg)
+    r.set_tuning(3, args.overlap)
     info = r.scene_info()
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
@@ -124,26 +210,18 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # one counting frame (outside the timed region): node / triangle fetches per ray
-    trace_variant = r.get_tuning(1)
-    r.set_profiling(counting=True)
-    step()
-    counted = r.frame_stats()
-    r.set_profiling(timing=True)
+    kernels, per_ray = kernel_roofline(r, step)
+    r.set_tuning(3, args.overlap)
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     rays0 = r.get_total_casted_rays()
-    t0 = time.perf_counter()
-    trace_ms = 0.0
-    trace_launches = 0
     walked = 0  # closest-hit rays traversed + shadow rays: the rays whose walk ran
+    t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         st = r.frame_stats()
-        trace_ms += st["traceMs"]
-        trace_launches += st["traceLaunches"]
         walked += st["walkedRays"] + st["shadowRays"]
     torch.cuda.synchronize()
     if world > 1:
@@ -159,31 +237,20 @@ def main():
         n = torch.tensor([rays, walked], dtype=torch.float64, device=red)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         rays, walked = [int(x) for x in n.tolist()]
-        agg = torch.tensor([counted["walkedRays"], counted["nodeRecords"], counted["triTests"], trace_ms,
-                            trace_launches], dtype=torch.float64, device=red)
-        dist.all_reduce(agg, op=dist.ReduceOp.SUM)
-        c_rays, c_nodes, c_tris, trace_ms, trace_launches = [float(x) for x in agg.tolist()]
-    else:
-        c_rays, c_nodes, c_tris = counted["walkedRays"], counted["nodeRecords"], counted["triTests"]
 
     if rank != 0:
         dist.destroy_process_group()
         return
 
-    # roofline of the dominant kernel (k_trace, closest hit), SURVEY.md section 8(d):
-    # B_ray = 32 (ray read) + 16 (hit write) + 32 * N_node + 36 * N_tri, summed over the
-    # frame's closest-hit rays; per launch = frame bytes / launches per frame
     frames = max(1, args.steps)
-    launches_per_frame = trace_launches / frames
-    bytes_per_frame = 48.0 * c_rays + 32.0 * c_nodes + 36.0 * c_tris
-    bytes_per_launch = bytes_per_frame / max(1.0, launches_per_frame)  # launches of all ranks
-    avg_launch_ms = trace_ms / max(1.0, trace_launches)
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    traffic = pmc_traffic_per_launch() if world == 1 else None
+    traffic = pmc_traffic() if world == 1 else {}
+    for name, e in kernels.items():
+        tb = traffic.get(name)
+        e["traffic"] = tb
+        e["hbm_frac"] = (tb / (e["avg_launch_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS) if tb and e["avg_launch_ms"] > 0 else None
+    dom = kernels["k_trace"]
     out = {
         "metric": BASELINE_METRIC,
-        # rays whose walk ran: the depth-capped last level's rays (built, shaded to zero, walk
-        # skipped) are not counted; rays_built_per_frame is the reference's ray count
         "value": walked / elapsed / 1e6,
         "unit": "Mrays/s",
         "n_gpus": world,
@@ -209,23 +276,26 @@ def main():
             "rays_walked_per_frame": walked / frames,
             "rays_built_per_frame": rays / frames,
             "mrays_per_s_built": rays / elapsed / 1e6,
+            "value_counts": "walked rays (closest-hit walks run + shadow rays)",
+            "event_timing_in_timed_frames": False,
         },
         "roofline": {
-            "bound": "hbm",
+            # the walk is bound by the per-CU vector-memory path serving divergent gathers of a
+            # cache-resident scene (PMC: texture-data unit busy ~92 %, bytes beyond L2 ~11 % of the
+            # algorithmic bytes; profiles/), not by HBM
+            "bound": "vmem-gather",
             "kernel": "k_trace (closest hit)",
-            "achieved": achieved,
-            "peak": PEAK_HBM_GBS,
+            "achieved": dom["achieved"],
+            "peak": PEAK_VMEM_GBS,
             "unit": "GB/s",
-            "frac": achieved / PEAK_HBM_GBS,
-            "traffic": traffic,
-            "avg_launch_ms": avg_launch_ms,
-            "algorithmic_bytes_per_launch": bytes_per_launch,
-            "per_ray": {"nodes": c_nodes / max(1.0, c_rays), "tris": c_tris / max(1.0, c_rays)},
-            "frac_of_l2_peak": achieved / PEAK_L2_GBS,
-            "note": ("node/triangle gathers hit in L2 and the 256 MiB Infinity Cache (the Conference "
-                     "working set is ~30 MB), so algorithmic bytes/s is not capped by HBM; `traffic` "
-                     "is the rocprofv3-measured bytes beyond L2 per launch (profiles/pmc_trace_kernel.json)"),
-            "trace_variant": trace_variant,
+            "frac": dom["frac"],
+            "traffic": dom["traffic"],
+            "avg_launch_ms": dom["avg_launch_ms"],
+            "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
+            "per_ray": per_ray,
+            "peak_source": "MI355X_MICROARCH.md: L2 34.5 TB/s aggregate, 36.9 TB/s with L1 reuse",
+            "durations": "serialised frames (shadow stream off), HIP events on the render stream",
+            "kernels": kernels,
         },
         "cpu_baseline": None,
     }

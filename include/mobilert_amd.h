@@ -101,6 +101,9 @@ typedef struct mrt_frame_stats {
     uint64_t maxNodeRecordsPerRay; /* counting pass only: most node records one ray fetched */
     uint64_t walkedRays;           /* closest-hit rays traversed: `rays` minus the depth-capped last
                                       level's, whose walk is skipped (tuning key 7) */
+    uint64_t shadedVertices;       /* counting pass only: hits k_shade shaded (not emissive, under the
+                                      depth cap) */
+    int64_t shadeLaunches;         /* k_shade launches of the frame */
 } mrt_frame_stats;
 
 const char *mrt_last_error(void);

@@ -52,7 +52,7 @@ class MrtFrameStats(ctypes.Structure):
         ("levelRays", ctypes.c_uint64 * 16), ("levelShadowRays", ctypes.c_uint64 * 16),
         ("levelTraceMs", ctypes.c_double * 16), ("levelShadowMs", ctypes.c_double * 16),
         ("maxNodeRecordsPerRay", ctypes.c_uint64),
-        ("walkedRays", ctypes.c_uint64),
+        ("walkedRays", ctypes.c_uint64), ("shadedVertices", ctypes.c_uint64), ("shadeLaunches", ctypes.c_int64),
     ]
 
 

@@ -548,6 +548,10 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
         blockAllocPair(pair, active ? v.nChild : 0, active ? v.nShadow : 0, &childBase, &shadowBase, allocLds, parity);
         parity ^= 1;
         if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, deadNext != 0);
+        if (a.stats != nullptr) {  // counting pass: shaded (non-terminal) vertices
+            const uint64_t m = __ballot(active && !v.terminal);
+            if (laneId() == 0 && m != 0) atomicAdd(a.stats + kStatShaded, static_cast<unsigned long long>(__popcll(m)));
+        }
     }
 }
 

@@ -42,7 +42,9 @@ constexpr int kStatLevelRays = 8;                     // + level - 1: rays of ea
 constexpr int kStatLevelShadows = 8 + kMaxLevels;     // + level - 1: shadow rays of each level
 constexpr int kStatMaxNodesRay = 8 + 2 * kMaxLevels;  // counting builds: most node records of one ray
 constexpr int kStatSkipped = kStatMaxNodesRay + 1;   // rays of a last level whose walk was skipped
-constexpr int kNumStats = kStatSkipped + 1;
+constexpr int kStatShaded = kStatSkipped + 1;        // counting pass: vertices k_shade shaded (hit, not emissive, not capped)
+constexpr int kStatShadeLaunches = kStatShaded + 1;  // k_shade launches of the frame
+constexpr int kNumStats = kStatShadeLaunches + 1;
 
 // One level of the wavefront (SoA queues).
 struct Level {
@@ -91,6 +93,7 @@ struct ShadeArgs {
     int maxDepth;      // RayDepthMax
     int samplesLight;  // Config::samplesLight
     float maxPoint[3]; // DepthMap::maxPoint_ (C_wrapper.cpp:79-131 maxDist)
+    unsigned long long* stats;  // counting pass only (else null): kStatShaded
 };
 
 struct AccumArgs {

@@ -129,6 +129,7 @@ struct mrt_renderer {
     hipStream_t stream = nullptr;
     int overlap = 1;                     // tuning key 3: shadow rays on their own stream
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
+    int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
 
     // state (Renderer.hpp:30-40)
@@ -425,12 +426,14 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     const int shader = r->shader;
     const bool timing = (r->profileFlags & 1) != 0;
     const bool counting = (r->profileFlags & 2) != 0;
-    ShadeArgs sa{r->maxDepth, std::max(1, r->cfg.samplesLight), {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z}};
+    mrt_renderer::Pipe& pp = r->pipe;
+    ShadeArgs sa{r->maxDepth, std::max(1, r->cfg.samplesLight), {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z},
+                 counting ? pp.stats : nullptr};
     const int nLevels = r->nLevels;
     const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
-    mrt_renderer::Pipe& pp = r->pipe;
     MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * kNumStats, st));
     pp.evCount = 0;
+    r->shadeLaunches = 0;
     // Any-hit (shadow) rays of level L run on a second stream, overlapped with the closest-hit
     // trace and shading of level L+1: the persistent kernels' drain phases fill each other.
     // Orders: shade(L) -> shadow(L); shadow(L) -> shade(L+2) (shade(L+2) rewrites level L+2's
@@ -477,9 +480,11 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, st);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
-            if (!(skipLastShade && l == nLevels))
+            if (!(skipLastShade && l == nLevels)) {
                 launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, st,
                             skipLastShade && l + 1 == nLevels);
+                ++r->shadeLaunches;
+            }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             if (sb != st) {
                 const hipEvent_t shaded = syncEvent(pp, sync++);
@@ -536,6 +541,8 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->shadowNodeRecords += hs[kStatNodesShadow];
     fs->shadowTriTests += hs[kStatTrisShadow];
     fs->maxNodeRecordsPerRay = std::max<uint64_t>(fs->maxNodeRecordsPerRay, hs[kStatMaxNodesRay]);
+    fs->shadedVertices += hs[kStatShaded];
+    fs->shadeLaunches += r->shadeLaunches;
     for (int l = 0; l < kMaxLevels; ++l) {
         fs->levelRays[l] += hs[kStatLevelRays + l];
         fs->levelShadowRays[l] += hs[kStatLevelShadows + l];
@@ -614,6 +621,8 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs.shadowNodeRecords += prev.shadowNodeRecords;
                     fs.shadowTriTests += prev.shadowTriTests;
                     fs.maxNodeRecordsPerRay = std::max(fs.maxNodeRecordsPerRay, prev.maxNodeRecordsPerRay);
+                    fs.shadedVertices += prev.shadedVertices;
+                    fs.shadeLaunches += prev.shadeLaunches;
                     fs.traceMs += prev.traceMs;
                     fs.shadowMs += prev.shadowMs;
                     fs.shadeMs += prev.shadeMs;

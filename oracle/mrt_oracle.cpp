@@ -1063,6 +1063,19 @@ struct Engine {
     std::vector<float> shaderTable, samplerTable;
     std::atomic<uint64_t> rays{0};
     int64_t numTriangles = 0;
+    // Timing-faithful mode (bench.py cpu_baseline): draws come from the
+    // reference's shared atomic cursors instead of the deterministic index - the hemisphere's
+    // (Shader.cpp:189-194, two per call) and the light index's (:224-227) static cursors, and the
+    // per-instance cursors of the StaticHaltonSeq samplers (Sampler.hpp:58-63): the pixel sampler,
+    // the PathTracer's Russian roulette, one per area light.  Results then depend on thread
+    // scheduling, as the reference's do.
+    bool faithful = false;
+    mutable std::atomic<uint32_t> curHemi{0}, curLight{0}, curPixel{0}, curRR{0};
+    mutable std::vector<std::atomic<uint32_t>> curArea = std::vector<std::atomic<uint32_t>>(64);
+    uint32_t draw(uint32_t key, uint32_t tc, uint32_t purpose, std::atomic<uint32_t>& cursor) const {
+        if (!faithful) return sampleIndex(key, tc, purpose);
+        return cursor.fetch_add(1, std::memory_order_relaxed) & ArrayMask;
+    }
 
     struct Ctx {
         uint32_t key;
@@ -1134,8 +1147,8 @@ struct Engine {
     }
 
     Vec3 cosineSampleHemisphere(const Vec3& normal, Ctx ctx, uint32_t tc) const {  // Shader.cpp:188-216
-        const float uniformRandom1 = shaderTable[sampleIndex(ctx.key, tc, P_HEMI1)];
-        const float uniformRandom2 = shaderTable[sampleIndex(ctx.key, tc, P_HEMI2)];
+        const float uniformRandom1 = shaderTable[draw(ctx.key, tc, P_HEMI1, curHemi)];
+        const float uniformRandom2 = shaderTable[draw(ctx.key, tc, P_HEMI2, curHemi)];
         float cosPhi, sinPhi;
         hemisphereTrig(uniformRandom1, &cosPhi, &sinPhi);  // std::cos(phi), std::sin(phi), phi = 2 pi r1
         const float r2 = uniformRandom2;
@@ -1148,15 +1161,16 @@ struct Engine {
     }
 
     uint32_t lightIndex(Ctx ctx, uint32_t tc, int i) const {  // Shader.cpp:223-233
-        const float randomNumber = shaderTable[sampleIndex(ctx.key, tc, P_LIGHT + 3u * static_cast<uint32_t>(i))];
+        const float randomNumber = shaderTable[draw(ctx.key, tc, P_LIGHT + 3u * static_cast<uint32_t>(i), curLight)];
         const uint32_t sizeLights = static_cast<uint32_t>(lights.size());
         return static_cast<uint32_t>(std::floor(randomNumber * sizeLights * 0.99999F));
     }
 
     Vec3 lightPosition(const Light& l, Ctx ctx, uint32_t tc, int i) const {  // AreaLight.cpp:17-26
         if (!l.area) return l.position;
-        float r = samplerTable[sampleIndex(ctx.key, tc, P_LIGHT + 3u * static_cast<uint32_t>(i) + 1u)];
-        float s = samplerTable[sampleIndex(ctx.key, tc, P_LIGHT + 3u * static_cast<uint32_t>(i) + 2u)];
+        std::atomic<uint32_t>& cur = curArea[static_cast<size_t>(l.index) & 63u];
+        float r = samplerTable[draw(ctx.key, tc, P_LIGHT + 3u * static_cast<uint32_t>(i) + 1u, cur)];
+        float s = samplerTable[draw(ctx.key, tc, P_LIGHT + 3u * static_cast<uint32_t>(i) + 2u, cur)];
         if (r + s >= 1.0F) {
             r = 1.0F - r;
             s = 1.0F - s;
@@ -1266,7 +1280,7 @@ struct Engine {
                 Ld *= kD;
                 Ld /= static_cast<float>(cfg.samplesLight);
             }
-            if (rayDepth <= RayDepthMin || samplerTable[sampleIndex(ctx.key, tc, P_RUSSIAN)] > 0.5F) {
+            if (rayDepth <= RayDepthMin || samplerTable[draw(ctx.key, tc, P_RUSSIAN, curRR)] > 0.5F) {
                 const Vec3 newDirection = cosineSampleHemisphere(n, ctx, tc);
                 Ray secondary(newDirection, it.point, rayDepth + 1, false, it.primitive, &rays);
                 Vec3 LiD_RGB;
@@ -1322,8 +1336,8 @@ struct Engine {
         const uint32_t key = pathKey(static_cast<uint32_t>(y * W + x), static_cast<uint32_t>(sample));
         float r1 = 0.5F, r2 = 0.5F;  // Constant(0.5) unless spp > 1 (C_wrapper.cpp:144-148)
         if (cfg.samplesPixel > 1) {
-            r1 = samplerTable[sampleIndex(key, 0u, P_JITTER_U)];
-            r2 = samplerTable[sampleIndex(key, 0u, P_JITTER_V)];
+            r1 = samplerTable[draw(key, 0u, P_JITTER_U, curPixel)];
+            r2 = samplerTable[draw(key, 0u, P_JITTER_V, curPixel)];
         }
         const float u = x * invImgWidth, v = y * invImgHeight;
         const float deviationU = (r1 - 0.5F) * 2.0F * pixelWidth;
@@ -1438,6 +1452,9 @@ void* oracle_create(const OracleConfig* c) {
 }
 
 void oracle_destroy(void* h) { delete static_cast<oracle::Engine*>(h); }
+
+// timing-faithful sample draws (shared atomic cursors, as the reference): 1 on, 0 off
+void oracle_set_faithful(void* h, int on) { static_cast<oracle::Engine*>(h)->faithful = on != 0; }
 
 int oracle_num_tiles(void* h) { return static_cast<int>(static_cast<oracle::Engine*>(h)->tiles().size()); }
 

@@ -39,6 +39,7 @@ def lib():
         L.oracle_create.restype = vp
         L.oracle_create.argtypes = [P(_Cfg)]
         L.oracle_destroy.argtypes = [vp]
+        L.oracle_set_faithful.argtypes = [vp, ctypes.c_int]
         L.oracle_num_tiles.argtypes = [vp]
         L.oracle_render.restype = ctypes.c_uint64
         L.oracle_render.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -190,6 +191,11 @@ class Oracle:
         self._h = lib().oracle_create(ctypes.byref(c))
         if not self._h:
             raise RuntimeError("oracle could not load the scene")
+
+    def set_faithful(self, on=True):
+        """Timing-faithful draws: the reference's shared atomic sampler cursors (results then
+        depend on thread scheduling, as the reference's do)."""
+        lib().oracle_set_faithful(self._h, int(on))
 
     def num_tiles(self):
         return lib().oracle_num_tiles(self._h)

@@ -1,39 +1,48 @@
-"""Summarise rocprofv3 --pmc CSVs (FETCH_SIZE / WRITE_SIZE passes) for the trace kernel.
+"""Summarise rocprofv3 --pmc CSVs of tools/pmc_run.sh into bytes beyond L2 per launch per kernel.
 
-usage: python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
+usage: python tools/pmc_summary.py <pmc_run output dir> <out.json>
 
-FETCH_SIZE / WRITE_SIZE are in KiB.  Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section) FETCH_SIZE
-on gfx950 reads exactly half of the bytes of a wide (16 B/lane) coalesced stream, so the read side
-is doubled; the trace kernel's loads are 16-byte (float4) gathers, the regime the correction was
-measured in.  Both counters count memory-side (L2 -> fabric) traffic: Infinity-Cache hits are
-included, so this is "bytes beyond L2", an upper bound on HBM bytes.
+FETCH_SIZE / WRITE_SIZE are in KiB.  Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section)
+FETCH_SIZE on gfx950 reads exactly half of the bytes of a wide (16 B/lane) stream, so the read
+side is doubled; the kernels' loads are 12- and 16-byte gathers, near that regime.  Both
+counters count memory-side (L2 -> fabric) traffic: Infinity-Cache hits are included, so this is
+"bytes beyond L2", an upper bound on HBM bytes.  Other counters of the run (TCC hit rate, SQ and
+TA / TD busy) are averaged per kernel as they are.
 """
-import csv, json, sys
+import csv, glob, json, os, re, sys
 from collections import defaultdict
 
-def load(path, counter):
-    per = defaultdict(list)
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if row.get("Counter_Name") != counter:
-                continue
-            per[row["Kernel_Name"]].append(float(row["Counter_Value"]))
-    return per
+PRODUCT = {"k_trace": r"k_trace<false, 1, 1>", "k_shadow": r"k_shadow<false, 1, 1>", "k_shade": r"k_shade<2>"}
 
-fetch = load(sys.argv[1], "FETCH_SIZE")
-write = load(sys.argv[2], "WRITE_SIZE")
-out = {"kernels": {}}
-for k in sorted(set(fetch) | set(write)):
-    f = fetch.get(k, []); w = write.get(k, [])
-    if not f:
-        continue
-    fk = sum(f) / len(f); wk = (sum(w) / len(w)) if w else 0.0
-    out["kernels"][k] = {"launches": len(f), "fetch_kib_avg": fk, "write_kib_avg": wk,
-                         "hbm_bytes_per_launch": (2.0 * fk + wk) * 1024.0}
-trace = [k for k in out["kernels"] if "k_trace<false" in k]
-if trace:
-    out["trace_kernel"] = trace[0]
-    out["hbm_bytes_per_launch"] = out["kernels"][trace[0]]["hbm_bytes_per_launch"]
-out["note"] = "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes; includes Infinity-Cache hits"
-json.dump(out, open(sys.argv[3], "w"), indent=1)
-print(json.dumps({k: v for k, v in out.items() if k != "kernels"}))
+
+def rows(d):
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            yield from csv.DictReader(f)
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values (one per dispatch)
+    for row in rows(src):
+        per[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    out = {"bytes_beyond_l2_per_launch": {}, "counters": {}, "kernels": {},
+           "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, averaged over the dispatches of "
+                   "the profiled command; includes Infinity-Cache hits"}
+    for short, pat in PRODUCT.items():
+        names = [k for k in per if pat in k]
+        if not names:
+            continue
+        c = per[names[0]]
+        avg = {k: sum(v) / len(v) for k, v in c.items() if v}
+        out["counters"][short] = avg
+        out["kernels"][short] = names[0]
+        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+            out["bytes_beyond_l2_per_launch"][short] = (2.0 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
+        if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
+            out["counters"][short]["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out["bytes_beyond_l2_per_launch"]))
+
+
+main()
