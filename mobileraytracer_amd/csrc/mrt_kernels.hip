@@ -572,15 +572,15 @@ __global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int
         float hitLight = 0.0F;
         if (kind != kMiss) {  // Shader.cpp:122: shade only on a hit
             v3 Le, Kd{0, 0, 0}, Ks{0, 0, 0}, Kt{0, 0, 0};
-            if (kind == kLight) {
-                Le = xyz(s.lights[4 * primIndex(code) + 3]);  // Light::radiance_
-            } else {
-                const float4* m = s.mats + 4 * hitMaterial(s, code);
+            {
+                // a light hit carries the light's own material (Light::radiance_, AreaLight.cpp:32-41)
+                const int mi = kind == kLight ? __float_as_int(s.lights[4 * primIndex(code) + 3].w) : hitMaterial(s, code);
+                const float4* m = s.mats + 4 * mi;
                 Le = xyz(m[0]);
                 Kd = xyz(m[1]);
                 Ks = xyz(m[2]);
                 Kt = xyz(m[3]);
-                if (s.textured != 0) {
+                if (s.textured != 0 && kind != kLight) {
                     const float4 kw = textureWrite(s, h);
                     if (kw.w >= 0.0F) Kd = xyz(kw);
                 }

@@ -300,11 +300,16 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
             v.push_back(make_float4(0, 0, 0, 0));
             v.push_back(make_float4(0, 0, 0, 0));
         }
-        v.push_back(f4(l.radiance.Le, 0.0F));
+        // w: the index of the light's own material (Light::radiance_, appended after the scene's):
+        // a hit on an area light carries that material (AreaLight.cpp:32-41), whose Kd / Ks / Kt
+        // DiffuseMaterial reads (DiffuseMaterial.cpp:12-28)
+        v.push_back(f4(l.radiance.Le, asFloat(static_cast<int32_t>(sc.materials.size() + (&l - sc.lights.data())))));
     }
     d.lights = r->sceneMem.upload(v, st);
     v.clear();
-    for (const HMaterial& m : sc.materials) {
+    std::vector<HMaterial> allMats = sc.materials;
+    for (const HLight& l : sc.lights) allMats.push_back(l.radiance);
+    for (const HMaterial& m : allMats) {
         v.push_back(f4(m.Le, m.ior));
         v.push_back(f4(m.Kd, asFloat(m.texId)));  // w: texture index (-1 none)
         v.push_back(f4(m.Ks, 0.0F));

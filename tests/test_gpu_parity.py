@@ -137,6 +137,9 @@ def test_whitted_bit_exact(oracle_mod, case):
     dict(width=96, height=96, scene="conference", shader=3),
     dict(width=128, height=128, scene="teapot", shader=4),           # DiffuseMaterial: the texel
     dict(width=128, height=128, scene="teapot", shader=0),           # NoShadows with texel Kd
+    dict(width=128, height=128, scene="water", shader=4),            # DiffuseMaterial: a light hit shows the light's Kd
+    dict(width=128, height=128, sceneIndex=2, shader=4),             # ... and the built-in area lights'
+    dict(width=128, height=128, scene="water", shader=0, spl=2),     # NoShadows: light hits
     dict(width=100, height=60, sceneIndex=3, shader=2, spp=2),       # PathTracer: tolerance below
 ])
 def test_other_scenes_and_shaders(oracle_mod, case):
