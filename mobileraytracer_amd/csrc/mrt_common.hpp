@@ -119,20 +119,21 @@ MRT_HD uint32_t pathKey(uint32_t pixelIndex, uint32_t globalSample) {
     return hash32(pixelIndex * 0x9E3779B9u ^ hash32(globalSample + 0x632BE5ABu));
 }
 // treeCode: 1 for the camera ray's vertex; child = code * 4 + slot (slot 1 diffuse,
-// 2 specular, 3 transmission).  purpose: one of the kP* constants below.  The draws of one
-// vertex are CONSECUTIVE table entries from a hashed start, as the reference's sampler
-// cursors hand out consecutive entries (Sampler.hpp:58-63, Shader.cpp:189-194); on the GPU
-// this keeps a vertex's draws in one or two cache lines per table.
+// 2 specular, 3 transmission); 0 for the pixel sampler.  purpose: one of the kP* constants
+// below.  The draws of one vertex are CONSECUTIVE table entries from a hashed start aligned to
+// 8 entries, as the reference's sampler cursors hand out consecutive entries (Sampler.hpp:58-63,
+// Shader.cpp:189-194); on the GPU every draw of a vertex (samplesLight 1) then comes from ONE
+// 128-byte line of the interleaved table.
 MRT_HD uint32_t sampleIndex(uint32_t key, uint32_t treeCode, uint32_t purpose) {
-    return (hash32(key ^ hash32(treeCode * 0x9E3779B9u + 0x7F4A7C15u)) + purpose) & kArrayMask;
+    return ((hash32(key ^ hash32(treeCode * 0x9E3779B9u + 0x7F4A7C15u)) & ~7u) + purpose) & kArrayMask;
 }
 // purposes
-constexpr uint32_t kPJitterU = 0;   // pixel sampler, r1   (Renderer.cpp:137)
-constexpr uint32_t kPJitterV = 1;   // pixel sampler, r2   (Renderer.cpp:138)
-constexpr uint32_t kPRussian = 2;   // PathTracer RR       (PathTracer.cpp:89)
-constexpr uint32_t kPHemi1 = 3;     // hemisphere r1       (Shader.cpp:190)
-constexpr uint32_t kPHemi2 = 4;     // hemisphere r2       (Shader.cpp:191)
-constexpr uint32_t kPLightBase = 8; // + 3*i + {0 pick, 1 r, 2 s} for light sample i
+constexpr uint32_t kPJitterU = 0;   // pixel sampler, r1   (Renderer.cpp:137), tree code 0
+constexpr uint32_t kPJitterV = 1;   // pixel sampler, r2   (Renderer.cpp:138), tree code 0
+constexpr uint32_t kPRussian = 0;   // PathTracer RR       (PathTracer.cpp:89)
+constexpr uint32_t kPHemi1 = 1;     // hemisphere r1       (Shader.cpp:190)
+constexpr uint32_t kPHemi2 = 2;     // hemisphere r2       (Shader.cpp:191)
+constexpr uint32_t kPLightBase = 3; // + 3*i + {0 pick, 1 r, 2 s} for light sample i
 MRT_HD uint32_t purposeLightPick(int i) { return kPLightBase + 3u * static_cast<uint32_t>(i); }
 MRT_HD uint32_t purposeLightR(int i) { return kPLightBase + 3u * static_cast<uint32_t>(i) + 1u; }
 MRT_HD uint32_t purposeLightS(int i) { return kPLightBase + 3u * static_cast<uint32_t>(i) + 2u; }

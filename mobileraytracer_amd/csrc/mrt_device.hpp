@@ -29,9 +29,9 @@ struct DScene {
     const GNode* sphereNodes;
     const float4* lights;      // 4 per light: A or position (w = kind bits), AB, AC, Le
     const float4* mats;        // 4 per material: Le (w = ior), Kd, Ks, Kt
-    const float2* tables;  // 2^20 x {shader (Shader.cpp:23), sampler (StaticHaltonSeq.cpp)}
-                           // shuffled Halton values
-    const float2* trig;    // 2^20 x {cos, sin} of 2 pi * shader entry (libm, fillHemisphereTrig)
+    // 2^20 x {shader (Shader.cpp:23), sampler (StaticHaltonSeq.cpp) shuffled Halton values,
+    // cos and sin of 2 pi * shader entry by the host libm (fillHemisphereTrig)}
+    const float4* tables;
     GRoot triRoot, planeRoot, sphereRoot;
     int32_t nLights;
     int32_t nMats;

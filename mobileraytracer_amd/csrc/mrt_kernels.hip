@@ -412,9 +412,9 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     const float lr0 = s.tables[sampleIndex(v.key, tc, purposeLightR(0))].y;
     const float lq0 = s.tables[sampleIndex(v.key, tc, purposeLightS(0))].y;
     const float rr = s.tables[sampleIndex(v.key, tc, kPRussian)].y;
-    const float2 hemi1 = s.trig[sampleIndex(v.key, tc, kPHemi1)];  // cos, sin of 2 pi r1
-    v.hcos = hemi1.x;
-    v.hsin = hemi1.y;
+    const float4 hemi1 = s.tables[sampleIndex(v.key, tc, kPHemi1)];  // .zw: cos, sin of 2 pi r1
+    v.hcos = hemi1.z;
+    v.hsin = hemi1.w;
     v.hemi2 = s.tables[sampleIndex(v.key, tc, kPHemi2)].x;
     const uint32_t code = fbits(h.w);
     const uint32_t kind = primKind(code);

@@ -79,7 +79,7 @@ struct PixelMap {
 struct RaygenArgs {
     GCamera cam;
     PixelMap map;
-    const float2* tables;  // .y: the sampler table
+    const float4* tables;  // .y: the sampler table
     int width, height;
     int slotBase;    // first pixel slot of this chunk
     int nPaths;      // slots in chunk * spp

@@ -338,20 +338,15 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
             if (!std::isfinite(c.x) || !std::isfinite(c.y) || !std::isfinite(c.z)) d.matsFinite = 0;
     }
 
-    // the two sample tables interleaved: one vertex's draws (consecutive indices, both
-    // tables) share one or two cache lines
-    std::vector<float> shaderT, samplerT, both;
+    // the sample tables interleaved with the hemisphere's cos / sin: one vertex's draws
+    // (consecutive indices from an 8-aligned start) are one 128-byte line
+    std::vector<float> shaderT, samplerT, trig;
     fillHaltonTable(&shaderT, kSeedShaderTable);
     fillHaltonTable(&samplerT, kSeedSamplerTable);
-    both.resize(2 * shaderT.size());
-    for (size_t k = 0; k < shaderT.size(); ++k) {
-        both[2 * k] = shaderT[k];
-        both[2 * k + 1] = samplerT[k];
-    }
-    d.tables = reinterpret_cast<const float2*>(r->sceneMem.upload(both, st));
-    std::vector<float> trig;
     fillHemisphereTrig(shaderT, &trig);
-    d.trig = reinterpret_cast<const float2*>(r->sceneMem.upload(trig, st));
+    std::vector<float4> tab(shaderT.size());
+    for (size_t k = 0; k < shaderT.size(); ++k) tab[k] = make_float4(shaderT[k], samplerT[k], trig[2 * k], trig[2 * k + 1]);
+    d.tables = r->sceneMem.upload(tab, st);
     MRT_HIP(hipStreamSynchronize(st));
 }
 

@@ -136,9 +136,10 @@ uint32_t pathKey(uint32_t pixelIndex, uint32_t globalSample) {
     return hash32(pixelIndex * 0x9E3779B9u ^ hash32(globalSample + 0x632BE5ABu));
 }
 uint32_t sampleIndex(uint32_t key, uint32_t treeCode, uint32_t purpose) {
-    return (hash32(key ^ hash32(treeCode * 0x9E3779B9u + 0x7F4A7C15u)) + purpose) & ArrayMask;
+    // a vertex's draws: consecutive entries from a hashed start aligned to 8 entries
+    return ((hash32(key ^ hash32(treeCode * 0x9E3779B9u + 0x7F4A7C15u)) & ~7u) + purpose) & ArrayMask;
 }
-enum Purpose : uint32_t { P_JITTER_U = 0, P_JITTER_V = 1, P_RUSSIAN = 2, P_HEMI1 = 3, P_HEMI2 = 4, P_LIGHT = 8 };
+enum Purpose : uint32_t { P_JITTER_U = 0, P_JITTER_V = 1, P_RUSSIAN = 0, P_HEMI1 = 1, P_HEMI2 = 2, P_LIGHT = 3 };
 
 float haltonSequence(uint32_t index, uint32_t base) {  // Utils.cpp:43-53
     float fraction = 1.0F;
