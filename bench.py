@@ -294,6 +294,11 @@ def main():
             "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
             "per_ray": per_ray,
             "peak_source": "MI355X_MICROARCH.md: L2 34.5 TB/s aggregate, 36.9 TB/s with L1 reuse",
+            # measured on MI355X by tools/gather_ceiling.hip (profiles/r02_gather_ceiling.jsonl): dependent
+            # 64-byte record chains from a 32 MiB table, every lane at a different record vs every lane of
+            # a wave at the same one; the walk's rays sit between the two (coherent camera rays, scattered
+            # bounces)
+            "measured_ceilings_gbs": {"divergent_64B_records_32MiB": 6648.4, "wave_coherent_64B_records_32MiB": 27859.6},
             "durations": "serialised frames (shadow stream off), HIP events on the render stream",
             "kernels": kernels,
         },
