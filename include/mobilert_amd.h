@@ -140,6 +140,16 @@ int mrt_primary_hits(mrt_renderer *r, int32_t *kind, int32_t *index, float *t);
  * (min xyz, max xyz), offsets[N] / counts[N] (BVHNode::indexOffset / numPrimitives) and
  * order[triangles] (input index of each triangle in BVH order). */
 int64_t mrt_triangle_bvh(const mrt_config *cfg, float *boxes, int32_t *offsets, int32_t *counts, int32_t *order);
+/* Host only: the RegularGrid accelerator's build (RegularGrid.hpp:112-289, gridSize 32) for one
+ * primitive kind of the scene cfg names (kind 0 planes, 1 spheres, 2 triangles).  Returns the
+ * total list length L or -1; with non-NULL outputs fills world[12] (min xyz, max xyz, cellSize
+ * xyz, cellSizeInverted xyz), start[32768 + 1] (cell c's list is items[start[c], start[c+1]),
+ * cell c = x + 32 y + 1024 z) and items[L] (input index of each listed primitive). */
+int64_t mrt_regular_grid(const mrt_config *cfg, int32_t kind, float *world, int32_t *start, int32_t *items);
+/* Host only: the membership test of a grid cell (Triangle::intersect(const AABB&),
+ * Triangle.cpp:142-229; Plane.cpp:146-155; Sphere.cpp:102-123).  kind 0: prim = A, B, C xyz;
+ * 1: point xyz, normal xyz; 2: center xyz, radius.  box = min xyz, max xyz.  1 / 0, or -1. */
+int mrt_grid_box_test(int32_t kind, const float *prim, const float *box);
 /* Host only: decode a map_Kd texture file as the renderer does (Texture::createTexture,
  * Texture.cpp:83-114: 8-bit channels with stb_image's conventions).  Returns the byte count
  * width*height*channels (and fills dims[3] = width, height, channels) or -1; with non-NULL

@@ -114,8 +114,9 @@ class Renderer:
         _native.check(self._lib.mrt_set_profiling(self._h, int(timing) | (2 * int(counting))))
 
     def set_tuning(self, key: int, value: int) -> None:
-        """A/B knobs (identical results): 1 = trace walk (0 reference, 1 default), 2 = t-culling,
-        3 = shadow rays on their own stream."""
+        """A/B knobs (identical results): 1 = trace walk (0 reference, 1 default), 2 = t-cull mode
+        (0 none, 1 fast, 2 certified), 3 = shadow rays on their own stream, 4 = binned emission
+        of child / shadow rays, 7 = no walk for the depth-capped last level."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 
     def get_tuning(self, key: int) -> int:
@@ -186,6 +187,33 @@ def triangle_bvh(config: Config):
     if n2 != n:
         raise RuntimeError(lib.mrt_last_error().decode())
     return boxes, off, cnt, order[:int(cnt[0])] if n == 1 else order
+
+
+def regular_grid(config: Config, kind: int):
+    """Host-side RegularGrid (accelerator 2, RegularGrid.hpp with gridSize 32) of one primitive
+    kind of the configured scene (0 planes, 1 spheres, 2 triangles), no GPU: world (12 floats:
+    min, max, cellSize, cellSizeInverted), start (32^3 + 1), items (input indices)."""
+    lib = _native.lib()
+    c = config.to_c()
+    n = lib.mrt_regular_grid(ctypes.byref(c), kind, None, None, None)
+    if n < 0:
+        raise RuntimeError(lib.mrt_last_error().decode())
+    world, start, items = np.empty(12, np.float32), np.empty(32 ** 3 + 1, np.int32), np.empty(max(n, 1), np.int32)
+    if lib.mrt_regular_grid(ctypes.byref(c), kind, _ptr(world), _ptr(start), _ptr(items)) != n:
+        raise RuntimeError(lib.mrt_last_error().decode())
+    return world, start, items[:n]
+
+
+def grid_box_test(kind: int, prim, box) -> bool:
+    """The RegularGrid fill's cell membership test (Triangle / Plane / Sphere::intersect(const
+    AABB&)) as the renderer's host build evaluates it.  kind 0 prim = A + B + C, 1 = point +
+    normal, 2 = center + (radius,); box = min + max."""
+    p = np.ascontiguousarray(prim, np.float32)
+    b = np.ascontiguousarray(box, np.float32)
+    rc = _native.lib().mrt_grid_box_test(kind, _ptr(p), _ptr(b))
+    if rc < 0:
+        raise ValueError(_native.lib().mrt_last_error().decode())
+    return bool(rc)
 
 
 def decode_texture(path: str) -> np.ndarray:

@@ -17,7 +17,7 @@ EXPORTED_SYMBOLS = (
     "mrt_unpack_gathered", "mrt_stop_render", "mrt_get_sample", "mrt_get_total_casted_rays",
     "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits", "mrt_set_tuning",
     "mrt_get_tuning", "mrt_triangle_bvh", "mrt_decode_texture", "mrt_kat_slab", "mrt_kat_triangle",
-    "mrt_trace_rays", "mrt_sample_tables",
+    "mrt_trace_rays", "mrt_sample_tables", "mrt_regular_grid", "mrt_grid_box_test",
     "RayTrace", "stopRender",
 )
 
@@ -96,6 +96,8 @@ def load_library(path=LIB_PATH):
         "mrt_get_tuning": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
         "mrt_triangle_bvh": (ctypes.c_int64, [vp, vp, vp, vp, vp]),
         "mrt_decode_texture": (ctypes.c_int64, [ctypes.c_char_p, vp, vp]),
+        "mrt_regular_grid": (ctypes.c_int64, [vp, ctypes.c_int32, vp, vp, vp]),
+        "mrt_grid_box_test": (ctypes.c_int, [ctypes.c_int32, vp, vp]),
         "mrt_sample_tables": (ctypes.c_int, [vp, vp, vp]),
         "mrt_kat_slab": (ctypes.c_int, [vp, vp, vp, ctypes.c_int32, vp]),
         "mrt_kat_triangle": (ctypes.c_int, [vp, vp, vp, ctypes.c_int32, vp, vp]),

@@ -193,6 +193,27 @@ struct GRoot {
     int32_t count;   // number of primitives (0 => empty BVH, BVH.hpp:328-330)
 };
 
+// x86 cvttss2si, the reference's float -> int32 conversion (static_cast<int32_t>): truncation,
+// and INT32_MIN for NaN and out-of-range values (where the GPU's v_cvt_i32_f32 saturates)
+MRT_HD int32_t x86Trunc(float f) {
+    return (f >= -2147483648.0F && f < 2147483648.0F) ? static_cast<int32_t>(f) : static_cast<int32_t>(0x80000000u);
+}
+
+// RegularGrid<T> (RegularGrid.hpp) with gridSize 32 (Shader.cpp:57): one per primitive kind.
+// Cell (x, y, z) is x + (y << 5) + (z << 10) (getCellIndex, gridShift 5); its primitives are
+// items[start[c] .. start[c + 1]) (BVH-order indices, ascending input order; mrt_grid.cpp).
+constexpr int kGridSize = 32;
+constexpr int kGridShift = 5;  // bitCounter(gridSize - 1), RegularGrid.hpp:123,173-180
+constexpr int kGridCells = kGridSize * kGridSize * kGridSize;
+struct GGrid {
+    float mn[3];   // worldBoundaries_ min (Scene::getBounds, Epsilon-widened)
+    float cs[3];   // cellSize_
+    float csi[3];  // cellSizeInverted_
+    int32_t count; // primitives of this kind (0: the walk tests nothing)
+    const int32_t* start;
+    const int32_t* items;
+};
+
 // Camera parameters (Camera.cpp:14-19, Perspective.cpp:8-14)
 struct GCamera {
     v3 position, direction, right, up;

@@ -44,12 +44,13 @@ struct DScene {
     const int4* texInfo;       // per texture: width, height, channels, first byte in texels
     const uint8_t* texels;
     int32_t textured;
-    // Config::accelerator (Shader.hpp:20-24): 1 Naive, 2 RegularGrid (served by the BVH), 3 BVH,
-    // anything else builds no accelerator (only lights are hit, Shader.cpp:86-111)
+    // Config::accelerator (Shader.hpp:20-24): 1 Naive, 2 RegularGrid, 3 BVH, anything else
+    // builds no accelerator (only lights are hit, Shader.cpp:86-111)
     int32_t accel;
     const int* triNaive;       // Naive: BVH-order index of the i-th triangle / plane / sphere of the input
     const int* planeNaive;
     const int* sphereNaive;
+    GGrid planeGrid, sphereGrid, triGrid;  // RegularGrid (accelerator 2 only)
 };
 
 __device__ __forceinline__ float4 ld4(const float4* p) { return *p; }
@@ -278,6 +279,76 @@ __device__ __forceinline__ bool naiveWalk(const DScene& s, v3 o, v3 d, uint32_t 
         if (leafSpheres<kAny, false>(s, s.sphereNaive[i], 1, o, d, b)) return true;
     for (int i = 0; i < s.triRoot.count; ++i)
         if (leafTriangles<kAny, false>(s, s.triNaive[i], 1, o, d, src, b, &nTri)) return true;
+    return false;
+}
+
+// RegularGrid<T>::intersect (RegularGrid.hpp:333-515): the 3D-DDA from the origin's (clamped)
+// cell.  Every primitive of a visited cell is tested in list order with the plain `t >= best`
+// rejection (ties: the first tested wins; a primitive listed in several cells is re-tested with
+// the same result).  Shadow rays return at the first primitive closer than their distance.  A
+// closest-hit walk stops at the grid's edge or, once THIS kind has improved the hit (the jump to
+// `testloop`), at the first cell boundary beyond the hit.  Every step moves one axis toward its
+// exit, so at most 3 x kGridSize cells are visited.
+template <int kKind, bool kAny>
+__device__ __forceinline__ bool gridWalk(const DScene& s, const GGrid& g, v3 o, v3 d, uint32_t src, Best* b) {
+    if (g.count == 0) return false;  // no primitive of this kind: nothing is ever tested
+    const v3 mn{g.mn[0], g.mn[1], g.mn[2]}, cs{g.cs[0], g.cs[1], g.cs[2]};
+    // RegularGrid.hpp:337-347
+    int c[3];
+    const float cf[3] = {(o.x - mn.x) * g.csi[0], (o.y - mn.y) * g.csi[1], (o.z - mn.z) * g.csi[2]};
+    int step[3], out[3];
+    float tmax[3], tdelta[3] = {0.0F, 0.0F, 0.0F};
+    const float dir[3] = {d.x, d.y, d.z}, org[3] = {o.x, o.y, o.z}, mnA[3] = {mn.x, mn.y, mn.z}, csA[3] = {cs.x, cs.y, cs.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        int ci = x86Trunc(cf[a]);
+        ci = min(ci, kGridSize - 1);
+        ci = max(ci, 0);
+        c[a] = ci;
+        float cb;  // RegularGrid.hpp:353-381
+        if (dir[a] > 0) {
+            step[a] = 1;
+            out[a] = kGridSize;
+            cb = mnA[a] + (static_cast<float>(ci) + 1.0F) * csA[a];
+        } else {
+            step[a] = -1;
+            out[a] = -1;
+            cb = mnA[a] + static_cast<float>(ci) * csA[a];
+        }
+        if (fabsf(dir[a]) > 1.19209290e-07F) {  // numeric_limits<float>::epsilon(), :384-406
+            const float r = 1.0F / dir[a];
+            tmax[a] = (cb - org[a]) * r;
+            tdelta[a] = csA[a] * static_cast<float>(step[a]) * r;
+        } else {
+            tmax[a] = kRayLengthMax;
+        }
+    }
+    bool improved = false;  // this kind has found a closer hit (the reference's jump to testloop)
+    for (int iter = 0; iter <= 3 * kGridSize; ++iter) {
+        const int cell = c[0] + (c[1] << kGridShift) + (c[2] << (2 * kGridShift));
+        const int e = g.start[cell + 1];
+        uint32_t nTri = 0;
+        for (int k = g.start[cell]; k < e; ++k) {
+            const int j = g.items[k];
+            const float before = b->t;
+            bool any = false;
+            if (kKind == kTriangle) any = leafTriangles<kAny, false>(s, j, 1, o, d, src, b, &nTri);
+            if (kKind == kPlane) any = leafPlanes<kAny, false>(s, j, 1, o, d, src, b);
+            if (kKind == kSphere) any = leafSpheres<kAny, false>(s, j, 1, o, d, b);
+            if (kAny && any) return true;
+            improved = improved || b->t < before;
+        }
+        // RegularGrid.hpp:429-457 / 472-512
+        const int a = tmax[0] < tmax[1] ? (tmax[0] < tmax[2] ? 0 : 2) : (tmax[1] < tmax[2] ? 1 : 2);
+        const float tm = a == 0 ? tmax[0] : (a == 1 ? tmax[1] : tmax[2]);
+        if (improved && b->t < tm) break;
+        c[a] += step[a];
+        if (c[a] == out[a]) break;
+        const float td = a == 0 ? tdelta[0] : (a == 1 ? tdelta[1] : tdelta[2]);
+        if (a == 0) tmax[0] = tm + td;
+        else if (a == 1) tmax[1] = tm + td;
+        else tmax[2] = tm + td;
+    }
     return false;
 }
 

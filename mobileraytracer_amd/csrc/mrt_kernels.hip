@@ -86,6 +86,97 @@ __device__ __forceinline__ void blockAllocPair(unsigned long long* pair, int nLo
     *baseHi = static_cast<int>(static_cast<unsigned>(e >> 32));
 }
 
+// Binned form of blockAllocPair: the block's slots stay ONE contiguous range per counter (one
+// 64-bit atomic per block), laid out bin-major, so rays with equal keys land next to each other
+// and a wave of the next launch walks rays of one direction octant from one patch of parents
+// (the north_star "sorting with ballot / prefix-sum", staged per block).
+//   lo: nLo in [0, 3] slots under key keyLo; hi: nHi in [0, 2^hiBits) slots under key keyHi;
+//   keys in [0, kEmitBins).  A lane's rank inside its (wave, bin) is a sum of ballot popcounts
+//   over the bits of its count; wave 0 scans the (bin, wave) totals.
+// lds: 2 x (2 * kWaves * kEmitBins + 2) ints, alternated by parity.
+__device__ __forceinline__ void blockAllocBinned(unsigned long long* pair, int nLo, int keyLo, int nHi, int keyHi,
+                                                 int hiBits, int* baseLo, int* baseHi, int* lds, int parity) {
+    constexpr int kWaves = kBlock / 64;
+    constexpr int kB = kEmitBins;
+    const int lane = laneId();
+    const int wave = static_cast<int>(threadIdx.x >> 6);
+    const uint64_t below = (1ull << lane) - 1ull;
+    int rankLo = 0, rankHi = 0, totLo = 0, totHi = 0;
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        const bool inLo = keyLo == b, inHi = keyHi == b;
+        const uint64_t l0 = __ballot(inLo && (nLo & 1) != 0);
+        const uint64_t l1 = __ballot(inLo && (nLo & 2) != 0);
+        const int rl = __popcll(l0 & below) + 2 * __popcll(l1 & below);
+        const int tl = __popcll(l0) + 2 * __popcll(l1);
+        int rh = 0, th = 0;
+        for (int k = 0; k < hiBits; ++k) {
+            const uint64_t m = __ballot(inHi && ((nHi >> k) & 1) != 0);
+            rh += __popcll(m & below) << k;
+            th += __popcll(m) << k;
+        }
+        if (inLo) rankLo = rl;
+        if (inHi) rankHi = rh;
+        if (lane == b) {
+            totLo = tl;
+            totHi = th;
+        }
+    }
+    int* buf = lds + parity * (2 * kWaves * kB + 2);
+    int* cLo = buf;                 // [wave][bin] -> count, then the exclusive offset in the block
+    int* cHi = buf + kWaves * kB;
+    if (lane < kB) {
+        cLo[wave * kB + lane] = totLo;
+        cHi[wave * kB + lane] = totHi;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // lane b < kB: bin b's total over the waves, scanned over the bins
+        unsigned long long v = 0;
+        int pl[kWaves], ph[kWaves];
+        if (lane < kB) {
+            int sl = 0, sh = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                pl[w] = sl;
+                ph[w] = sh;
+                sl += cLo[w * kB + lane];
+                sh += cHi[w * kB + lane];
+            }
+            v = (static_cast<unsigned long long>(static_cast<unsigned>(sh)) << 32) | static_cast<unsigned>(sl);
+        }
+        unsigned long long x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned long long y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        const unsigned long long sum = __shfl(x, 63, 64);
+        unsigned long long base = 0;
+        if (lane == 0 && sum != 0) base = atomicAdd(pair, sum);
+        base = __shfl(base, 0, 64);
+        if (lane < kB) {
+            const unsigned long long e = base + (x - v);  // bin start (both halves; no carry: counts < 2^31)
+            const int el = static_cast<int>(static_cast<unsigned>(e & 0xFFFFFFFFull));
+            const int eh = static_cast<int>(static_cast<unsigned>(e >> 32));
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                cLo[w * kB + lane] = el + pl[w];
+                cHi[w * kB + lane] = eh + ph[w];
+            }
+        }
+    }
+    __syncthreads();
+    *baseLo = cLo[wave * kB + keyLo] + rankLo;
+    *baseHi = cHi[wave * kB + keyHi] + rankHi;
+}
+
+// emission keys (binMode 1): a child run by its first ray's direction octant and lobe, shadow
+// rays by the light of their first sample
+__device__ __forceinline__ int octantKey(v3 d, bool specular) {
+    return (d.x < 0.0F ? 1 : 0) | (d.y < 0.0F ? 2 : 0) | (d.z < 0.0F ? 4 : 0) | (specular ? 8 : 0);
+}
+
 // ---------------------------------------------------------------------------------------
 // pixel mapping: path p -> (pixel slot, sample); slot -> (x, y) through the unit table
 __device__ __forceinline__ void slotToXY(const PixelMap& m, int slot, int* x, int* y) {
@@ -233,8 +324,9 @@ __global__ __launch_bounds__(kWalkThreads, 1) void k_shadow(DScene s, Level lv, 
 }
 
 // Closest hit (kAny false: lv.rO / rD -> lv.hit) or shadow test (true: lv.sO / sD -> lv.sC.w)
-// without the BVH: Naive (accelerator 1) walks every primitive; any other id except 2 / 3
-// builds no accelerator in the reference, so only the area lights can be hit.
+// without the BVH: Naive (accelerator 1) walks every primitive, RegularGrid (2) the 3D-DDA of
+// gridWalk; any other id except 3 builds no accelerator in the reference, so only the area
+// lights can be hit.
 template <bool kAny>
 __global__ __launch_bounds__(256) void k_trace_other(DScene s, Level lv, int* counters, int level) {
     const int count = kAny ? min(counters[cntShadows(level)], lv.shadowCap) : min(counters[cntRays(level)], lv.cap);
@@ -246,7 +338,13 @@ __global__ __launch_bounds__(256) void k_trace_other(DScene s, Level lv, int* co
         const uint32_t src = kAny ? fbits(o4.w) : fbits(d4.w);
         Best b{kAny ? d4.w : kRayLengthMax, 0.0F, 0.0F, kNoPrim};
         bool occluded = false;
-        if (s.accel == kAccNaive) occluded = naiveWalk<kAny>(s, o, d, src, &b);
+        if (s.accel == kAccNaive) {
+            occluded = naiveWalk<kAny>(s, o, d, src, &b);
+        } else if (s.accel == kAccGrid) {  // Shader.cpp:97-101, 142-146: planes, spheres, triangles
+            occluded = gridWalk<kPlane, kAny>(s, s.planeGrid, o, d, src, &b) ||
+                       gridWalk<kSphere, kAny>(s, s.sphereGrid, o, d, src, &b) ||
+                       gridWalk<kTriangle, kAny>(s, s.triGrid, o, d, src, &b);
+        }
         if (kAny) {
             lv.sC[i].w = occluded ? 1.0F : 0.0F;
             continue;
@@ -348,12 +446,17 @@ __device__ __forceinline__ v3 cosineHemisphere(v3 n, float cphi, float sphi, flo
     return normalize(dir);
 }
 
+// Shader.cpp:231 / PathTracer.cpp:55: the light a sample picks
+__device__ __forceinline__ uint32_t lightChoice(const DScene& s, float pick) {
+    return static_cast<uint32_t>(floorf(pick * static_cast<float>(s.nLights) * 0.99999F));
+}
+
 // Light sample i of a shading point (Whitted.cpp:41-53, PathTracer.cpp:53-67):
 // returns false when cos <= 0 (no shadow ray is built).
 // pick / r / q: the three table draws of this sample (light choice, area-light point)
 __device__ __forceinline__ bool lightSample(const DScene& s, const HitGeom& g, float pick, float r, float q,
                                            v3* dirOut, float* distOut, v3* contribOut) {
-    const uint32_t chosen = static_cast<uint32_t>(floorf(pick * static_cast<float>(s.nLights) * 0.99999F));
+    const uint32_t chosen = lightChoice(s, pick);
     const float4* l = s.lights + 4 * chosen;
     const float4 a4 = l[0];
     v3 pos;
@@ -391,6 +494,8 @@ struct ShadeState {
     v3 ld0, lc0;  // light sample 0 (kept in registers)
     float dist0, hcos, hsin, hemi2;
     int nShadow, nChild;
+    int light0;  // the light chosen by sample 0 (emission key of the shadow rays)
+    v3 dir0;     // direction of the first child (computed before the slots are allocated)
 };
 
 // kw: textureWrite of this hit (w >= 0: the material's Kd is that texel when shade() runs)
@@ -442,6 +547,7 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     v.direct = hasPositive(Kd) && s.nLights > 0;
     if (v.direct) {
         v.ok0 = lightSample(s, v.g, pick0, lr0, lq0, &v.ld0, &v.dist0, &v.lc0);
+        v.light0 = static_cast<int>(lightChoice(s, pick0));
         v.nShadow = static_cast<int>(v.ok0);
         for (int k = 1; k < a.samplesLight; ++k) {
             v3 ld, lc;
@@ -512,12 +618,21 @@ __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, 
             nx.rD[j] = make_float4(dir.x, dir.y, dir.z, bitsf(v.g.src));
             nx.tree[j] = v.tc * 4u + slot;
         };
-        if (v.wantD) emit(cosineHemisphere(v.g.N, v.hcos, v.hsin, v.hemi2), 1u);
-        if (v.wantS) emit(reflect(v.d, v.g.N), 2u);
-        if (v.wantT) emit(refract(v.d, v.g.N, 1.0F / v.ior), 3u);
+        // the first child's direction was computed before allocation (firstChildDir)
+        if (v.wantD) emit(v.dir0, 1u);
+        if (v.wantS) emit(v.wantD ? reflect(v.d, v.g.N) : v.dir0, 2u);
+        if (v.wantT) emit(v.wantD || v.wantS ? refract(v.d, v.g.N, 1.0F / v.ior) : v.dir0, 3u);
     }
     const int mask = (v.wantD ? 1 : 0) | (v.wantS ? 2 : 0) | (v.wantT ? 4 : 0);
     lv.vtx[i] = make_int4(v.mat, shadowBase, childBase, (v.nShadow << 3) | mask);
+}
+
+// direction of a vertex's first child: diffuse (PathTracer.cpp:90-91), else specular
+// (:118-120), else transmission (:129-131)
+__device__ __forceinline__ v3 firstChildDir(const ShadeState& v) {
+    if (v.wantD) return cosineHemisphere(v.g.N, v.hcos, v.hsin, v.hemi2);
+    if (v.wantS) return reflect(v.d, v.g.N);
+    return refract(v.d, v.g.N, 1.0F / v.ior);
 }
 
 template <int kShader>
@@ -528,6 +643,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
     auto* pair = reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1));
     static_assert(cntShadows(1) == cntRays(2) + 1, "pair layout");
     __shared__ unsigned long long allocLds[2 * (kBlock / 64 + 1)];
+    __shared__ int binLds[2 * (2 * (kBlock / 64) * kEmitBins + 2)];
+    const bool dead = deadNext != 0;
     int parity = 0;
     for (int base = static_cast<int>(blockIdx.x * blockDim.x); base < count;
          base += static_cast<int>(gridDim.x * blockDim.x)) {
@@ -543,11 +660,19 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
                 lv.last[i] = kw;
             }
             v = shadePrepare<kShader>(s, lv.rO[i], lv.rD[i], h, lv.tree[i], level, a, kw);
+            if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
         }
         int childBase, shadowBase;
-        blockAllocPair(pair, active ? v.nChild : 0, active ? v.nShadow : 0, &childBase, &shadowBase, allocLds, parity);
+        const int nC = active ? v.nChild : 0, nS = active ? v.nShadow : 0;
+        if (a.binMode == 1 && !dead) {
+            const int cKey = nC > 0 ? octantKey(v.dir0, !v.wantD) : 0;
+            const int sKey = nS > 0 ? (v.light0 & (kEmitBins - 1)) : 0;
+            blockAllocBinned(pair, nC, cKey, nS, sKey, a.shadowBits, &childBase, &shadowBase, binLds, parity);
+        } else {
+            blockAllocPair(pair, nC, nS, &childBase, &shadowBase, allocLds, parity);
+        }
         parity ^= 1;
-        if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, deadNext != 0);
+        if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, dead);
         if (a.stats != nullptr) {  // counting pass: shaded (non-terminal) vertices
             const uint64_t m = __ballot(active && !v.terminal);
             if (laneId() == 0 && m != 0) atomicAdd(a.stats + kStatShaded, static_cast<unsigned long long>(__popcll(m)));
@@ -877,7 +1002,7 @@ int persistentGrid(K kernel, int slot, int maxThreads) {
 
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
-    if (s.accel != kAccBVH && s.accel != kAccGrid) {
+    if (s.accel != kAccBVH) {
         hipLaunchKernelGGL((k_trace_other<false>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }
@@ -886,7 +1011,7 @@ void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int
 
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
-    if (s.accel != kAccBVH && s.accel != kAccGrid) {
+    if (s.accel != kAccBVH) {
         hipLaunchKernelGGL((k_trace_other<true>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }

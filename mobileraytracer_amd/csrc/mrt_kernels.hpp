@@ -94,7 +94,13 @@ struct ShadeArgs {
     int samplesLight;  // Config::samplesLight
     float maxPoint[3]; // DepthMap::maxPoint_ (C_wrapper.cpp:79-131 maxDist)
     unsigned long long* stats;  // counting pass only (else null): kStatShaded
+    // emission order of child and shadow rays inside a k_shade block (tuning key 4, never changes
+    // results): 0 compaction only (parent order), 1 binned - children by direction octant and
+    // lobe (diffuse / specular+transmission), shadow rays by light - with ballot multi-scans
+    int binMode;
+    int shadowBits;  // bits of the largest shadow-ray count of a vertex (samplesLight)
 };
+constexpr int kEmitBins = 16;
 
 struct AccumArgs {
     PixelMap map;

@@ -129,6 +129,7 @@ struct mrt_renderer {
     hipStream_t stream = nullptr;
     int overlap = 1;                     // tuning key 3: shadow rays on their own stream
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
+    int binMode = 0;                     // tuning key 4: binned emission of child / shadow rays (ShadeArgs::binMode)
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
 
@@ -326,6 +327,30 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.triNaive = r->sceneMem.upload(inverse(r->triOrder), st);
     d.planeNaive = r->sceneMem.upload(inverse(r->planeOrder), st);
     d.sphereNaive = r->sceneMem.upload(inverse(r->sphereOrder), st);
+    // RegularGrid (accelerator 2): one 32^3 grid per primitive kind (Shader.cpp:56-61)
+    auto gridOf = [&](const HGrid& h) {
+        GGrid gg{};
+        const v3 m = h.world.mn;
+        const float mnv[3] = {m.x, m.y, m.z}, csv[3] = {h.cellSize.x, h.cellSize.y, h.cellSize.z},
+                    csiv[3] = {h.cellSizeInv.x, h.cellSizeInv.y, h.cellSizeInv.z};
+        for (int a = 0; a < 3; ++a) {
+            gg.mn[a] = mnv[a];
+            gg.cs[a] = csv[a];
+            gg.csi[a] = csiv[a];
+        }
+        gg.count = h.count;
+        gg.start = r->sceneMem.upload(h.start, st);
+        gg.items = r->sceneMem.upload(h.items.empty() ? std::vector<int32_t>(1, 0) : h.items, st);
+        return gg;
+    };
+    d.planeGrid = GGrid{};
+    d.sphereGrid = GGrid{};
+    d.triGrid = GGrid{};
+    if (d.accel == kAccGrid) {
+        d.planeGrid = gridOf(buildGrid(sc.planes, r->planeOrder));
+        d.sphereGrid = gridOf(buildGrid(sc.spheres, r->sphereOrder));
+        d.triGrid = gridOf(buildGrid(sc.triangles, r->triOrder));
+    }
     d.nLights = static_cast<int32_t>(sc.lights.size());
     d.nMats = static_cast<int32_t>(sc.materials.size());
     d.cull = r->cfg.cull;
@@ -427,8 +452,11 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     const bool timing = (r->profileFlags & 1) != 0;
     const bool counting = (r->profileFlags & 2) != 0;
     mrt_renderer::Pipe& pp = r->pipe;
-    ShadeArgs sa{r->maxDepth, std::max(1, r->cfg.samplesLight), {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z},
-                 counting ? pp.stats : nullptr};
+    const int spl = std::max(1, r->cfg.samplesLight);
+    int splBits = 0;
+    while ((spl >> splBits) != 0) ++splBits;
+    ShadeArgs sa{r->maxDepth, spl, {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z}, counting ? pp.stats : nullptr,
+                 r->binMode, splBits};
     const int nLevels = r->nLevels;
     const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
     MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * kNumStats, st));
@@ -810,6 +838,10 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->skipLast = value;
         return 0;
     }
+    if (key == 4 && (value == 0 || value == 1)) {
+        r->binMode = value;
+        return 0;
+    }
     gLastError = "unknown tuning key/value";
     return -1;
 }
@@ -839,6 +871,56 @@ int64_t mrt_triangle_bvh(const mrt_config* cfg, float* boxes, int32_t* offsets, 
             counts[i] = b.numPrimitives;
         }
         std::memcpy(order, perm.data(), perm.size() * sizeof(int32_t));
+    });
+    return rc == 0 ? n : -1;
+}
+
+int mrt_grid_box_test(int32_t kind, const float* prim, const float* box) {
+    using namespace mrt;
+    const HAABB b{v3{box[0], box[1], box[2]}, v3{box[3], box[4], box[5]}};
+    const v3 p0{prim[0], prim[1], prim[2]}, p1{prim[3], prim[4], prim[5]};
+    if (kind == 0) return boxIntersect(makeTriangle(p0, p1, v3{prim[6], prim[7], prim[8]}), b) ? 1 : 0;
+    if (kind == 1) return boxIntersect(makePlane(p0, p1, -1), b) ? 1 : 0;
+    if (kind == 2) return boxIntersect(makeSphere(p0, prim[3], -1), b) ? 1 : 0;
+    gLastError = "grid box test: kind must be 0 (triangle), 1 (plane) or 2 (sphere)";
+    return -1;
+}
+
+int64_t mrt_regular_grid(const mrt_config* cfg, int32_t kind, float* world, int32_t* start, int32_t* items) {
+    using namespace mrt;
+    int64_t n = -1;
+    const int rc = guarded([&] {
+        if (kind < 0 || kind > 2) throw std::runtime_error("regular grid: kind must be 0 (planes), 1 (spheres), 2 (triangles)");
+        HScene sc;
+        if (cfg->sceneIndex >= 0 && cfg->sceneIndex <= 3) {
+            sc = builtinScene(cfg->sceneIndex);
+        } else {
+            std::string err;
+            if (!loadObjScene(cfg->objFilePath ? cfg->objFilePath : "", cfg->mtlFilePath ? cfg->mtlFilePath : "", &sc,
+                              &err))
+                throw std::runtime_error(err);
+        }
+        std::vector<int32_t> order;
+        HGrid g;
+        if (kind == 0) {
+            buildBVH(&sc.planes, &order);
+            g = buildGrid(sc.planes, order);
+        } else if (kind == 1) {
+            buildBVH(&sc.spheres, &order);
+            g = buildGrid(sc.spheres, order);
+        } else {
+            buildBVH(&sc.triangles, &order);
+            g = buildGrid(sc.triangles, order);
+        }
+        n = static_cast<int64_t>(g.items.size());
+        if (world != nullptr) {
+            const float w[12] = {g.world.mn.x, g.world.mn.y, g.world.mn.z, g.world.mx.x, g.world.mx.y, g.world.mx.z,
+                                 g.cellSize.x, g.cellSize.y, g.cellSize.z, g.cellSizeInv.x, g.cellSizeInv.y, g.cellSizeInv.z};
+            std::memcpy(world, w, sizeof(w));
+        }
+        if (start != nullptr) std::memcpy(start, g.start.data(), g.start.size() * sizeof(int32_t));
+        if (items != nullptr)  // input order indices, as the reference's grid holds its primitives
+            for (size_t k = 0; k < g.items.size(); ++k) items[k] = order[static_cast<size_t>(g.items[k])];
     });
     return rc == 0 ? n : -1;
 }
@@ -878,6 +960,7 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 2: *value = r->ds.cull; return 0;
         case 3: *value = r->overlap; return 0;
         case 7: *value = r->skipLast; return 0;
+        case 4: *value = r->binMode; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

@@ -142,6 +142,21 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
 // (already in BVH order): the normal-line cone and the conditioning bound K of its triangles.
 std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris);
 
+// RegularGrid<T> build (mrt_grid.cpp): prims in BVH order, order[j] = input index of prims[j]
+struct HGrid {
+    HAABB world;
+    v3 cellSize, cellSizeInv;
+    int32_t count = 0;
+    std::vector<int32_t> start, items;  // CSR over kGridCells cells
+};
+// the primitives' box tests that decide cell membership (Triangle.cpp:142-229, Plane.cpp:146-155,
+// Sphere.cpp:102-123)
+bool boxIntersect(const HTriangle& t, const HAABB& box);
+bool boxIntersect(const HPlane& p, const HAABB& box);
+bool boxIntersect(const HSphere& s, const HAABB& box);
+template <class T>
+HGrid buildGrid(const std::vector<T>& prims, const std::vector<int32_t>& order);
+
 // Utils.cpp:43-53 haltonSequence
 float haltonSequence(uint32_t index, uint32_t base);
 // Utils.hpp:209-218 with std::mt19937(seed) instead of random_device

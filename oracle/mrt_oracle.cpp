@@ -25,6 +25,7 @@
 //     thread's own copy of the materials (the reference shares them between threads);
 //   * each pixel receives its samples in order (no tile-claim race, Renderer.cpp:190-193).
 #include <algorithm>
+#include <limits>
 #include <map>
 #include <array>
 #include <atomic>
@@ -565,6 +566,218 @@ struct BVH {
     }
 };
 
+// ---- RegularGrid (RegularGrid.hpp) ------------------------------------------------------
+// The primitives' own box tests, used only to fill the grid.
+// Triangle::intersect(const AABB&) (Triangle.cpp:142-229): an edge half-line crosses the box,
+// or the box's min->max diagonal ray hits the triangle, or that diagonal is parallel to it.
+inline bool gridEdgeHitsBox(const Vec3& orig, const Vec3& vec, const AABB& box) {  // :143-201
+    Vec3 t1, t2;
+    float tNear = std::numeric_limits<float>::min();
+    float tFar = std::numeric_limits<float>::max();
+    for (int a = 0; a < 3; ++a) {
+        if (std::fabs(vec[a]) < std::numeric_limits<float>::epsilon()) {
+            if ((orig[a] < box.pointMin[a]) || ((orig[a] + vec[a]) > box.pointMax[a])) return false;
+        } else {
+            t1[a] = (box.pointMin[a] - orig[a]) / vec[a];
+            t2[a] = (box.pointMax[a] - orig[a]) / vec[a];
+            if (t1[a] > t2[a]) std::swap(t1, t2);
+            tNear = std::max(t1[a], tNear);
+            tFar = std::min(t2[a], tFar);
+            if ((tNear > tFar) || (tFar < 0)) return false;  // isNearFarInvalid (:132-134)
+        }
+    }
+    return true;
+}
+inline bool boxIntersect(const Triangle& t, const AABB& box) {
+    const Vec3 vec = box.pointMax - box.pointMin;
+    const Ray ray(vec, box.pointMin, 1, false, nullptr, nullptr);
+    const bool ab = gridEdgeHitsBox(t.pointA, t.AB, box);
+    const bool ac = gridEdgeHitsBox(t.pointA, t.AC, box);
+    const Vec3 pointB = t.pointA + t.AB;
+    const Vec3 pointC = t.pointA + t.AC;
+    const bool bc = gridEdgeHitsBox(pointB, pointC - pointB, box);
+    Intersection it(ray);
+    const float lastDist = it.length;
+    it = t.intersect(it);
+    const bool hitRay = it.length < lastDist;
+    const bool inside = std::abs(dot(t.AB, cross(vec, t.AC))) < Epsilon;
+    return ab || ac || bc || hitRay || inside;
+}
+inline float planeDistance(const Plane& p, const Vec3& q) {  // Plane.cpp:117-138
+    const float d = p.normal[0] * -p.point[0] + p.normal[1] * -p.point[1] + p.normal[2] * -p.point[2];
+    const float numerator = p.normal[0] * q[0] + p.normal[1] * q[1] + p.normal[2] * q[2] + d;
+    const float denumerator = std::sqrt(p.normal[0] * p.normal[0] + p.normal[1] * p.normal[1] + p.normal[2] * p.normal[2]);
+    return numerator / denumerator;
+}
+inline bool boxIntersect(const Plane& p, const AABB& box) {  // Plane.cpp:146-155
+    const float distanceP = planeDistance(p, box.pointMax);
+    const float distanceN = planeDistance(p, box.pointMin);
+    return (distanceP <= 0 && distanceN >= 0) || (distanceP >= 0 && distanceN <= 0);
+}
+inline bool boxIntersect(const Sphere& s, const AABB& box) {  // Sphere.cpp:102-123
+    float dmin = 0.0F;
+    for (int a = 0; a < 3; ++a) {
+        if (s.center[a] < box.pointMin[a]) {
+            dmin = dmin + (s.center[a] - box.pointMin[a]) * (s.center[a] - box.pointMin[a]);
+        } else if (s.center[a] > box.pointMax[a]) {
+            dmin = dmin + (s.center[a] - box.pointMax[a]) * (s.center[a] - box.pointMax[a]);
+        }
+    }
+    return dmin <= s.sqRadius;
+}
+
+// static_cast<int32_t>(float) as x86 cvttss2si evaluates it (NaN / out of range: INT32_MIN),
+// spelled out so the oracle does not depend on the compiler's treatment of that UB
+inline int32_t cvtt(float f) {
+    return (f >= -2147483648.0F && f < 2147483648.0F) ? static_cast<int32_t>(f) : std::numeric_limits<int32_t>::min();
+}
+
+template <typename T>
+struct RegularGrid {  // RegularGrid.hpp:23-101, gridSize 32 (Shader.cpp:57)
+    std::vector<std::vector<const T*>> grid;
+    std::vector<T> primitives;
+    int32_t gridSize = 32;
+    uint32_t gridShift = 0;
+    AABB worldBoundaries;
+    Vec3 cellSizeInverted, cellSize;
+
+    static uint32_t bitCounter(uint32_t value) {  // :173-180
+        uint32_t counter = 0;
+        while (value > 0) {
+            ++counter;
+            value >>= 1;
+        }
+        return counter;
+    }
+
+    RegularGrid(std::vector<T> prims, uint32_t size)  // :112-152
+        : grid(static_cast<size_t>(size) * size * size), primitives(std::move(prims)),
+          gridSize(static_cast<int32_t>(size)), gridShift(bitCounter(size - 1U)) {
+        // Scene::getBounds (Scene.hpp:51-62)
+        AABB bounds{Vec3(RayLengthMax), Vec3(-RayLengthMax)};
+        for (const T& p : primitives) bounds = surroundingBox(p.getAABB(), bounds);
+        worldBoundaries = AABB{bounds.pointMin - Vec3(Epsilon), bounds.pointMax + Vec3(Epsilon)};
+        const Vec3 ext = worldBoundaries.pointMax - worldBoundaries.pointMin;
+        cellSizeInverted = Vec3(static_cast<float>(gridSize) / ext[0], static_cast<float>(gridSize) / ext[1],
+                                static_cast<float>(gridSize) / ext[2]);
+        cellSize = ext * (1.0F / static_cast<float>(gridSize));
+        addPrimitives();
+    }
+
+    // addPrimitivesThreadWork (:216-289) on one thread: every cell list in input order (the
+    // reference's threads append under per-cell mutexes, in lock order)
+    void addPrimitives() {
+        const Vec3 worldBoundsMin = worldBoundaries.pointMin;
+        const Vec3 size = worldBoundaries.pointMax - worldBoundsMin;
+        const float dx = size[0] / gridSize, dy = size[1] / gridSize, dz = size[2] / gridSize;
+        const float dxReci = dx > 0 ? 1.0F / dx : 1.0F;
+        const float dyReci = dy > 0 ? 1.0F / dy : 1.0F;
+        const float dzReci = dz > 0 ? 1.0F / dz : 1.0F;
+        auto range = [&](float lo, float hi, float wmin, float sz, float reci, int32_t* a, int32_t* b) {
+            int32_t v1 = cvtt((lo - wmin) * reci);
+            int32_t v2 = cvtt((hi - wmin) * reci) + 1;
+            v1 = std::max(0, v1);
+            v2 = std::min(v2, gridSize - 1);
+            v2 = std::fabs(sz) < std::numeric_limits<float>::epsilon() ? 0 : v2;
+            v1 = std::min(v1, v2);
+            *a = v1;
+            *b = v2;
+        };
+        for (const T& primitive : primitives) {
+            const AABB bound = primitive.getAABB();
+            int32_t x1, x2, y1, y2, z1, z2;
+            range(bound.pointMin[0], bound.pointMax[0], worldBoundsMin[0], size[0], dxReci, &x1, &x2);
+            range(bound.pointMin[1], bound.pointMax[1], worldBoundsMin[1], size[1], dyReci, &y1, &y2);
+            range(bound.pointMin[2], bound.pointMax[2], worldBoundsMin[2], size[2], dzReci, &z1, &z2);
+            for (int32_t x = x1; x <= x2; ++x) {
+                for (int32_t y = y1; y <= y2; ++y) {
+                    for (int32_t z = z1; z <= z2; ++z) {
+                        const uint32_t idx = static_cast<uint32_t>(x + y * gridSize + z * gridSize * gridSize);
+                        const Vec3 pos(worldBoundsMin[0] + static_cast<float>(x) * dx,
+                                       worldBoundsMin[1] + static_cast<float>(y) * dy,
+                                       worldBoundsMin[2] + static_cast<float>(z) * dz);
+                        const AABB cell{pos, pos + Vec3(dx, dy, dz)};
+                        if (boxIntersect(primitive, cell)) grid[idx].push_back(&primitive);
+                    }
+                }
+            }
+        }
+    }
+
+    int32_t cellIndex(int32_t x, int32_t y, int32_t z) const {  // getCellIndex (:526-538)
+        return static_cast<int32_t>(static_cast<uint32_t>(x) + (static_cast<uint32_t>(y) << gridShift) +
+                                    (static_cast<uint32_t>(z) << (gridShift * 2U)));
+    }
+
+    Intersection intersect(Intersection intersection) const {  // :333-515
+        const Vec3 worldBoundsMin = worldBoundaries.pointMin;
+        const Vec3 cell = (intersection.ray.origin - worldBoundsMin) * cellSizeInverted;
+        int32_t cellX = cvtt(cell[0]), cellY = cvtt(cell[1]), cellZ = cvtt(cell[2]);
+        cellX = std::max(std::min(cellX, gridSize - 1), 0);
+        cellY = std::max(std::min(cellY, gridSize - 1), 0);
+        cellZ = std::max(std::min(cellZ, gridSize - 1), 0);
+        int32_t stepX, outX, stepY, outY, stepZ, outZ;
+        Vec3 cb;
+        const Vec3& dir = intersection.ray.direction;
+        const Vec3& org = intersection.ray.origin;
+        if (dir[0] > 0) { stepX = 1; outX = gridSize; cb[0] = worldBoundsMin[0] + (static_cast<float>(cellX) + 1.0F) * cellSize[0]; }
+        else { stepX = -1; outX = -1; cb[0] = worldBoundsMin[0] + static_cast<float>(cellX) * cellSize[0]; }
+        if (dir[1] > 0) { stepY = 1; outY = gridSize; cb[1] = worldBoundsMin[1] + (static_cast<float>(cellY) + 1.0F) * cellSize[1]; }
+        else { stepY = -1; outY = -1; cb[1] = worldBoundsMin[1] + static_cast<float>(cellY) * cellSize[1]; }
+        if (dir[2] > 0) { stepZ = 1; outZ = gridSize; cb[2] = worldBoundsMin[2] + (static_cast<float>(cellZ) + 1.0F) * cellSize[2]; }
+        else { stepZ = -1; outZ = -1; cb[2] = worldBoundsMin[2] + static_cast<float>(cellZ) * cellSize[2]; }
+        Vec3 tmax, tdelta;
+        const float eps = std::numeric_limits<float>::epsilon();
+        if (std::fabs(dir[0]) > eps) { const float r = 1.0F / dir[0]; tmax[0] = (cb[0] - org[0]) * r; tdelta[0] = cellSize[0] * static_cast<float>(stepX) * r; }
+        else { tmax[0] = RayLengthMax; }
+        if (std::fabs(dir[1]) > eps) { const float r = 1.0F / dir[1]; tmax[1] = (cb[1] - org[1]) * r; tdelta[1] = cellSize[1] * static_cast<float>(stepY) * r; }
+        else { tmax[1] = RayLengthMax; }
+        if (std::fabs(dir[2]) > eps) { const float r = 1.0F / dir[2]; tmax[2] = (cb[2] - org[2]) * r; tdelta[2] = cellSize[2] * static_cast<float>(stepZ) * r; }
+        else { tmax[2] = RayLengthMax; }
+        // first loop: until a primitive of this grid improves the hit (shadow rays return there)
+        while (true) {
+            for (const T* primitive : grid[static_cast<size_t>(cellIndex(cellX, cellY, cellZ))]) {
+                const float lastDist = intersection.length;
+                intersection = primitive->intersect(intersection);
+                if (intersection.length < lastDist) {
+                    if (intersection.ray.shadowTrace) return intersection;
+                    goto testloop;
+                }
+            }
+            if (tmax[0] < tmax[1]) {
+                if (tmax[0] < tmax[2]) { cellX += stepX; if (cellX == outX) return intersection; tmax[0] = tmax[0] + tdelta[0]; }
+                else { cellZ += stepZ; if (cellZ == outZ) return intersection; tmax[2] = tmax[2] + tdelta[2]; }
+            } else {
+                if (tmax[1] < tmax[2]) { cellY += stepY; if (cellY == outY) return intersection; tmax[1] = tmax[1] + tdelta[1]; }
+                else { cellZ += stepZ; if (cellZ == outZ) return intersection; tmax[2] = tmax[2] + tdelta[2]; }
+            }
+        }
+    testloop:
+        while (true) {
+            for (const T* primitive : grid[static_cast<size_t>(cellIndex(cellX, cellY, cellZ))])
+                intersection = primitive->intersect(intersection);
+            if (tmax[0] < tmax[1]) {
+                if (tmax[0] < tmax[2]) {
+                    if (intersection.length < tmax[0]) break;
+                    cellX += stepX; if (cellX == outX) break; tmax[0] = tmax[0] + tdelta[0];
+                } else {
+                    if (intersection.length < tmax[2]) break;
+                    cellZ += stepZ; if (cellZ == outZ) break; tmax[2] = tmax[2] + tdelta[2];
+                }
+            } else {
+                if (tmax[1] < tmax[2]) {
+                    if (intersection.length < tmax[1]) break;
+                    cellY += stepY; if (cellY == outY) break; tmax[1] = tmax[1] + tdelta[1];
+                } else {
+                    if (intersection.length < tmax[2]) break;
+                    cellZ += stepZ; if (cellZ == outZ) break; tmax[2] = tmax[2] + tdelta[2];
+                }
+            }
+        }
+        return intersection;
+    }
+};
+
 // ---- lights -------------------------------------------------------------------------------
 struct Light {
     Material radiance;
@@ -1058,6 +1271,9 @@ struct Engine {
     std::unique_ptr<BVH<Plane>> planes;
     std::unique_ptr<BVH<Sphere>> spheres;
     std::unique_ptr<BVH<Triangle>> triangles;
+    std::unique_ptr<RegularGrid<Plane>> gridPlanes;  // RegularGrid accelerator (Shader.cpp:56-61)
+    std::unique_ptr<RegularGrid<Sphere>> gridSpheres;
+    std::unique_ptr<RegularGrid<Triangle>> gridTriangles;
     std::vector<Plane> naivePlanes;  // input order (Naive accelerator)
     std::vector<Sphere> naiveSpheres;
     std::vector<Triangle> naiveTriangles;
@@ -1116,7 +1332,11 @@ struct Engine {
             it = naive(naivePlanes, it);
             it = naive(naiveSpheres, it);
             it = naive(naiveTriangles, it);
-        } else if (cfg.accelerator == 2 || cfg.accelerator == 3) {  // RegularGrid served by the BVH
+        } else if (cfg.accelerator == 2) {
+            it = gridPlanes->intersect(it);
+            it = gridSpheres->intersect(it);
+            it = gridTriangles->intersect(it);
+        } else if (cfg.accelerator == 3) {
             it = planes->intersect(it);
             it = spheres->intersect(it);
             it = triangles->intersect(it);
@@ -1415,6 +1635,11 @@ Engine* create(const Config& cfg) {
     e->planes = std::make_unique<BVH<Plane>>(s.planes);
     e->spheres = std::make_unique<BVH<Sphere>>(s.spheres);
     e->triangles = std::make_unique<BVH<Triangle>>(s.triangles);
+    if (cfg.accelerator == 2) {
+        e->gridPlanes = std::make_unique<RegularGrid<Plane>>(s.planes, 32U);
+        e->gridSpheres = std::make_unique<RegularGrid<Sphere>>(s.spheres, 32U);
+        e->gridTriangles = std::make_unique<RegularGrid<Triangle>>(s.triangles, 32U);
+    }
     e->naivePlanes = s.planes;
     e->naiveSpheres = s.spheres;
     e->naiveTriangles = s.triangles;
@@ -1453,6 +1678,46 @@ void* oracle_create(const OracleConfig* c) {
 }
 
 void oracle_destroy(void* h) { delete static_cast<oracle::Engine*>(h); }
+
+// a grid cell's membership test (Triangle.cpp:142-229, Plane.cpp:146-155, Sphere.cpp:102-123):
+// kind 0 prim = A, B, C; 1 = point, normal; 2 = center, radius; box = min, max
+int oracle_grid_box_test(int kind, const float* prim, const float* box) {
+    using namespace oracle;
+    const AABB b{Vec3(box[0], box[1], box[2]), Vec3(box[3], box[4], box[5])};
+    const Vec3 p0(prim[0], prim[1], prim[2]), p1(prim[3], prim[4], prim[5]);
+    if (kind == 0) return boxIntersect(Triangle::build(p0, p1, Vec3(prim[6], prim[7], prim[8]), nullptr, nullptr, nullptr, -1), b);
+    if (kind == 1) return boxIntersect(Plane(p0, p1, -1), b);
+    if (kind == 2) return boxIntersect(Sphere(p0, prim[3], -1), b);
+    return -1;
+}
+
+// the RegularGrid of one kind (0 planes, 1 spheres, 2 triangles) of an accelerator-2 engine:
+// world[12] = min, max, cellSize, cellSizeInverted; start[32^3 + 1]; items = input indices
+int64_t oracle_regular_grid(void* h, int kind, float* world, int32_t* start, int32_t* items) {
+    auto* e = static_cast<oracle::Engine*>(h);
+    int64_t n = -1;
+    auto dump = [&](const auto& g) {
+        const oracle::Vec3 w[4] = {g->worldBoundaries.pointMin, g->worldBoundaries.pointMax, g->cellSize,
+                                   g->cellSizeInverted};
+        for (int i = 0; i < 4; ++i)
+            for (int a = 0; a < 3; ++a)
+                if (world != nullptr) world[3 * i + a] = w[i][a];
+        int64_t k = 0;
+        for (size_t c = 0; c < g->grid.size(); ++c) {
+            if (start != nullptr) start[c] = static_cast<int32_t>(k);
+            for (const auto* p : g->grid[c]) {
+                if (items != nullptr) items[k] = static_cast<int32_t>(p->inputIndex);
+                ++k;
+            }
+        }
+        if (start != nullptr) start[g->grid.size()] = static_cast<int32_t>(k);
+        n = k;
+    };
+    if (kind == 0 && e->gridPlanes) dump(e->gridPlanes);
+    if (kind == 1 && e->gridSpheres) dump(e->gridSpheres);
+    if (kind == 2 && e->gridTriangles) dump(e->gridTriangles);
+    return n;
+}
 
 // timing-faithful sample draws (shared atomic cursors, as the reference): 1 on, 0 off
 void oracle_set_faithful(void* h, int on) { static_cast<oracle::Engine*>(h)->faithful = on != 0; }

@@ -71,6 +71,9 @@ def lib():
         L.oracle_fast_arctan.argtypes = [ctypes.c_float]
         L.oracle_selftest_partition.argtypes = [ctypes.c_uint32, ctypes.c_int]
         L.oracle_register_texture.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp]
+        L.oracle_grid_box_test.argtypes = [ctypes.c_int, f, f]
+        L.oracle_regular_grid.restype = ctypes.c_int64
+        L.oracle_regular_grid.argtypes = [vp, ctypes.c_int, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -246,6 +249,17 @@ class Oracle:
         lib().oracle_triangle_bvh(self._h, boxes.ctypes.data, off.ctypes.data, cnt.ctypes.data, order.ctypes.data)
         return boxes, off, cnt, order
 
+    def regular_grid(self, kind):
+        """RegularGrid of kind 0 planes / 1 spheres / 2 triangles (engine built with accelerator 2):
+        world (12 floats: min, max, cellSize, cellSizeInverted), start (32^3 + 1), items (input
+        indices)."""
+        n = lib().oracle_regular_grid(self._h, kind, None, None, None)
+        if n < 0:
+            raise RuntimeError("the engine has no regular grid (accelerator != 2)")
+        world, start, items = np.empty(12, np.float32), np.empty(32 ** 3 + 1, np.int32), np.empty(max(n, 1), np.int32)
+        lib().oracle_regular_grid(self._h, kind, world.ctypes.data, start.ctypes.data, items.ctypes.data)
+        return world, start, items[:n]
+
     def close(self):
         if getattr(self, "_h", None):
             lib().oracle_destroy(self._h)
@@ -260,6 +274,12 @@ def kat_triangle(a, b, c, orig, direction, from_self=False):
     hit = lib().oracle_kat_triangle(fvec(*a), fvec(*b), fvec(*c), fvec(*orig), fvec(*direction), int(from_self),
                                     ctypes.byref(t))
     return bool(hit), t.value
+
+
+def grid_box_test(kind, prim, box):
+    """Cell membership test of the RegularGrid fill: kind 0 prim = A + B + C, 1 = point + normal,
+    2 = center + (radius,); box = min + max."""
+    return bool(lib().oracle_grid_box_test(kind, fvec(*prim), fvec(*box)))
 
 
 def kat_aabb(mn, mx, orig, direction):

@@ -177,6 +177,64 @@ def test_naive_and_missing_accelerator(oracle_mod, case):
         assert all(np.array_equal(a, b) for a, b in zip(g, r))
 
 
+# ---- RegularGrid (accelerator 2; RegularGrid.hpp, gridSize 32): the reference's 3D-DDA over the
+# cell lists its own membership tests fill (tests/test_grid_cpu.py pins the build); ties go to
+# the first primitive tested, a closest-hit walk stops at the first cell boundary past its hit ----
+@pytest.mark.parametrize("case", [
+    dict(width=128, height=128, shader=1, accelerator=2),                       # Cornell: planes, spheres, triangles
+    dict(width=96, height=96, shader=1, scene="water", accelerator=2),          # 7,088 triangles, transmission
+    dict(width=128, height=128, sceneIndex=2, shader=1, accelerator=2),         # area lights
+    dict(width=64, height=64, sceneIndex=1, shader=3, accelerator=2),           # spheres, DepthMap
+    dict(width=64, height=64, sceneIndex=3, shader=0, accelerator=2),           # NoShadows
+    dict(width=64, height=64, shader=2, spp=2, accelerator=2),                  # PathTracer
+    dict(width=64, height=64, shader=1, scene="teapot", accelerator=2),         # textured
+    dict(width=96, height=64, shader=1, scene="conference", accelerator=2),     # 331,179 triangles
+    dict(width=64, height=48, shader=2, scene="conference", accelerator=2, max_depth=5),
+])
+def test_regular_grid(oracle_mod, case):
+    cfg = make_cfg(**case)
+    bm, rays, _ = gpu_render(cfg)
+    ref, ref_rays = oracle_render(oracle_mod, cfg)
+    once = coverage(cfg.width, cfg.height) == 1
+    assert np.array_equal(bm[once], ref[once]), int((bm[once] != ref[once]).sum())
+    assert rays == ref_rays
+    assert len(np.unique(bm)) > 1
+    if cfg.shader == 1:  # primary hit ids, bit-exact
+        g = gpu_hits(cfg)
+        o = oracle_for(oracle_mod, cfg)
+        r = o.primary_hits()
+        o.close()
+        assert all(np.array_equal(a, b) for a, b in zip(g, r))
+
+
+@pytest.mark.parametrize("scene", [None, "water", "conference"])
+def test_regular_grid_random_rays(oracle_mod, scene):
+    """Random rays from inside and outside the grid (clamped start cells), closest hit and
+    shadow test to a random distance, through the device grid walk vs the oracle's."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, shader=1, scene=scene, accelerator=2)
+    w, _, _ = m.regular_grid(cfg, 2)
+    lo, hi = w[:3], w[3:6]
+    rng = np.random.default_rng(11)
+    n = 20000
+    o = (lo - 0.25 * (hi - lo) + rng.random((n, 3)) * 1.5 * (hi - lo)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    d[: n // 10, rng.integers(0, 3)] = 0.0  # axis-parallel directions: the tmax = RayLengthMax branch
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    dist = (rng.random(n) * np.linalg.norm(hi - lo)).astype(np.float32)
+    with m.Renderer(cfg) as r:
+        hits = r.trace_rays(o, d)
+        occ = r.trace_rays(o, d, dist=dist, any_hit=True)[0]
+    ob = oracle_for(oracle_mod, cfg)
+    ok, oi, ot = ob.trace_rays(o, d)
+    oocc = ob.trace_rays(o, d, dist=dist, any_hit=True)[0]
+    ob.close()
+    assert (hits[0] > 0).mean() > 0.2 and 0.02 < occ.mean() < 0.98
+    assert np.array_equal(hits[0], ok) and np.array_equal(hits[1], oi)
+    assert np.array_equal(hits[2].view(np.int32), ot.view(np.int32))
+    assert np.array_equal(occ, oocc)
+
+
 def test_unknown_shader_ids_are_noshadows():
     """C_wrapper.cpp:188-193: every shader id other than 1-4 builds NoShadows."""
     a, ra, _ = gpu_render(make_cfg(64, 64, shader=0, sceneIndex=3))
@@ -269,6 +327,31 @@ def test_shadow_stream_overlap_is_invariant():
                 outs.append((bm, st["rays"], st["shadowRays"]))
         for bm, rays, shadows in outs[1:]:
             assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
+
+
+def test_binned_emission_is_invariant():
+    """Binned emission (tuning key 4: child rays grouped by direction octant and lobe, shadow rays
+    by light, inside each k_shade block) only reorders the queues: every pixel, ray count and
+    shadow-ray count is the same as with plain compaction, for Whitted (3-child vertices),
+    PathTracer, more than one light sample and textures."""
+    import mobileraytracer_amd as m
+    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+             make_cfg(128, 128, shader=1, scene="water", max_depth=4),
+             make_cfg(96, 96, shader=2, scene="water", spp=2, max_depth=4, spl=3),
+             make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3),
+             make_cfg(64, 64, shader=2, spp=3, max_depth=6))
+    for cfg in cases:
+        outs = []
+        with m.Renderer(cfg) as r:
+            for b in (0, 1):
+                r.set_tuning(4, b)
+                assert r.get_tuning(4) == b
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"])))
+        assert np.array_equal(outs[0][0], outs[1][0]), cfg
+        assert outs[0][1:] == outs[1][1:], cfg
 
 
 def test_last_level_walk_skip_is_invariant():
