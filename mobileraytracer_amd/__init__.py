@@ -116,7 +116,8 @@ class Renderer:
     def set_tuning(self, key: int, value: int) -> None:
         """A/B knobs (identical results): 1 = trace walk (0 reference, 1 default), 2 = t-cull mode
         (0 none, 1 fast, 2 certified), 3 = shadow rays on their own stream, 4 = binned emission
-        of child / shadow rays, 7 = no walk for the depth-capped last level."""
+        of child / shadow rays, 5 = shadow-walk child order (0 near first, 1 far first),
+        7 = no walk for the depth-capped last level."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 
     def get_tuning(self, key: int) -> int:

@@ -39,6 +39,7 @@ struct DScene {
     int32_t variant;           // trace walk: 0 per-wave reference walk, 1 persistent while-while
     int32_t triTop;            // triNodes[0, triTop) are the breadth-first top of the tree
     int32_t matsFinite;        // every material's Kd / Ks / Kt component is finite
+    int32_t anyOrder;          // shadow walk child order (tuning key 5): 0 near first, 1 far first (default)
     // textures (map_Kd): scenes with a textured material only (`textured` != 0)
     const float4* triTex;      // 2 per triangle: (tA.xy, tB.xy), (tC.xy, -, -)
     const int4* texInfo;       // per texture: width, height, channels, first byte in texels

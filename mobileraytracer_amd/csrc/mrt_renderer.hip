@@ -357,6 +357,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.variant = kDefaultTraceVariant;
     // the depth-capped last level's children count as absent in the resolve only while no
     // material coefficient is infinite or NaN (inf * 0 would be NaN in the reference)
+    d.anyOrder = 1;
     d.matsFinite = 1;
     for (const HMaterial& m : sc.materials) {
         for (const v3 c : {m.Kd, m.Ks, m.Kt})
@@ -838,6 +839,10 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->skipLast = value;
         return 0;
     }
+    if (key == 5 && (value == 0 || value == 1)) {
+        r->ds.anyOrder = value;
+        return 0;
+    }
     if (key == 4 && (value == 0 || value == 1)) {
         r->binMode = value;
         return 0;
@@ -961,6 +966,7 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 3: *value = r->overlap; return 0;
         case 7: *value = r->skipLast; return 0;
         case 4: *value = r->binMode; return 0;
+        case 5: *value = r->ds.anyOrder; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

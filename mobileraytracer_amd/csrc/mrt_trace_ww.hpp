@@ -114,7 +114,7 @@ __device__ __forceinline__ float cullKey(uint32_t w, float mnx, float mny, float
 
 // Culling against the keys, near-first order (by box entry) and the push of the far child.
 __device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float tr, float kl, float kr, int refL,
-                                              int refR, float lim, bool cull, TStack& st) {
+                                              int refR, float lim, bool cull, TStack& st, bool rightFirst) {
     if (cull) {
         hl = hl && !(kl > lim);
         hr = hr && !(kr > lim);
@@ -122,7 +122,7 @@ __device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float 
     if (hl && hr) {
         int nearRef = refL, farRef = refR;
         float farK = kr;
-        if (cull && tr < tl) {
+        if (cull && rightFirst) {
             nearRef = refR;
             farRef = refL;
             farK = kl;
@@ -158,7 +158,8 @@ __device__ __forceinline__ float cullLimit(float best) {
 // exact slab, and the certified mode does not cull)
 template <int kCull>
 __device__ __forceinline__ int innerStep(BufRes nodes, const GNode* ldsTop, int top, int ref, v3 o, v3 d, v3 inv,
-                                         float lim, TStack& st, TravCount* cnt, bool count, bool finite) {
+                                         float lim, TStack& st, TravCount* cnt, bool count, bool finite,
+                                         int order) {
     constexpr bool cull = kCull != kCullNone;
     float4 n0, n1, n2;
     int4 n3;
@@ -208,7 +209,12 @@ __device__ __forceinline__ int innerStep(BufRes nodes, const GNode* ldsTop, int 
         hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, inv, &tl);
         hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, inv, &tr);
     }
-    return chooseChildren(hl, hr, tl, tr, kl, kr, n3.x, n3.y, lim, cull, st);
+    // both children hit (culling modes): the nearer entry first (order 0), or the farther (1).  Shadow
+    // rays walk far first by default: an occluder between a surface point and the light is found
+    // sooner from the light's side on the Conference frame (-2 % frame time);
+    // the order changes which occluder is found first, never whether one is
+    const bool rightFirst = order == 0 ? tr < tl : !(tr < tl);
+    return chooseChildren(hl, hr, tl, tr, kl, kr, n3.x, n3.y, lim, cull, st, rightFirst);
 }
 
 // Copies the BVH2 top into LDS (all threads; ends with a barrier).
@@ -359,7 +365,8 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
             const float curLim = cullLimit<kCull>(bt);
             const bool finite = __ballot(!finiteInv(inv)) == 0;
-            ref = innerStep<kCull>(nodeBuf, ldsTop, top, ref, o, d, inv, curLim, st, cnt, kCount, finite);
+            ref = innerStep<kCull>(nodeBuf, ldsTop, top, ref, o, d, inv, curLim, st, cnt, kCount, finite,
+                                   kAny ? s.anyOrder : 0);
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
                 ref = popCulled(st, curLim, cull);

@@ -329,10 +329,11 @@ def test_shadow_stream_overlap_is_invariant():
             assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
 
 
-def test_binned_emission_is_invariant():
+def test_binned_emission_and_shadow_order_are_invariant():
     """Binned emission (tuning key 4: child rays grouped by direction octant and lobe, shadow rays
-    by light, inside each k_shade block) only reorders the queues: every pixel, ray count and
-    shadow-ray count is the same as with plain compaction, for Whitted (3-child vertices),
+    by light, inside each k_shade block) only reorders the queues, and the shadow walk's child
+    order (key 5: near or far first) only changes which occluder is found first: every pixel, ray
+    count and shadow-ray count is the same in all combinations, for Whitted (3-child vertices),
     PathTracer, more than one light sample and textures."""
     import mobileraytracer_amd as m
     cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
@@ -343,15 +344,17 @@ def test_binned_emission_is_invariant():
     for cfg in cases:
         outs = []
         with m.Renderer(cfg) as r:
-            for b in (0, 1):
+            for b, a in ((0, 1), (1, 1), (0, 0)):
                 r.set_tuning(4, b)
-                assert r.get_tuning(4) == b
+                r.set_tuning(5, a)
+                assert r.get_tuning(4) == b and r.get_tuning(5) == a
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
                 r.render_frame(bm)
                 st = r.frame_stats()
                 outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"])))
-        assert np.array_equal(outs[0][0], outs[1][0]), cfg
-        assert outs[0][1:] == outs[1][1:], cfg
+        for other in outs[1:]:
+            assert np.array_equal(outs[0][0], other[0]), cfg
+            assert outs[0][1:] == other[1:], cfg
 
 
 def test_last_level_walk_skip_is_invariant():

@@ -58,7 +58,45 @@ __global__ __launch_bounds__(256, 1) void k_gather(const uint4* __restrict__ tab
     out[tid] = acc;
 }
 
-template <int kVec4, bool kCoherent>
+// Quad-cooperative form of the divergent chase (64-B records): in round k the four lanes of a
+// quad fetch the four 16-B pieces of lane (4q + k)'s record with one LDS-DMA load
+// (global_load_lds_dwordx4), so one wave instruction touches 16 lines, 4 lanes each, instead of
+// 64 lines; the record of lane 4q + k lands contiguously at round k's base + 64 q, and each
+// lane reads its own record back with ds_read_b128.  Rounds are padded by 16 B (bank spread).
+__global__ __launch_bounds__(256, 1) void k_gather_quad(const uint4* __restrict__ table, uint32_t nRecords, int iters,
+                                                       uint32_t* out) {
+    constexpr int kRound = 65;  // uint4 per round: 64 lanes + 1 pad
+    __shared__ uint4 stage[4][4 * kRound];
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = static_cast<int>(threadIdx.x & 63u), wave = static_cast<int>(threadIdx.x >> 6);
+    uint32_t idx = mix(tid) % nRecords;
+    uint32_t acc = 0;
+    for (int i = 0; i < iters; ++i) {
+        uint32_t ik[4];
+        ik[0] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(idx), 0x00, 0xF, 0xF, false));
+        ik[1] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(idx), 0x55, 0xF, 0xF, false));
+        ik[2] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(idx), 0xAA, 0xF, 0xF, false));
+        ik[3] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(idx), 0xFF, 0xF, 0xF, false));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4* g = table + ik[k] * 4u + static_cast<uint32_t>(lane & 3);
+            __builtin_amdgcn_global_load_lds(g, &stage[wave][k * kRound], 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint4* mine = &stage[wave][(lane & 3) * kRound + (lane >> 2) * 4];
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = mine[k];
+            x ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+        acc += x;
+        idx = mix(idx ^ x ^ static_cast<uint32_t>(i)) % nRecords;
+    }
+    out[tid] = acc;
+}
+
+template <int kVec4, bool kCoherent, bool kQuad = false>
 void run(size_t tableBytes, int blocksPerCU, const char* label) {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -77,12 +115,18 @@ void run(size_t tableBytes, int blocksPerCU, const char* label) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    hipLaunchKernelGGL((k_gather<kVec4, kCoherent>), dim3(blocks), dim3(256), 0, 0, table, nRecords, 50, out);
+    auto launch = [&](int it) {
+        if (kQuad)
+            hipLaunchKernelGGL(k_gather_quad, dim3(blocks), dim3(256), 0, 0, table, nRecords, it, out);
+        else
+            hipLaunchKernelGGL((k_gather<kVec4, kCoherent>), dim3(blocks), dim3(256), 0, 0, table, nRecords, it, out);
+    };
+    launch(50);
     CK(hipDeviceSynchronize());
     float best = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
         CK(hipEventRecord(a, 0));
-        hipLaunchKernelGGL((k_gather<kVec4, kCoherent>), dim3(blocks), dim3(256), 0, 0, table, nRecords, iters, out);
+        launch(iters);
         CK(hipEventRecord(b, 0));
         CK(hipEventSynchronize(b));
         float ms = 0;
@@ -108,6 +152,8 @@ int main() {
         run<1, false>(mib << 20, 6, "divergent");
     }
     run<4, true>(32u << 20, 6, "wave-coherent");
+    for (size_t mib : {4, 32, 128}) run<4, false, true>(mib << 20, 6, "quad-cooperative-lds-dma");
+    run<4, false, true>(32u << 20, 4, "quad-cooperative-lds-dma");
     run<4, false>(32u << 20, 8, "divergent");
     return 0;
 }

@@ -17,7 +17,8 @@ def main():
     bm, pk = (d.data_ptr(), 0) if ranks == 1 else (0, d.data_ptr())
     sh = torch.cuda.current_stream().cuda_stream
     # "V[:O[:K[:C[:B]]]]": trace walk V (0 reference, 1 default), shadow-stream overlap O (default 1),
-    # last-level walk skip K (default 1), t-cull C (default 1), binned emission B (default 1)
+    # last-level walk skip K (default 1), t-cull C (default 1), binned emission B (default 0),
+    # shadow-walk child order A (0 near first, default 1 far first): "V:O:K:C:B:A"
     variants = os.environ.get("VARIANTS", "1,1:0").split(",")
     imgs = {}
     res = {v: [] for v in variants}
@@ -25,12 +26,13 @@ def main():
     for rnd in range(3):
         for v in variants:
             parts = v.split(":")
-            parts += ["1", "1", "1", "1"][len(parts) - 1:]
+            parts += ["1", "1", "1", "0", "1"][len(parts) - 1:]
             r.set_tuning(1, int(parts[0]))
             r.set_tuning(3, int(parts[1]))
             r.set_tuning(7, int(parts[2]))  # skip the last level's walk (default 1)
             r.set_tuning(2, int(parts[3]))  # near-first + t-cull (default 1)
-            r.set_tuning(4, int(parts[4]))  # binned emission (default 1)
+            r.set_tuning(4, int(parts[4]))  # binned emission (default 0)
+            r.set_tuning(5, int(parts[5]))  # shadow walk child order (default 1: far first)
             r.render_frame_device(bm, pk, sh)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
