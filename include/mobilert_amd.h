@@ -45,8 +45,8 @@ typedef struct mrt_config {
     int32_t samplesPixel;
     int32_t samplesLight;
     int32_t repeats;
-    int32_t accelerator;  /* Shader.hpp:20-24: 1 Naive, 2 RegularGrid (served by the BVH), 3 BVH;
-                             any other value builds no accelerator (only lights are hit) */
+    int32_t accelerator;  /* Shader.hpp:20-24: 1 Naive, 2 RegularGrid, 3 BVH; any other value
+                             builds no accelerator (only lights are hit) */
     int32_t printStdOut;
     const char *objFilePath;
     const char *mtlFilePath;
@@ -106,8 +106,31 @@ typedef struct mrt_frame_stats {
     int64_t shadeLaunches;         /* k_shade launches of the frame */
 } mrt_frame_stats;
 
+/* A named byte buffer (a map_Kd texture file handed over by the Android front end). */
+typedef struct mrt_blob {
+    const char *name;     /* file name (the part after the last '/') */
+    const uint8_t *bytes;
+    int64_t size;
+} mrt_blob;
+
 const char *mrt_last_error(void);
 int mrt_create(const mrt_config *cfg, mrt_renderer **out);
+/* mrt_create with the OBJ / MTL / CAM given as text and the textures as named blobs, as the
+ * Android front end hands them over (MainActivity.readFile -> JNI readFile, JNI_layer.cpp:994-1063,
+ * then rtInitialize, :464-716, which parses them from memory).  cfg's file paths are ignored for
+ * OBJ scenes (sceneIndex outside 0-3); an empty obj fails with "OBJ file not read!" (:552-555).
+ * Such a renderer keeps a host copy of its triangles for mrt_preview_arrays. */
+int mrt_create_from_memory(const mrt_config *cfg, const char *obj, int64_t objLen, const char *mtl, int64_t mtlLen,
+                           const char *cam, int64_t camLen, const mrt_blob *textures, int32_t nTextures,
+                           mrt_renderer **out);
+/* The GL preview arrays of the Android front end (rtInitVerticesArray / rtInitColorsArray /
+ * rtInitCameraArray, JNI_layer.cpp:153-389), for a renderer made by mrt_create_from_memory:
+ * vertices[12 T] (A, B, C of every triangle in BVH order, xyz with z negated, w 1), colors[12 T]
+ * (per triangle: Kd, or Ks / Kt / Le where greater in all components, w 1, three times), camera[20]
+ * (position, direction, up, right as xyz1; then hFov, vFov in degrees, 0, 0 for a perspective
+ * camera or 0, 0, sizeH / 2, sizeV / 2 for an orthographic one).  NULL outputs are skipped.
+ * Returns T (triangles) or -1. */
+int64_t mrt_preview_arrays(const mrt_renderer *r, float *vertices, float *colors, float *camera);
 void mrt_destroy(mrt_renderer *r);
 /* bitmap: host array of width*height int32 ABGR pixels, updated in place */
 int mrt_render_frame(mrt_renderer *r, int32_t *bitmap);

@@ -17,7 +17,12 @@ EXPORTED_SYMBOLS = (
     "mrt_unpack_gathered", "mrt_stop_render", "mrt_get_sample", "mrt_get_total_casted_rays",
     "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits", "mrt_set_tuning",
     "mrt_get_tuning", "mrt_triangle_bvh", "mrt_decode_texture", "mrt_kat_slab", "mrt_kat_triangle",
-    "mrt_trace_rays", "mrt_sample_tables", "mrt_regular_grid", "mrt_grid_box_test",
+    "mrt_trace_rays", "mrt_sample_tables", "mrt_regular_grid", "mrt_grid_box_test", "mrt_create_from_memory",
+    "mrt_preview_arrays",
+    "mrt_android_read_file", "mrt_android_initialize", "mrt_android_render_into_bitmap", "mrt_android_start_render",
+    "mrt_android_stop_render", "mrt_android_finish_render", "mrt_android_state", "mrt_android_fps",
+    "mrt_android_time_renderer", "mrt_android_sample", "mrt_android_number_of_lights", "mrt_android_resize",
+    "mrt_android_vertices", "mrt_android_colors", "mrt_android_camera", "mrt_android_reset",
     "RayTrace", "stopRender",
 )
 
@@ -33,6 +38,16 @@ class MrtConfig(ctypes.Structure):
         ("device", ctypes.c_int32), ("cull", ctypes.c_int32), ("maxPathsPerPass", ctypes.c_int32),
         ("progressive", ctypes.c_int32),
     ]
+
+
+class MrtAndroidConfig(ctypes.Structure):  # include/mobilert_android.h
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "scene", "shader", "accelerator", "width", "height", "samplesPixel", "samplesLight")] + [
+        ("objFilePath", ctypes.c_char_p)]
+
+
+class MrtBlob(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("bytes", ctypes.c_char_p), ("size", ctypes.c_int64)]
 
 
 class MrtSceneInfo(ctypes.Structure):
@@ -98,6 +113,26 @@ def load_library(path=LIB_PATH):
         "mrt_decode_texture": (ctypes.c_int64, [ctypes.c_char_p, vp, vp]),
         "mrt_regular_grid": (ctypes.c_int64, [vp, ctypes.c_int32, vp, vp, vp]),
         "mrt_grid_box_test": (ctypes.c_int, [ctypes.c_int32, vp, vp]),
+        "mrt_create_from_memory": (ctypes.c_int, [P(MrtConfig), ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p,
+                                                  ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64, vp, ctypes.c_int32,
+                                                  P(vp)]),
+        "mrt_preview_arrays": (ctypes.c_int64, [vp, vp, vp, vp]),
+        "mrt_android_read_file": (None, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
+        "mrt_android_initialize": (ctypes.c_int32, [P(MrtAndroidConfig)]),
+        "mrt_android_render_into_bitmap": (None, [vp, ctypes.c_int32]),
+        "mrt_android_start_render": (None, [ctypes.c_int32]),
+        "mrt_android_stop_render": (None, [ctypes.c_int32]),
+        "mrt_android_finish_render": (None, []),
+        "mrt_android_state": (ctypes.c_int32, []),
+        "mrt_android_fps": (ctypes.c_float, []),
+        "mrt_android_time_renderer": (ctypes.c_int64, []),
+        "mrt_android_sample": (ctypes.c_int32, []),
+        "mrt_android_number_of_lights": (ctypes.c_int32, []),
+        "mrt_android_resize": (ctypes.c_int32, [ctypes.c_int32]),
+        "mrt_android_vertices": (ctypes.c_int64, [vp]),
+        "mrt_android_colors": (ctypes.c_int64, [vp]),
+        "mrt_android_camera": (ctypes.c_int64, [vp]),
+        "mrt_android_reset": (None, []),
         "mrt_sample_tables": (ctypes.c_int, [vp, vp, vp]),
         "mrt_kat_slab": (ctypes.c_int, [vp, vp, vp, ctypes.c_int32, vp]),
         "mrt_kat_triangle": (ctypes.c_int, [vp, vp, vp, ctypes.c_int32, vp, vp]),

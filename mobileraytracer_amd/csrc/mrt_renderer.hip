@@ -11,6 +11,8 @@
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <map>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -133,6 +135,12 @@ struct mrt_renderer {
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
 
+    // host copies for the GL preview of the Android front end (mrt_preview_arrays; kept only for
+    // renderers made by mrt_create_from_memory): triangles in BVH order and the materials
+    bool keepHost = false;
+    std::vector<mrt::HTriangle> hostTris;
+    std::vector<mrt::HMaterial> hostMats;
+
     // state (Renderer.hpp:30-40)
     std::atomic<bool> stopFlag{false};
     std::atomic<int32_t> sample{0};
@@ -230,6 +238,10 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     r->maxBvhDepth = std::max({r->triDepth, bvhDepth(pn), bvhDepth(sn)});
     r->stackNeed = r->maxBvhDepth + 2;
 
+    if (r->keepHost) {
+        r->hostTris = sc.triangles;  // BVH order, as Shader::getTriangles returns them
+        r->hostMats = sc.materials;
+    }
     std::vector<GNode> g;
     DScene& d = r->ds;
     const std::vector<uint32_t> cones = triangleConeWords(tn, sc.triangles);
@@ -682,9 +694,17 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
     r->totalRays.fetch_add(fs.rays + fs.shadowRays);
 }
 
-mrt_renderer* createRenderer(const mrt_config* cfg) {
+// An OBJ scene handed over as text (the Android front end reads the files through descriptors,
+// JNI_layer.cpp:994-1063) with its map_Kd textures by file name.
+struct MemScene {
+    std::string obj, mtl, cam;
+    std::map<std::string, std::string> textures;
+};
+
+mrt_renderer* createRenderer(const mrt_config* cfg, const MemScene* mem = nullptr) {
     using namespace mrt;
     auto r = std::make_unique<mrt_renderer>();
+    r->keepHost = mem != nullptr;
     r->cfg = *cfg;
     r->objPath = cfg->objFilePath ? cfg->objFilePath : "";
     r->mtlPath = cfg->mtlFilePath ? cfg->mtlFilePath : "";
@@ -718,6 +738,18 @@ mrt_renderer* createRenderer(const mrt_config* cfg) {
         sc = builtinScene(cfg->sceneIndex);
         r->cam = builtinCamera(cfg->sceneIndex, ratio);
         r->maxPoint = builtinMaxPoint(cfg->sceneIndex);
+    } else if (mem != nullptr) {
+        if (mem->obj.empty()) throw std::runtime_error("OBJ file not read!");  // JNI_layer.cpp:552-555
+        std::string err;
+        std::istringstream obj(mem->obj), mtl(mem->mtl), cam(mem->cam);
+        const TextureSource textures = [mem](const std::string& name, HTexture* tex) {
+            const auto it = mem->textures.find(name.substr(name.find_last_of('/') + 1));
+            if (it == mem->textures.end()) return false;
+            std::string terr;
+            return decodePng(std::vector<uint8_t>(it->second.begin(), it->second.end()), tex, &terr);
+        };
+        if (!loadObjStreams(obj, mem->mtl.empty() ? nullptr : &mtl, textures, &sc, &err)) throw std::runtime_error(err);
+        if (!loadCameraStream(cam, ratio, &r->cam, &err, "camera definition")) throw std::runtime_error(err);
     } else {
         std::string err;
         if (!loadObjScene(r->objPath, r->mtlPath, &sc, &err)) throw std::runtime_error(err);
@@ -757,6 +789,83 @@ int mrt_create(const mrt_config* cfg, mrt_renderer** out) {
     return guarded([&] { *out = createRenderer(cfg); });
 }
 
+int mrt_create_from_memory(const mrt_config* cfg, const char* obj, int64_t objLen, const char* mtl, int64_t mtlLen,
+                           const char* cam, int64_t camLen, const mrt_blob* textures, int32_t nTextures,
+                           mrt_renderer** out) {
+    *out = nullptr;
+    return guarded([&] {
+        MemScene m;
+        if (obj != nullptr && objLen > 0) m.obj.assign(obj, static_cast<size_t>(objLen));
+        if (mtl != nullptr && mtlLen > 0) m.mtl.assign(mtl, static_cast<size_t>(mtlLen));
+        if (cam != nullptr && camLen > 0) m.cam.assign(cam, static_cast<size_t>(camLen));
+        for (int32_t i = 0; i < nTextures; ++i) {
+            const mrt_blob& b = textures[i];
+            m.textures[b.name != nullptr ? b.name : ""].assign(reinterpret_cast<const char*>(b.bytes),
+                                                                static_cast<size_t>(b.size));
+        }
+        *out = createRenderer(cfg, &m);
+    });
+}
+
+int64_t mrt_preview_arrays(const mrt_renderer* r, float* vertices, float* colors, float* camera) {
+    using namespace mrt;
+    if (!r->keepHost) {
+        gLastError = "preview arrays: the renderer keeps no host scene (create it with mrt_create_from_memory)";
+        return -1;
+    }
+    size_t i = 0, j = 0;
+    for (const HTriangle& t : r->hostTris) {
+        // rtInitVerticesArray (JNI_layer.cpp:243-311): A, A + AB, A + AC with z negated for GL
+        const v3 a = t.A, b = v3{a.x + t.AB.x, a.y + t.AB.y, a.z + t.AB.z}, c = v3{a.x + t.AC.x, a.y + t.AC.y, a.z + t.AC.z};
+        if (vertices != nullptr)
+            for (const v3& p : {a, b, c}) {
+                vertices[i++] = p.x;
+                vertices[i++] = p.y;
+                vertices[i++] = -p.z;
+                vertices[i++] = 1.0F;
+            }
+        // rtInitColorsArray (:314-389): Kd, replaced by Ks / Kt / Le where each is greater in all
+        // three components
+        if (colors != nullptr) {
+            HMaterial m;
+            if (t.mat >= 0) m = r->hostMats[static_cast<size_t>(t.mat)];
+            auto greater = [](v3 x, v3 y) { return x.x > y.x && x.y > y.y && x.z > y.z; };
+            v3 col = m.Kd;
+            col = greater(m.Ks, col) ? m.Ks : col;
+            col = greater(m.Kt, col) ? m.Kt : col;
+            col = greater(m.Le, col) ? m.Le : col;
+            for (int k = 0; k < 3; ++k) {
+                colors[j++] = col.x;
+                colors[j++] = col.y;
+                colors[j++] = col.z;
+                colors[j++] = 1.0F;
+            }
+        }
+    }
+    if (camera != nullptr) {  // rtInitCameraArray (:153-240)
+        const GCamera& c = r->cam;
+        const v3 rows[4] = {c.position, c.direction, c.up, c.right};
+        for (int k = 0; k < 4; ++k) {
+            camera[4 * k] = rows[k].x;
+            camera[4 * k + 1] = rows[k].y;
+            camera[4 * k + 2] = rows[k].z;
+            camera[4 * k + 3] = 1.0F;
+        }
+        if (c.kind == 0) {  // Perspective::getHFov / getVFov in degrees (Camera.cpp:50-53)
+            camera[16] = (c.hFov / kPi) * 180.0F;
+            camera[17] = (c.vFov / kPi) * 180.0F;
+            camera[18] = 0.0F;
+            camera[19] = 0.0F;
+        } else {  // Orthographic::getSizeH / getSizeV (the half sizes)
+            camera[16] = 0.0F;
+            camera[17] = 0.0F;
+            camera[18] = c.hFov;
+            camera[19] = c.vFov;
+        }
+    }
+    return static_cast<int64_t>(r->hostTris.size());
+}
+
 void mrt_destroy(mrt_renderer* r) {
     if (r != nullptr) {
         (void)hipStreamSynchronize(r->stream);
@@ -766,6 +875,7 @@ void mrt_destroy(mrt_renderer* r) {
 
 int mrt_render_frame(mrt_renderer* r, int32_t* bitmap) {
     return guarded([&] {
+        MRT_HIP(hipSetDevice(r->device));  // the calling thread may not be the one that created r
         const size_t n = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
         MRT_HIP(hipMemcpyAsync(r->dBitmap, bitmap, n * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
         renderFrameDevice(r, r->dBitmap, nullptr, r->stream, bitmap);
@@ -774,6 +884,7 @@ int mrt_render_frame(mrt_renderer* r, int32_t* bitmap) {
 
 int mrt_render_frame_device(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, void* stream) {
     return guarded([&] {
+        MRT_HIP(hipSetDevice(r->device));
         hipStream_t st = stream != nullptr ? static_cast<hipStream_t>(stream) : r->stream;
         renderFrameDevice(r, dBitmap, dPacked, st);
     });

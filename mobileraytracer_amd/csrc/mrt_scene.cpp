@@ -276,6 +276,10 @@ bool loadCameraFile(const std::string& path, float ratio, GCamera* out, std::str
         *err = "cannot open camera file " + path;
         return false;
     }
+    return loadCameraStream(f, ratio, out, err, path);
+}
+
+bool loadCameraStream(std::istream& f, float ratio, GCamera* out, std::string* err, const std::string& path) {
     std::string line;
     bool perspective = false;
     while (std::getline(f, line)) {
@@ -483,17 +487,29 @@ v3 normalizeColor(v3 c) {
 }  // namespace
 
 bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene* scene, std::string* err) {
-    std::vector<RawMat> mats;
-    std::unordered_map<std::string, int> names;
-    {
-        std::ifstream mf(mtlPath);
-        if (mf) parseMtl(mf, &mats, &names);
-    }
+    std::ifstream mf(mtlPath);
     std::ifstream f(objPath);
     if (!f) {
         *err = "cannot open OBJ file " + objPath;
         return false;
     }
+    // map_Kd textures are read from the OBJ's directory (the reference reads filePath + texname,
+    // filePath being the OBJ's directory)
+    const std::string objDir = objPath.find('/') == std::string::npos ? std::string() : objPath.substr(0, objPath.rfind('/') + 1);
+    return loadObjStreams(f, mf ? &mf : nullptr,
+                          [&objDir](const std::string& name, HTexture* tex) {
+                              std::string terr;
+                              return loadTextureFile(objDir + name, tex, &terr);
+                          },
+                          scene, err);
+}
+
+bool loadObjStreams(std::istream& f, std::istream* mtl, const TextureSource& textureSource, HScene* scene,
+                    std::string* err) {
+    (void)err;
+    std::vector<RawMat> mats;
+    std::unordered_map<std::string, int> names;
+    if (mtl != nullptr) parseMtl(*mtl, &mats, &names);
     std::vector<float> vs, vns, vts, cols;
     vs.reserve(1 << 20);
     cols.reserve(1 << 20);
@@ -574,17 +590,14 @@ bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene
         }
     }
 
-    // map_Kd textures, loaded once per file name (OBJLoader.cpp:224-242) from the OBJ's directory
-    // (the reference reads filePath + texname, filePath being the OBJ's directory)
+    // map_Kd textures, loaded once per file name (OBJLoader.cpp:224-242)
     std::unordered_map<std::string, int32_t> texCache;
-    const std::string objDir = objPath.find('/') == std::string::npos ? std::string() : objPath.substr(0, objPath.rfind('/') + 1);
     auto textureOf = [&](const std::string& name) -> int32_t {
         auto it = texCache.find(name);
         if (it != texCache.end()) return it->second;
         HTexture tex;
-        std::string terr;
         int32_t id = -1;
-        if (loadTextureFile(objDir + name, &tex, &terr)) {  // Texture::isValid (Texture.cpp:137-139)
+        if (textureSource(name, &tex)) {  // Texture::isValid (Texture.cpp:137-139)
             id = static_cast<int32_t>(scene->textures.size());
             scene->textures.push_back(std::move(tex));
         }

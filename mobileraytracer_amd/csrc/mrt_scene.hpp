@@ -9,6 +9,8 @@
 
 #include "mrt_common.hpp"
 
+#include <functional>
+#include <istream>
 #include <string>
 #include <vector>
 
@@ -99,8 +101,14 @@ GCamera cornellBoxCamera(float ratio);                        // Scenes.cpp:139-
 GCamera makePerspective(v3 position, v3 lookAt, v3 up, float hFovDeg, float vFovDeg);
 // CameraFactory.cpp + PerspectiveLoader.cpp:18-64 (position.x negated, hFov = fov.u * ratio)
 bool loadCameraFile(const std::string& path, float ratio, GCamera* out, std::string* err);
+// the same from a stream (the Android front end hands the .cam text over, JNI_layer.cpp:994-1063)
+bool loadCameraStream(std::istream& in, float ratio, GCamera* out, std::string* err, const std::string& name = "");
 // OBJLoader.cpp:18-497 (+ tinyobjloader v1.0.7 parsing / fan triangulation); fills in file order
 bool loadObjScene(const std::string& objPath, const std::string& mtlPath, HScene* scene, std::string* err);
+// the same from streams; map_Kd textures come from textureSource(name) (false: not available)
+using TextureSource = std::function<bool(const std::string&, HTexture*)>;
+bool loadObjStreams(std::istream& obj, std::istream* mtl, const TextureSource& textureSource, HScene* scene,
+                    std::string* err);
 
 // ---- acceleration structure ------------------------------------------------------------
 // libstdc++ std::partition (bidirectional overload), restated so the build is pinned.

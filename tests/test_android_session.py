@@ -1,0 +1,196 @@
+"""The Android front end's native session (include/mobilert_android.h, csrc/mrt_android.cpp):
+the state machine and data path behind the JNI exports of mobileraytracer_amd/jni/mrt_jni.cpp,
+which keep the names of app/System_dependent/Android_JNI/JNI_layer.cpp.  The sequence the app
+runs - readFile for the OBJ / MTL / CAM (and textures), rtInitialize, rtStartRender,
+rtRenderIntoBitmap, polling rtGetState / rtGetSample, rtStopRender / rtFinishRender, the GL
+preview arrays - is driven from Python and checked against the oracle (bitmaps bit-exact) and
+against the scene files (preview arrays)."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def test_resize_rounds_down_to_tiles():
+    """rtResize: roundDownToMultipleOf(size, 16) with the reference's rest > 1 rule (Utils.cpp:26-31)."""
+    from mobileraytracer_amd import android as A
+    assert [A.resize(s) for s in (100, 97, 96, 33, 16, 15, 1, 0)] == [96, 97, 96, 33, 16, 0, 1, 0]
+
+
+def test_idle_session_getters():
+    from mobileraytracer_amd import android as A
+    A.reset()
+    assert A.state() == A.IDLE and A.sample() == 0 and A.number_of_lights() == 0
+    assert len(A.vertices()) == 0 and len(A.camera()) == 0
+
+
+def _wait_idle(A, timeout=60.0):
+    t0 = time.time()
+    while A.state() != A.IDLE:
+        assert time.time() - t0 < timeout, "render thread did not finish"
+        time.sleep(0.005)
+
+
+def _scene_files(name):
+    from mobileraytracer_amd import scenes
+    return {"water": scenes.cornell_water, "teapot": scenes.teapot}[name]()
+
+
+def _render_session(A, scene, shader, width, height, spp=1, files=None, textures=()):
+    A.reset()
+    obj = ""
+    if files is not None:
+        obj, mtl, cam = files
+        for p in (obj, mtl, cam) + tuple(textures):
+            A.read_file(p)
+    n = A.initialize(scene, shader, 3, width, height, spp, 1, obj)
+    assert n > 0, n
+    pixels = np.zeros(width * height, np.int32)
+    A.start_render(False)
+    assert A.state() == A.BUSY
+    A.render_into_bitmap(pixels)
+    _wait_idle(A)
+    return n, pixels
+
+
+@pytest.mark.gpu
+def test_obj_scene_from_memory_matches_oracle(oracle_mod):
+    """CornellBox-Water handed over as file contents (readFile), Whitted 64 x 64: the bitmap the
+    render thread fills equals the oracle's, the primitive count is rtInitialize's
+    triangles + spheres + planes, two lights, one sample."""
+    from mobileraytracer_amd import android as A
+    files = _scene_files("water")
+    n, pixels = _render_session(A, -1, 1, 64, 64, files=files)
+    ref, _ = oracle_mod.Oracle(64, 64, 1, -1, obj=files[0], mtl=files[1], cam=files[2]).render(threads=4)
+    assert np.array_equal(pixels, ref)
+    counts = oracle_mod.Oracle(64, 64, 1, -1, obj=files[0], mtl=files[1], cam=files[2]).counts()
+    assert n == counts["triangles"] + counts["spheres"] + counts["planes"]
+    assert A.number_of_lights() == counts["lights"] == 2
+    assert A.sample() == 1 and A.fps() > 0.0 and A.time_renderer() >= 0
+
+
+@pytest.mark.gpu
+def test_textured_scene_from_memory_matches_oracle(oracle_mod):
+    """The teapot's map_Kd texture arrives through readFile like the scene files (texturesCache_)."""
+    from mobileraytracer_amd import android as A
+    files = _scene_files("teapot")
+    tex = os.path.join(os.path.dirname(files[0]), "default.png")
+    assert os.path.exists(tex)
+    _, pixels = _render_session(A, -1, 1, 64, 64, files=files, textures=(tex,))
+    ref, _ = oracle_mod.Oracle(64, 64, 1, -1, obj=files[0], mtl=files[1], cam=files[2]).render(threads=4)
+    assert np.array_equal(pixels, ref)
+
+
+@pytest.mark.gpu
+def test_builtin_scene_pathtracer_matches_oracle(oracle_mod):
+    from mobileraytracer_amd import android as A
+    n, pixels = _render_session(A, 0, 2, 64, 64, spp=2)
+    ref, _ = oracle_mod.Oracle(64, 64, 2, 0, 2).render(threads=4)
+    assert np.array_equal(pixels, ref)
+    assert A.sample() == 2
+
+
+@pytest.mark.gpu
+def test_obj_not_read_is_an_error():
+    """rtInitialize of an OBJ scene with no OBJ handed over: "OBJ file not read!" (:552-555), -2."""
+    from mobileraytracer_amd import android as A
+    from mobileraytracer_amd import _native
+    A.reset()
+    assert A.initialize(-1, 1, 3, 64, 64) == -2
+    assert b"OBJ file not read" in _native.lib().mrt_last_error()
+    assert A.state() == A.IDLE
+
+
+def _parse_obj_triangles(obj, mtl):
+    """The scene file's triangles as the reference's loader makes them (fan triangulation, x
+    negated, emissive materials become lights) and the MTL's coefficient values."""
+    verts, tris, emissive, cur, mat_vals, name = [], [], set(), None, set(), None
+    for line in open(mtl):
+        t = line.split()
+        if not t:
+            continue
+        if t[0] == "newmtl":
+            name = t[1]
+        elif t[0] in ("Kd", "Ks", "Tf", "Kt") and len(t) >= 4:
+            mat_vals.add(tuple(np.float32(x) for x in t[1:4]))
+        elif t[0] == "Ke" and any(float(x) > 0 for x in t[1:4]):
+            emissive.add(name)
+    for line in open(obj):
+        t = line.split()
+        if not t:
+            continue
+        if t[0] == "v":
+            verts.append([-np.float32(t[1]), np.float32(t[2]), np.float32(t[3])])
+        elif t[0] == "usemtl":
+            cur = t[1]
+        elif t[0] == "f" and cur not in emissive:
+            idx = [int(x.split("/")[0]) for x in t[1:]]
+            idx = [i - 1 if i > 0 else len(verts) + i for i in idx]
+            for k in range(2, len(idx)):
+                tris.append((idx[0], idx[k - 1], idx[k]))
+    return np.array(verts, np.float32), tris, mat_vals
+
+
+@pytest.mark.gpu
+def test_preview_arrays(oracle_mod):
+    """rtInitVerticesArray / rtInitColorsArray / rtInitCameraArray: the triangles in BVH order as
+    A, A + AB, A + AC with z negated (float32 arithmetic), per-triangle colours from the MTL, the
+    camera of the .cam file (position, direction, up, right, fov in degrees)."""
+    import mobileraytracer_amd as m
+    from mobileraytracer_amd import android as A
+    files = _scene_files("water")
+    _render_session(A, -1, 1, 64, 48, files=files)
+    verts, tris, mat_vals = _parse_obj_triangles(files[0], files[1])
+    cfg = m.Config(width=64, height=48, sceneIndex=-1, objFilePath=files[0], mtlFilePath=files[1], camFilePath=files[2])
+    _, _, _, order = m.triangle_bvh(cfg)
+    v = A.vertices().reshape(-1, 3, 4)
+    assert len(v) == len(tris) == len(order)
+    T = np.array(tris)[order]
+    a, b, c = verts[T[:, 0]], verts[T[:, 1]], verts[T[:, 2]]
+    ab, ac = b - a, c - a  # the Triangle's AB / AC (Triangle.cpp:14-26), then A + AB, A + AC
+    exp = np.stack([a, a + ab, a + ac], 1)
+    exp[..., 2] = -exp[..., 2]
+    assert np.array_equal(v[..., :3], exp) and np.all(v[..., 3] == 1.0)
+    col = A.colors().reshape(-1, 3, 4)
+    assert len(col) == len(tris) and np.all(col[..., 3] == 1.0)
+    assert np.all(col[:, 0] == col[:, 1]) and np.all(col[:, 0] == col[:, 2])
+    assert {tuple(x) for x in col[:, 0, :3]} <= mat_vals | {(0.0, 0.0, 0.0)}
+    cam = A.camera()
+    ref = oracle_mod.kat_camera(files[2], 64 / 48)
+    assert np.array_equal(cam[:16].reshape(4, 4)[:, :3],
+                          np.array([ref["position"], ref["direction"], ref["up"], ref["right"]], np.float32))
+    assert np.array_equal(cam[16:18], np.array([ref["hfov"], ref["vfov"]], np.float32)) and np.all(cam[18:] == 0)
+
+
+@pytest.mark.gpu
+def test_stop_and_finish_render():
+    """rtStopRender during a long progressive frame: the render thread ends early (STOPPED, then
+    IDLE) with fewer samples; rtFinishRender resets fps / time; a new rtStartRender(wait) does not
+    block once the previous render finished."""
+    from mobileraytracer_amd import android as A
+    from mobileraytracer_amd import scenes
+    files = scenes.conference()
+    A.reset()
+    for p in files:
+        A.read_file(p)
+    assert A.initialize(-1, 2, 3, 320, 240, 64, 1, files[0]) > 0
+    pixels = np.zeros(320 * 240, np.int32)
+    A.start_render(True)
+    A.render_into_bitmap(pixels)
+    t0 = time.time()
+    while A.sample() < 1 and time.time() - t0 < 30:
+        time.sleep(0.001)
+    A.stop_render(True)
+    assert A.state() in (A.STOPPED, A.IDLE)
+    _wait_idle(A)
+    assert 1 <= A.sample() < 64
+    assert len(np.unique(pixels)) > 1
+    A.finish_render()
+    assert A.state() == A.IDLE and A.fps() == 0.0 and A.time_renderer() == 0
+    A.start_render(True)  # finishedRendering_ is set: returns at once
+    assert A.state() == A.BUSY
+    A.finish_render()
+    A.reset()
