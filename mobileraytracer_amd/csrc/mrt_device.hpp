@@ -32,7 +32,10 @@ struct DScene {
     // 2^20 x {shader (Shader.cpp:23), sampler (StaticHaltonSeq.cpp) shuffled Halton values,
     // cos and sin of 2 pi * shader entry by the host libm (fillHemisphereTrig)}
     const float4* tables;
-    GRoot triRoot, planeRoot, sphereRoot;
+    // triRoot: the walk tree (the reference leaves regrouped, rebuildOverLeaves); triRootRef: the
+    // reference tree (BVH.hpp), in the same node array - for rays with a non-finite 1/d, whose slab
+    // NaNs break the leaf-box reachability argument, and for the per-wave reference walk
+    GRoot triRoot, triRootRef, planeRoot, sphereRoot;
     int32_t nLights;
     int32_t nMats;
     int32_t cull;              // walk 1's cull mode: 0 none, 1 fast, 2 certified (mrt_trace_ww.hpp)
@@ -406,7 +409,7 @@ __device__ __forceinline__ Best closestHit(const DScene& s, v3 o, v3 d, uint32_t
     Best b{kRayLengthMax, 0.0F, 0.0F, kNoPrim};
     traverse<kPlane, false>(s, s.planeNodes, s.planeRoot, o, d, inv, src, &b, st, cnt);
     traverse<kSphere, false>(s, s.sphereNodes, s.sphereRoot, o, d, inv, src, &b, st, cnt);
-    traverse<kTriangle, false>(s, s.triNodes, s.triRoot, o, d, inv, src, &b, st, cnt);
+    traverse<kTriangle, false>(s, s.triNodes, s.triRootRef, o, d, inv, src, &b, st, cnt);
     for (int j = 0; j < s.nLights; ++j) {  // Shader.cpp:166-171, AreaLight.cpp:32-41
         const float4* l = s.lights + 4 * j;
         const float4 a4 = l[0];
@@ -432,7 +435,7 @@ __device__ __forceinline__ bool anyHit(const DScene& s, v3 o, v3 d, uint32_t src
     Best b{dist, 0.0F, 0.0F, kNoPrim};
     if (traverse<kPlane, true>(s, s.planeNodes, s.planeRoot, o, d, inv, src, &b, st, cnt)) return true;
     if (traverse<kSphere, true>(s, s.sphereNodes, s.sphereRoot, o, d, inv, src, &b, st, cnt)) return true;
-    return traverse<kTriangle, true>(s, s.triNodes, s.triRoot, o, d, inv, src, &b, st, cnt);
+    return traverse<kTriangle, true>(s, s.triNodes, s.triRootRef, o, d, inv, src, &b, st, cnt);
 }
 
 }  // namespace mrt

@@ -228,13 +228,19 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     std::vector<HBVHNode> pn = buildBVH(&sc.planes, &r->planeOrder);
     std::vector<HBVHNode> sn = buildBVH(&sc.spheres, &r->sphereOrder);
     std::vector<HBVHNode> tn = buildBVH(&sc.triangles, &r->triOrder);
+    // the walk tree: the reference leaves regrouped by a full-sweep SAH (rebuildOverLeaves; the
+    // reference tree itself with MOBILERT_WALK_TREE=0).  Rays with a non-finite 1/d and the
+    // per-wave reference walk use the reference tree, appended after it in the same node array.
+    const char* walkTree = std::getenv("MOBILERT_WALK_TREE");
+    const bool regroup = walkTree == nullptr || std::atoi(walkTree) != 0;
+    const std::vector<HBVHNode> wn = regroup ? rebuildOverLeaves(tn, 2) : tn;
     r->nTri = static_cast<int64_t>(sc.triangles.size());
     r->nPlanes = static_cast<int64_t>(sc.planes.size());
     r->nSpheres = static_cast<int64_t>(sc.spheres.size());
     r->nLights = static_cast<int64_t>(sc.lights.size());
     r->nMats = static_cast<int64_t>(sc.materials.size());
     r->nTriNodes = static_cast<int64_t>(tn.size());
-    r->triDepth = bvhDepth(tn);
+    r->triDepth = std::max(bvhDepth(tn), bvhDepth(wn));
     r->maxBvhDepth = std::max({r->triDepth, bvhDepth(pn), bvhDepth(sn)});
     r->stackNeed = r->maxBvhDepth + 2;
 
@@ -244,8 +250,21 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     }
     std::vector<GNode> g;
     DScene& d = r->ds;
-    const std::vector<uint32_t> cones = triangleConeWords(tn, sc.triangles);
-    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop, &cones);
+    // cull words (certified mode) for the reference tree only: that mode walks it for every ray
+    const std::vector<uint32_t> conesRef = triangleConeWords(tn, sc.triangles);
+    toDeviceBVH(wn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop, regroup ? nullptr : &conesRef);
+    d.triRootRef = d.triRoot;
+    if (regroup) {
+        std::vector<GNode> gr;
+        toDeviceBVH(tn, sc.triangles.size(), &gr, &d.triRootRef, 0, nullptr, &conesRef);
+        const int32_t off = static_cast<int32_t>(g.size());
+        for (GNode& n : gr) {
+            if (n.refL >= 0) n.refL += off;
+            if (n.refR >= 0) n.refR += off;
+        }
+        if (d.triRootRef.ref >= 0 && d.triRootRef.count > 0) d.triRootRef.ref += off;
+        g.insert(g.end(), gr.begin(), gr.end());
+    }
     d.triNodes = r->sceneMem.upload(g, st);
     toDeviceBVH(pn, sc.planes.size(), &g, &d.planeRoot);
     d.planeNodes = r->sceneMem.upload(g, st);

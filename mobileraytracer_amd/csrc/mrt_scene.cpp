@@ -1022,6 +1022,101 @@ uint32_t coneWord(const std::vector<HTriangle>& tris, size_t lo, size_t hi) {
 }
 }  // namespace
 
+// A second topology over the reference tree's leaves ("walk tree").
+// Reachability of a triangle in the reference walk is its leaf box passing the slab test: every
+// ancestor box contains the leaf box coordinatewise, and for a ray with finite 1/d each computed
+// slab interval grows monotonically with the box (correctly rounded - and * are monotone), so an
+// ancestor passes whenever the leaf does (BVH.hpp:327-384 tests the root, then child boxes).  Any
+// tree whose leaves are the reference leaves (same primitive ranges, same boxes) and whose inner
+// boxes are exact unions of the leaf boxes below therefore reaches exactly the reference's
+// triangles for such rays.  This one is grouped by a full-sweep SAH over the leaf centroids
+// (the reference groups triangles with 10 centroid buckets, BVH.hpp:197-240).
+std::vector<HBVHNode> rebuildOverLeaves(const std::vector<HBVHNode>& ref, int weight) {
+    if (ref.size() <= 1) return ref;
+    struct Leaf {
+        HAABB box;
+        v3 c;
+        int32_t first, count;
+    };
+    std::vector<Leaf> leaves;
+    for (const HBVHNode& n : ref) {
+        if (n.numPrimitives > 0) {
+            const v3 c{0.5F * (n.box.mn.x + n.box.mx.x), 0.5F * (n.box.mn.y + n.box.mx.y), 0.5F * (n.box.mn.z + n.box.mx.z)};
+            leaves.push_back(Leaf{n.box, c, n.indexOffset, n.numPrimitives});
+        }
+    }
+    const size_t n = leaves.size();
+    auto unite = [](const HAABB& a, const HAABB& b) { return HAABB{vmin(a.mn, b.mn), vmax(a.mx, b.mx)}; };
+    auto area = [](const HAABB& b) {
+        const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,
+                     dz = static_cast<double>(b.mx.z) - b.mn.z;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    };
+    std::vector<int32_t> idx(n);
+    for (size_t i = 0; i < n; ++i) idx[i] = static_cast<int32_t>(i);
+    std::vector<HBVHNode> out(1);
+    struct Task {
+        int32_t node, b, e;
+    };
+    std::vector<Task> st{{0, 0, static_cast<int32_t>(n)}};
+    std::vector<double> rightArea(n + 1);
+    std::vector<int32_t> tmp(n);
+    while (!st.empty()) {
+        const Task t = st.back();
+        st.pop_back();
+        HAABB box = leaves[static_cast<size_t>(idx[static_cast<size_t>(t.b)])].box;
+        for (int32_t i = t.b + 1; i < t.e; ++i) box = unite(box, leaves[static_cast<size_t>(idx[static_cast<size_t>(i)])].box);
+        if (t.e - t.b == 1) {
+            const Leaf& l = leaves[static_cast<size_t>(idx[static_cast<size_t>(t.b)])];
+            out[static_cast<size_t>(t.node)] = HBVHNode{l.box, l.first, l.count};
+            continue;
+        }
+        double best = 1e300;
+        int bestAxis = 0;
+        int32_t bestSplit = t.b + (t.e - t.b) / 2;
+        for (int axis = 0; axis < 3; ++axis) {
+            std::copy(idx.begin() + t.b, idx.begin() + t.e, tmp.begin() + t.b);
+            std::stable_sort(tmp.begin() + t.b, tmp.begin() + t.e, [&](int32_t x, int32_t y) {
+                return comp(leaves[static_cast<size_t>(x)].c, axis) < comp(leaves[static_cast<size_t>(y)].c, axis);
+            });
+            HAABB acc = leaves[static_cast<size_t>(tmp[static_cast<size_t>(t.e - 1)])].box;
+            rightArea[static_cast<size_t>(t.e - 1)] = area(acc);
+            for (int32_t i = t.e - 2; i > t.b; --i) {
+                acc = unite(acc, leaves[static_cast<size_t>(tmp[static_cast<size_t>(i)])].box);
+                rightArea[static_cast<size_t>(i)] = area(acc);
+            }
+            // weights: 0 one per leaf, 1 the leaf's triangle count, 2 one + count
+            auto wt = [&](int32_t i) {
+                const int32_t c = leaves[static_cast<size_t>(tmp[static_cast<size_t>(i)])].count;
+                return weight == 0 ? 1.0 : (weight == 1 ? static_cast<double>(c) : 1.0 + c);
+            };
+            double wTotal = 0.0;
+            for (int32_t i = t.b; i < t.e; ++i) wTotal += wt(i);
+            double wLeft = 0.0;
+            acc = leaves[static_cast<size_t>(tmp[static_cast<size_t>(t.b)])].box;
+            for (int32_t i = t.b + 1; i < t.e; ++i) {  // split: [b, i) | [i, e)
+                wLeft += wt(i - 1);
+                const double cost = area(acc) * wLeft + rightArea[static_cast<size_t>(i)] * (wTotal - wLeft);
+                if (cost < best) {
+                    best = cost;
+                    bestAxis = axis;
+                    bestSplit = i;
+                }
+                acc = unite(acc, leaves[static_cast<size_t>(tmp[static_cast<size_t>(i)])].box);
+            }
+        }
+        std::stable_sort(idx.begin() + t.b, idx.begin() + t.e, [&](int32_t x, int32_t y) {
+            return comp(leaves[static_cast<size_t>(x)].c, bestAxis) < comp(leaves[static_cast<size_t>(y)].c, bestAxis);
+        });
+        const int32_t left = static_cast<int32_t>(out.size());
+        out.resize(out.size() + 2);
+        out[static_cast<size_t>(t.node)] = HBVHNode{box, left, 0};
+        st.push_back({left + 1, bestSplit, t.e});
+        st.push_back({left, t.b, bestSplit});
+    }
+    return out;
+}
+
 std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris) {
     std::vector<uint32_t> out(nodes.size(), kConeNever);
     if (nodes.empty() || tris.empty()) return out;

@@ -146,6 +146,10 @@ std::vector<HBVHNode> buildBVH(std::vector<T>* prims, std::vector<int32_t>* orde
 // cones: the cull word of every reference node (triangleConeWords), or null (never culled).
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
                  int topCount = 0, int* topPlaced = nullptr, const std::vector<uint32_t>* cones = nullptr);
+// A tree over the same leaves (primitive ranges and boxes) as the reference tree `ref`, grouped
+// by a full-sweep SAH; its inner boxes are exact unions of the leaf boxes (reference numbering:
+// node 0 the root, an inner node's children at indexOffset and indexOffset + 1).
+std::vector<HBVHNode> rebuildOverLeaves(const std::vector<HBVHNode>& ref, int weight = 0);
 // The cull word (mrt_common.hpp) of every node of a triangle BVH built by buildBVH over tris
 // (already in BVH order): the normal-line cone and the conditioning bound K of its triangles.
 std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris);

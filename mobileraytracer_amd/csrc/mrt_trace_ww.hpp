@@ -344,10 +344,12 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     bcode = b.code;
                     if (rayIdx >= 0) {
                         float te;
-                        const GRoot& r = s.triRoot;
+                        const GRoot& r = s.triRoot;  // both trees have the same root box
                         if (r.count > 0 &&
                             slab(r.bmin[0], r.bmin[1], r.bmin[2], r.bmax[0], r.bmax[1], r.bmax[2], o, inv, &te)) {
-                            ref = r.ref;
+                            // a non-finite 1/d, and the certified cull (its bounds are the
+                            // reference nodes'), walk the reference tree (DScene::triRootRef)
+                            ref = finiteInv(inv) && kCull != kCullCertified ? r.ref : s.triRootRef.ref;
                             if (ref < 0) {  // the root is a leaf
                                 leaf = ref;
                                 ref = kRefDone;

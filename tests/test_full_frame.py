@@ -148,3 +148,59 @@ def test_random_rays_all_cull_modes(oracle_mod):
     assert np.array_equal(ok, ref_hits[0][sel]) and np.array_equal(oi, ref_hits[1][sel])
     assert np.array_equal(ot.view(np.int32), ref_hits[2][sel].view(np.int32))
     assert np.array_equal(occ, ref_occ[sel])
+
+
+@pytest.mark.parametrize("scene", ["conference", "water"])
+def test_walk_tree_rays_with_zero_direction_components(oracle_mod, scene):
+    """The walk tree regroups the reference leaves (rebuildOverLeaves); it reaches exactly the
+    reference's triangles for rays with a finite 1/d (leaf-box reachability).
+    Rays with a zero direction component (1/d infinite, NaN slabs on box faces) walk the reference
+    tree instead.  Both kinds, from random points and from points ON box planes (where the
+    reference's NaN order decides), equal the oracle: closest hit and shadow test."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, shader=1, scene=scene)
+    boxes, _, _, _ = m.triangle_bvh(cfg)
+    lo, hi = boxes[0, :3], boxes[0, 3:]
+    rng = np.random.default_rng(5)
+    n = 30000
+    o, d = random_rays(n, 3, lo, hi)
+    d = d.copy()
+    k = n // 3
+    d[:k, rng.integers(0, 3)] = 0.0                      # one zero component
+    d[k:2 * k:2, :] = 0.0
+    d[k:2 * k:2, rng.integers(0, 3)] = rng.choice([-1.0, 1.0])  # axis-aligned
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    leaf = boxes[np.any(boxes != 0, axis=1)]
+    pick = leaf[rng.integers(0, len(leaf), k)]
+    o[2 * k:, :] = pick[: n - 2 * k, :3]               # origins on box min corners (NaN slabs)
+    dist = (rng.random(n) * np.linalg.norm(hi - lo)).astype(np.float32)
+    with m.Renderer(cfg) as r:
+        hits = r.trace_rays(o, d)
+        occ = r.trace_rays(o, d, dist=dist, any_hit=True)[0]
+    ob = oracle_for(oracle_mod, cfg)
+    ok, oi, ot = ob.trace_rays(o, d)
+    oocc = ob.trace_rays(o, d, dist=dist, any_hit=True)[0]
+    ob.close()
+    assert np.array_equal(hits[0], ok) and np.array_equal(hits[1], oi)
+    assert np.array_equal(hits[2].view(np.int32), ot.view(np.int32))
+    assert np.array_equal(occ, oocc)
+
+
+def test_walk_tree_is_invariant():
+    """C4-style frames with the regrouped walk tree (default) and with the reference tree as the
+    walk tree (MOBILERT_WALK_TREE=0): identical bitmaps and ray counts."""
+    import os
+    import mobileraytracer_amd as m
+    outs = []
+    for env in ("0", "1"):
+        os.environ["MOBILERT_WALK_TREE"] = env
+        try:
+            cfg = make_cfg(320, 192, shader=2, scene="conference", spp=2, max_depth=5)
+            with m.Renderer(cfg) as r:
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"]))
+        finally:
+            del os.environ["MOBILERT_WALK_TREE"]
+    assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1:] == outs[1][1:]
