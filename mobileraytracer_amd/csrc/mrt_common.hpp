@@ -127,6 +127,10 @@ MRT_HD uint32_t pathKey(uint32_t pixelIndex, uint32_t globalSample) {
 MRT_HD uint32_t sampleIndex(uint32_t key, uint32_t treeCode, uint32_t purpose) {
     return ((hash32(key ^ hash32(treeCode * 0x9E3779B9u + 0x7F4A7C15u)) & ~7u) + purpose) & kArrayMask;
 }
+// the 8-entry block every draw of a vertex comes from (sampleIndex without the purpose)
+MRT_HD uint32_t sampleBlock(uint32_t key, uint32_t treeCode) {
+    return (hash32(key ^ hash32(treeCode * 0x9E3779B9u + 0x7F4A7C15u)) & kArrayMask) >> 3;
+}
 // purposes
 constexpr uint32_t kPJitterU = 0;   // pixel sampler, r1   (Renderer.cpp:137), tree code 0
 constexpr uint32_t kPJitterV = 1;   // pixel sampler, r2   (Renderer.cpp:138), tree code 0

@@ -32,6 +32,12 @@ struct DScene {
     // 2^20 x {shader (Shader.cpp:23), sampler (StaticHaltonSeq.cpp) shuffled Halton values,
     // cos and sin of 2 pi * shader entry by the host libm (fillHemisphereTrig)}
     const float4* tables;
+    // per 8-entry block b, the values a shading vertex draws with samplesLight 1 (purposes 0-5):
+    // [2b] = {sampler[8b] (Russian roulette), cos, sin of 2 pi shader[8b+1] (hemisphere r1),
+    // shader[8b+2] (hemisphere r2)}, [2b+1] = {shader[8b+3] (light pick), sampler[8b+4],
+    // sampler[8b+5] (area-light point), 0}: 32 B per vertex instead of a 128-B line, and a 4 MB
+    // table instead of 16 MB (the same values, relocated)
+    const float4* vertexDraws;
     // triRoot: the walk tree (the reference leaves regrouped, rebuildOverLeaves); triRootRef: the
     // reference tree (BVH.hpp), in the same node array - for rays with a non-finite 1/d, whose slab
     // NaNs break the leaf-box reachability argument, and for the per-wave reference walk

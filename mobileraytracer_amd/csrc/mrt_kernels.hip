@@ -513,14 +513,14 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     v.d = xyz(d4);
     if (level > a.maxDepth) return v;  // the depth cap below, taken before the gathers
     // issue every table gather of this vertex at once: their latencies overlap
-    const float pick0 = s.tables[sampleIndex(v.key, tc, purposeLightPick(0))].x;
-    const float lr0 = s.tables[sampleIndex(v.key, tc, purposeLightR(0))].y;
-    const float lq0 = s.tables[sampleIndex(v.key, tc, purposeLightS(0))].y;
-    const float rr = s.tables[sampleIndex(v.key, tc, kPRussian)].y;
-    const float4 hemi1 = s.tables[sampleIndex(v.key, tc, kPHemi1)];  // .zw: cos, sin of 2 pi r1
-    v.hcos = hemi1.z;
-    v.hsin = hemi1.w;
-    v.hemi2 = s.tables[sampleIndex(v.key, tc, kPHemi2)].x;
+    // purposes 0-5 of this vertex's block from the compact per-block copy (DScene::vertexDraws)
+    const uint32_t blk = sampleBlock(v.key, tc);
+    const float4 d0 = s.vertexDraws[2 * blk], d1 = s.vertexDraws[2 * blk + 1];
+    const float rr = d0.x;
+    v.hcos = d0.y;  // cos, sin of 2 pi r1
+    v.hsin = d0.z;
+    v.hemi2 = d0.w;
+    const float pick0 = d1.x, lr0 = d1.y, lq0 = d1.z;
     const uint32_t code = fbits(h.w);
     const uint32_t kind = primKind(code);
     // Shader.cpp:122: shade only if hit; Whitted.cpp:14-17 / PathTracer.cpp:25-28: depth cap

@@ -404,6 +404,13 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     std::vector<float4> tab(shaderT.size());
     for (size_t k = 0; k < shaderT.size(); ++k) tab[k] = make_float4(shaderT[k], samplerT[k], trig[2 * k], trig[2 * k + 1]);
     d.tables = r->sceneMem.upload(tab, st);
+    std::vector<float4> draws(2 * (tab.size() / 8));
+    for (size_t b = 0; b < tab.size() / 8; ++b) {
+        const float4* e = tab.data() + 8 * b;
+        draws[2 * b] = make_float4(e[kPRussian].y, e[kPHemi1].z, e[kPHemi1].w, e[kPHemi2].x);
+        draws[2 * b + 1] = make_float4(e[purposeLightPick(0)].x, e[purposeLightR(0)].y, e[purposeLightS(0)].y, 0.0F);
+    }
+    d.vertexDraws = r->sceneMem.upload(draws, st);
     MRT_HIP(hipStreamSynchronize(st));
 }
 
