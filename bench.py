@@ -132,11 +132,12 @@ def kernel_roofline(r, step):
     shadow_b = 36.0 * shadows + 32.0 * c["shadowNodeRecords"] + 36.0 * c["shadowTriTests"]
     # k_shade: per vertex 52 read (origin, direction, hit, tree code) + 16
     # written (vertex or result record); per shaded hit 48 (normals, material id) + 64 (material)
-    # + 64 (light) + 48 (six table draws); per shadow ray 48 written; per child ray 36 written
+    # + 64 (light) + 32 (the vertex's six draws, one compact block); per shadow ray 48 written;
+    # per child ray 36 written
     levels = c["levelRays"]
     shaded_rays = sum(levels[:r.config.maxDepth])  # levels 1..maxDepth (the last is not shaded)
     children = sum(levels[1:r.config.maxDepth + 1])
-    shade_b = 68.0 * shaded_rays + 224.0 * shaded + 48.0 * shadows + 36.0 * children
+    shade_b = 68.0 * shaded_rays + 208.0 * shaded + 48.0 * shadows + 36.0 * children
     fr = max(1, 2)
 
     def entry(name, frame_bytes, ms, launches):
