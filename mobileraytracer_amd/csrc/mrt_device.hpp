@@ -38,6 +38,7 @@ struct DScene {
     // sampler[8b+5] (area-light point), 0}: 32 B per vertex instead of a 128-B line, and a 4 MB
     // table instead of 16 MB (the same values, relocated)
     const float4* vertexDraws;
+    const float2* jitterDraws;  // per block: the pixel sampler's two draws (tree code 0, RaygenArgs::jitter)
     // triRoot: the walk tree (the reference leaves regrouped, rebuildOverLeaves); triRootRef: the
     // reference tree (BVH.hpp), in the same node array - for rays with a non-finite 1/d, whose slab
     // NaNs break the leaf-box reachability argument, and for the per-wave reference walk

@@ -210,9 +210,10 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
     const float u = static_cast<float>(x) * invW;
     const float v = static_cast<float>(y) * invH;
     float r1 = 0.5F, r2 = 0.5F;  // Constant(0.5) when spp <= 1 (C_wrapper.cpp:144-148)
-    if (a.sppTotal > 1) {
-        r1 = a.tables[sampleIndex(key, 0u, kPJitterU)].y;
-        r2 = a.tables[sampleIndex(key, 0u, kPJitterV)].y;
+    if (a.sppTotal > 1) {  // the two draws of the pixel sampler, one 8-byte read
+        const float2 j = a.jitter[sampleBlock(key, 0u)];
+        r1 = j.x;
+        r2 = j.y;
     }
     const float devU = (r1 - 0.5F) * 2.0F * pixW;
     const float devV = (r2 - 0.5F) * 2.0F * pixH;

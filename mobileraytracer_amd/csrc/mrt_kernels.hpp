@@ -80,6 +80,7 @@ struct RaygenArgs {
     GCamera cam;
     PixelMap map;
     const float4* tables;  // .y: the sampler table
+    const float2* jitter;  // per 8-entry block b: sampler[8b + kPJitterU], sampler[8b + kPJitterV]
     int width, height;
     int slotBase;    // first pixel slot of this chunk
     int nPaths;      // slots in chunk * spp

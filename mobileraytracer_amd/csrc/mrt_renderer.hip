@@ -411,6 +411,9 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
         draws[2 * b + 1] = make_float4(e[purposeLightPick(0)].x, e[purposeLightR(0)].y, e[purposeLightS(0)].y, 0.0F);
     }
     d.vertexDraws = r->sceneMem.upload(draws, st);
+    std::vector<float2> jit(tab.size() / 8);
+    for (size_t b = 0; b < jit.size(); ++b) jit[b] = make_float2(tab[8 * b + kPJitterU].y, tab[8 * b + kPJitterV].y);
+    d.jitterDraws = r->sceneMem.upload(jit, st);
     MRT_HIP(hipStreamSynchronize(st));
 }
 
@@ -526,6 +529,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.cam = r->cam;
         ra.map = map;
         ra.tables = r->ds.tables;
+        ra.jitter = r->ds.jitterDraws;
         ra.width = r->cfg.width;
         ra.height = r->cfg.height;
         ra.slotBase = slot0;
@@ -1145,6 +1149,7 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
                 ra.cam = r->cam;
                 ra.map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
                 ra.tables = r->ds.tables;
+        ra.jitter = r->ds.jitterDraws;
                 ra.width = r->cfg.width;
                 ra.height = r->cfg.height;
                 ra.slotBase = slot0;
