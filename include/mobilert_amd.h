@@ -146,12 +146,21 @@ int mrt_get_scene_info(const mrt_renderer *r, mrt_scene_info *info);
 /* enable per-launch HIP event timing (1) and/or node/triangle counting (2) */
 int mrt_set_profiling(mrt_renderer *r, int32_t flags);
 int mrt_get_frame_stats(const mrt_renderer *r, mrt_frame_stats *stats);
+/* counting mode: the last frame's wave log, out[2][16][8192][4] (closest / any-hit walk x level x
+ * wave: start, end in 100 MHz ticks, rays fetched, child records fetched; zero where no wave
+ * ran).  Returns the entry count (1,048,576) or -1; out NULL only counts. */
+int64_t mrt_wave_log(mrt_renderer *r, uint64_t *out);
 /* tuning knobs for A/B measurement (results are identical for every value):
  * key 1 = trace walk: 0 per-wave 64-ray batches with the plain DFS of BVH.hpp:327-384,
  *         1 persistent while-while walk (default),
  * key 2 = cull mode of walk 1: 0 none, 1 fast (default), 2 certified (mrt_config.cull),
  * key 3 = shadow rays on the same stream (0) or their own stream (1, default),
- * key 7 = skip the closest-hit walk of the depth-capped last level (1, default) */
+ * key 4 = binned emission of child / shadow rays (0 default, 1),
+ * key 5 = shadow walk child order: 0 near first, 1 far first (default),
+ * key 6 = shadow walk grid, percent of its occupancy grid (1-100; 0 default: by paths per walk lane),
+ * key 7 = skip the closest-hit walk of the depth-capped last level (1, default),
+ * key 8 = tail donation: idle lanes of a level's tail walk subtrees of their wave's rays (0, 1 default),
+ * key 9 = idle lanes before a walk wave fetches new rays (1-64, default 32) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /

@@ -4,7 +4,7 @@
  * The reference's JNI layer (app/System_dependent/Android_JNI/JNI_layer.cpp) keeps one renderer
  * and a small state machine in file statics and exports them as Java_puscas_mobilertapp_* methods.
  * This header is that session with plain C types: the JNI exports themselves
- * (mobileraytracer_amd/jni/JNI_layer.cpp, built with the Android NDK) only unpack the Java objects
+ * (mobileraytracer_amd/jni/mrt_jni.cpp, built with the Android NDK) only unpack the Java objects
  * and call these functions, one each:
  *
  *   mrt_android_read_file          MainActivity.readFile          (JNI_layer.cpp:994-1063)

@@ -117,13 +117,23 @@ class Renderer:
         """A/B knobs (identical results): 1 = trace walk (0 reference, 1 default), 2 = t-cull mode
         (0 none, 1 fast, 2 certified), 3 = shadow rays on their own stream, 4 = binned emission
         of child / shadow rays, 5 = shadow-walk child order (0 near first, 1 far first),
-        7 = no walk for the depth-capped last level."""
+        6 = shadow-walk grid percent (0 auto), 7 = no walk for the depth-capped last level, 8 = tail
+        donation (idle lanes of a level's tail walk subtrees of their wave's rays), 9 = refill
+        threshold of the walk waves."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 
     def get_tuning(self, key: int) -> int:
         v = ctypes.c_int32(0)
         _native.check(self._lib.mrt_get_tuning(self._h, key, ctypes.byref(v)))
         return v.value
+
+    def wave_log(self):
+        """Counting mode: the last frame's per-wave log, uint64 [2 (closest, any-hit), 16 levels,
+        8192 waves, 4 (start, end in 100 MHz ticks, rays fetched, child records fetched)]."""
+        n = int(self._lib.mrt_wave_log(self._h, None))
+        out = np.zeros(n, np.uint64)
+        _native.check(0 if self._lib.mrt_wave_log(self._h, out.ctypes.data_as(ctypes.c_void_p)) >= 0 else -1)
+        return out.reshape(2, 16, 8192, 4)
 
     def frame_stats(self) -> dict:
         s = _native.MrtFrameStats()

@@ -18,7 +18,7 @@ EXPORTED_SYMBOLS = (
     "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits", "mrt_set_tuning",
     "mrt_get_tuning", "mrt_triangle_bvh", "mrt_decode_texture", "mrt_kat_slab", "mrt_kat_triangle",
     "mrt_trace_rays", "mrt_sample_tables", "mrt_regular_grid", "mrt_grid_box_test", "mrt_create_from_memory",
-    "mrt_preview_arrays",
+    "mrt_preview_arrays", "mrt_wave_log",
     "mrt_android_read_file", "mrt_android_initialize", "mrt_android_render_into_bitmap", "mrt_android_start_render",
     "mrt_android_stop_render", "mrt_android_finish_render", "mrt_android_state", "mrt_android_fps",
     "mrt_android_time_renderer", "mrt_android_sample", "mrt_android_number_of_lights", "mrt_android_resize",
@@ -106,6 +106,7 @@ def load_library(path=LIB_PATH):
         "mrt_get_scene_info": (ctypes.c_int, [vp, P(MrtSceneInfo)]),
         "mrt_set_profiling": (ctypes.c_int, [vp, ctypes.c_int32]),
         "mrt_get_frame_stats": (ctypes.c_int, [vp, P(MrtFrameStats)]),
+        "mrt_wave_log": (ctypes.c_int64, [vp, vp]),
         "mrt_primary_hits": (ctypes.c_int, [vp, vp, vp, vp]),
         "mrt_set_tuning": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32]),
         "mrt_get_tuning": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),

@@ -50,6 +50,8 @@ struct DScene {
     int32_t triTop;            // triNodes[0, triTop) are the breadth-first top of the tree
     int32_t matsFinite;        // every material's Kd / Ks / Kt component is finite
     int32_t anyOrder;          // shadow walk child order (tuning key 5): 0 near first, 1 far first (default)
+    int32_t tailDonate;        // idle lanes of a level's tail help walking lanes (tuning key 8, mrt_trace_ww.hpp)
+    int32_t refill;            // idle lanes before a walk wave fetches new rays (tuning key 9, default 32)
     // textures (map_Kd): scenes with a textured material only (`textured` != 0)
     const float4* triTex;      // 2 per triangle: (tA.xy, tB.xy), (tC.xy, -, -)
     const int4* texInfo;       // per texture: width, height, channels, first byte in texels
@@ -273,8 +275,7 @@ struct TravCount {
     uint32_t tris;   // triangle tests
     uint32_t rayStart = 0;  // nodes at the current ray's fetch (per-ray maximum, counting builds)
     uint32_t rayMax = 0;
-    uint32_t assists = 0;   // tail-assist builds: subtrees this lane handed over
-    uint32_t ticksMax = 0;  // tail-assist builds: longest fetch-to-result time (100 MHz ticks)
+    uint32_t rays = 0;      // rays this lane fetched (the wave log of counting builds)
 };
 
 // Generic BVH walk.  kKind selects the leaf routine.  Returns true on an any-hit.

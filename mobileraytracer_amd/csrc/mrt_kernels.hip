@@ -261,19 +261,39 @@ __device__ __forceinline__ void reduceCounts(const TravCount& cnt, unsigned long
     }
 }
 
+// counting builds: this wave's entry of the wave log (kWaveLogWaves)
+__device__ __forceinline__ void waveLog(const TravCount& cnt, unsigned long long* stats, int kind, int level,
+                                        unsigned long long t0) {
+    unsigned long long n = cnt.nodes, r = cnt.rays;
+    for (int off = 32; off > 0; off >>= 1) {
+        n += __shfl_down(n, off, 64);
+        r += __shfl_down(r, off, 64);
+    }
+    const int wave = static_cast<int>(blockIdx.x * (kWalkThreads / 64) + threadIdx.x / 64);
+    if (laneId() == 0 && wave < kWaveLogWaves && level < kMaxLevels) {
+        unsigned long long* e = stats + kNumStats + ((static_cast<size_t>(kind) * kMaxLevels + level) * kWaveLogWaves + wave) * 4;
+        e[0] = t0;
+        e[1] = __builtin_amdgcn_s_memrealtime();
+        e[2] = r;
+        e[3] = n;
+    }
+}
+
 template <bool kCount, int kVariant, int kCull>
 __global__ __launch_bounds__(kWalkThreads, 1) void k_trace(DScene s, Level lv, int* counters, int level,
                                                             int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
               kWalkStack, kWalkThreads};
+    const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int count = min(counters[cntRays(level)], lv.cap);
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
     if (kVariant == 1) {
         __shared__ GNode ldsTop[kWalkTop];
+        __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop);
+        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, tailBest);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -291,6 +311,7 @@ __global__ __launch_bounds__(kWalkThreads, 1) void k_trace(DScene s, Level lv, i
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris);
         atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
+        waveLog(cnt, stats, 0, level, t0);
     }
 }
 
@@ -300,13 +321,15 @@ __global__ __launch_bounds__(kWalkThreads, 1) void k_shadow(DScene s, Level lv, 
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
               kWalkStack, kWalkThreads};
+    const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int count = min(counters[cntShadows(level)], lv.shadowCap);
     int* fetch = counters + kCntFetchShards + (kMaxLevels + level) * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
     if (kVariant == 1) {
         __shared__ GNode ldsTop[kWalkTop];
+        __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop);
+        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -321,7 +344,10 @@ __global__ __launch_bounds__(kWalkThreads, 1) void k_shadow(DScene s, Level lv, 
             lv.sC[i].w = occ ? 1.0F : 0.0F;
         }
     }
-    if (kCount) reduceCounts<kCount>(cnt, stats, kStatNodesShadow, kStatTrisShadow);
+    if (kCount) {
+        reduceCounts<kCount>(cnt, stats, kStatNodesShadow, kStatTrisShadow);
+        waveLog(cnt, stats, 1, level, t0);
+    }
 }
 
 // Closest hit (kAny false: lv.rO / rD -> lv.hit) or shadow test (true: lv.sO / sD -> lv.sC.w)
@@ -987,7 +1013,7 @@ int persistentGrid(K kernel, int slot, int maxThreads) {
 // variant 0 (reference walk, never culls) and variant 1 in each cull mode; slot: occupancy cache
 #define MRT_LAUNCH_ONE(KERNEL, V, C, SLOT)                                                                      \
     do {                                                                                                       \
-        const int g = persistentGrid(KERNEL<false, V, C>, SLOT, maxThreads);                                   \
+        const int g = std::max(1, persistentGrid(KERNEL<false, V, C>, SLOT, maxThreads) * gridPct / 100);    \
         if (countStats)                                                                                        \
             hipLaunchKernelGGL((KERNEL<true, V, C>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats); \
         else                                                                                                   \
@@ -1007,11 +1033,12 @@ void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int
         hipLaunchKernelGGL((k_trace_other<false>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }
+    const int gridPct = 100;
     MRT_LAUNCH_WALK(k_trace, 0);
 }
 
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
-                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
+                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st, int gridPct) {
     if (s.accel != kAccBVH) {
         hipLaunchKernelGGL((k_trace_other<true>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;

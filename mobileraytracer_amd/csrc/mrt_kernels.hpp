@@ -45,6 +45,10 @@ constexpr int kStatSkipped = kStatMaxNodesRay + 1;   // rays of a last level who
 constexpr int kStatShaded = kStatSkipped + 1;        // counting pass: vertices k_shade shaded (hit, not emissive, not capped)
 constexpr int kStatShadeLaunches = kStatShaded + 1;  // k_shade launches of the frame
 constexpr int kNumStats = kStatShadeLaunches + 1;
+// counting builds: per walk launch (closest / any-hit x level) and wave {start, end (100 MHz
+// ticks), rays fetched, child records fetched}, after the statistics (mrt_wave_log)
+constexpr int kWaveLogWaves = 8192;
+constexpr int kWaveLogEntries = 2 * kMaxLevels * kWaveLogWaves * 4;
 
 // One level of the wavefront (SoA queues).
 struct Level {
@@ -117,7 +121,7 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
-                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
+                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st, int gridPct = 100);
 // deadNext: level + 1 is the depth-capped last level (its rays are counted, never written)
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st, bool deadNext = false);

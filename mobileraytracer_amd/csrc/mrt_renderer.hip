@@ -132,6 +132,7 @@ struct mrt_renderer {
     int overlap = 1;                     // tuning key 3: shadow rays on their own stream
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
     int binMode = 0;                     // tuning key 4: binned emission of child / shadow rays (ShadeArgs::binMode)
+    int shadowGridPct = 0;               // tuning key 6: shadow walk grid, percent of its occupancy grid (0 auto)
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
 
@@ -389,6 +390,8 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     // the depth-capped last level's children count as absent in the resolve only while no
     // material coefficient is infinite or NaN (inf * 0 would be NaN in the reference)
     d.anyOrder = 1;
+    d.tailDonate = 1;
+    d.refill = 32;  // kWalkRefill
     d.matsFinite = 1;
     for (const HMaterial& m : sc.materials) {
         for (const v3 c : {m.Kd, m.Ks, m.Kt})
@@ -456,7 +459,7 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
         lv.last = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
     }
     pp.counters = r->queueMem.alloc<int>(kNumCounters);
-    pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats);
+    pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats + kWaveLogEntries);
     pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
     pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
 }
@@ -501,7 +504,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                  r->binMode, splBits};
     const int nLevels = r->nLevels;
     const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
-    MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * kNumStats, st));
+    MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * (kNumStats + (counting ? kWaveLogEntries : 0)), st));
     pp.evCount = 0;
     r->shadeLaunches = 0;
     // Any-hit (shadow) rays of level L run on a second stream, overlapped with the closest-hit
@@ -538,6 +541,12 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.sppTotal = r->cfg.samplesPixel;
         ra.sampleBase = sampleBase;
         launchRaygen(ra, pp.levels[1], pp.counters, st);
+        // With few paths per resident walk lane (a small shard: C4 at N >= 4) the levels are short
+        // and tail-bound, and a full-width shadow walk starves the next level's shading of CUs;
+        // a narrower shadow grid leaves them room (C4 shard at N = 8: 2.92 -> 2.83 ms; at N = 1 the
+        // full grid is 2.6 % faster).  Results do not depend on the grid.
+        const double pathsPerLane = static_cast<double>(ra.nPaths) / std::max(1, r->traceThreads);
+        const int shadowPct = r->shadowGridPct > 0 ? r->shadowGridPct : pathsPerLane < 4.0 ? 60 : pathsPerLane < 8.0 ? 75 : 100;
         size_t sync = 0;
         hipEvent_t shadowDone[kMaxLevels] = {};
         if (sb != st) {
@@ -566,7 +575,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             // the last level (depth > RayDepthMax) shades nothing: no shadow rays
             if (l < nLevels) {
                 launchShadow(r->ds, pp.levels[l], pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
-                             r->traceThreads, sb);
+                             r->traceThreads, sb, shadowPct);
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
             if (sb != st) {
@@ -963,6 +972,20 @@ int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
     return 0;
 }
 
+int64_t mrt_wave_log(mrt_renderer* r, uint64_t* out) {
+    using namespace mrt;
+    if (r == nullptr) return -1;
+    if (out == nullptr) return kWaveLogEntries;
+    int64_t n = -1;
+    const int rc = guarded([&] {
+        if (r->pipe.stats == nullptr) throw std::runtime_error("no frame rendered");
+        MRT_HIP(hipSetDevice(r->device));
+        MRT_HIP(hipMemcpy(out, r->pipe.stats + kNumStats, sizeof(uint64_t) * kWaveLogEntries, hipMemcpyDeviceToHost));
+        n = kWaveLogEntries;
+    });
+    return rc == 0 ? n : -1;
+}
+
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
     if (key == 1 && value >= 0 && value < mrt::kTraceVariants) {
         r->ds.variant = value;
@@ -986,6 +1009,18 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
     }
     if (key == 4 && (value == 0 || value == 1)) {
         r->binMode = value;
+        return 0;
+    }
+    if (key == 9 && value >= 1 && value <= 64) {
+        r->ds.refill = value;
+        return 0;
+    }
+    if (key == 8 && (value == 0 || value == 1)) {
+        r->ds.tailDonate = value;
+        return 0;
+    }
+    if (key == 6 && value >= 0 && value <= 100) {
+        r->shadowGridPct = value;
         return 0;
     }
     gLastError = "unknown tuning key/value";
@@ -1108,6 +1143,9 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 7: *value = r->skipLast; return 0;
         case 4: *value = r->binMode; return 0;
         case 5: *value = r->ds.anyOrder; return 0;
+        case 6: *value = r->shadowGridPct; return 0;
+        case 8: *value = r->ds.tailDonate; return 0;
+        case 9: *value = r->ds.refill; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";
@@ -1149,7 +1187,7 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
                 ra.cam = r->cam;
                 ra.map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
                 ra.tables = r->ds.tables;
-        ra.jitter = r->ds.jitterDraws;
+                ra.jitter = r->ds.jitterDraws;
                 ra.width = r->cfg.width;
                 ra.height = r->cfg.height;
                 ra.slotBase = slot0;

@@ -27,7 +27,7 @@
 namespace mrt {
 
 constexpr int kRefDone = 0x7FFFFFFF;  // sentinel: no node (never a valid inner index)
-constexpr int kWalkRefill = 32;       // idle lanes before a wave fetches new rays
+constexpr int kWalkRefill = 32;       // idle lanes before a wave fetches new rays (DScene::refill default)
 constexpr int kWalkShards = 8;        // work cursors per level (one per XCD group of workgroups)
 constexpr int kWalkStack = kLdsStackMin;  // LDS stack entries per thread (deeper ones spill)
 constexpr int kWalkTop = kTopNodesMax;
@@ -233,7 +233,9 @@ __device__ __forceinline__ void stageTop(const DScene& s, GNode* ldsTop) {
 template <bool kAny, bool kCount, int kCull>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                TStack& st, TravCount* cnt, const GNode* ldsTop) {
+                                                TStack& st, TravCount* cnt, const GNode* ldsTop, int* tailBest) {
+    constexpr int kHelper = -2;  // rayIdx of a lane walking a subtree given by another lane
+    const bool donate = s.tailDonate != 0;
     const int top = min(kWalkTop, s.triTop);
     const BufRes nodeBuf = bufferOf(s.triNodes);
     const BufRes triBuf = bufferOf(s.triGeom);
@@ -251,12 +253,66 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
     int leaf = 0;  // < 0: a postponed leaf
     int seg = static_cast<int>(blockIdx.x % kWalkShards);  // wave-uniform cursor state
     int segsLeft = kWalkShards;
+    // tail donation (DScene::tailDonate): a helper lane walks a subtree of its owner's ray and
+    // hands its best hit (closest) or occlusion (any) back; the owner finishes when all its
+    // helpers have.  Exact: the owner and its helpers visit the owner's subtrees between them,
+    // each culling against a best no better than the final one, and betterThan is a total order.
+    // In tail mode an owner and its helpers share, through the owner's LDS word in tailBest, the
+    // best t any of them has accepted (closest hit: the cull limit of all of them; it is the t of an
+    // accepted candidate, so never below the final best) or the occlusion (any-hit: 0, they stop).
+    int owner = -1;     // helper: the lane owning the ray
+    int pend = 0;       // owner: helpers still walking
+    bool occ = false;   // any-hit: an occluder found (by this lane, or merged from a helper)
+    bool tailMode = false;  // wave-uniform: this wave has donated (its queue is exhausted)
+    float shT = __builtin_inff();  // tail mode: the best t shared by the ray's lanes
+    int* const waveBest = tailBest + (threadIdx.x & ~63u);
     while (true) {
+        if (tailMode && rayIdx != -1) {
+            const int ol = rayIdx >= 0 ? lane : owner;
+            const int mine = kAny ? (occ ? 0 : 0x7FFFFFFF) : __float_as_int(bt);
+            const int v = min(atomicMin(waveBest + ol, mine), mine);
+            if (kAny) {
+                if (v == 0 && !occ) {  // another lane of this ray found an occluder: stop
+                    occ = rayIdx >= 0;
+                    st.sp = 0;
+                    ref = kRefDone;
+                    leaf = 0;
+                }
+            } else {
+                shT = __int_as_float(v);
+            }
+        }
+        const bool over = ref == kRefDone && leaf >= 0;
+        if (donate) {  // helpers whose subtree is done merge into their owner (wave-uniform loop)
+            uint64_t hm = __ballot(rayIdx == kHelper && over);
+            while (hm != 0) {
+                const int h = __ffsll(static_cast<unsigned long long>(hm)) - 1;
+                hm &= hm - 1;
+                const int ol = __builtin_amdgcn_readlane(owner, h);
+                const float ht = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bt), h));
+                const uint32_t hc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bcode), h));
+                const int ho = __builtin_amdgcn_readlane(occ ? 1 : 0, h);
+                if (lane == ol) {
+                    if (kAny) {
+                        occ = occ || ho != 0;
+                    } else if (betterThan(ht, hc, bt, bcode)) {
+                        bt = ht;
+                        bcode = hc;
+                    }
+                    --pend;
+                }
+            }
+            if (rayIdx == kHelper && over) {
+                rayIdx = -1;
+                occ = false;
+            }
+        }
         // ---- lanes whose triangle walk is over: lights (closest only), write the result ----
-        if (rayIdx >= 0 && ref == kRefDone && leaf >= 0) {
+        if (rayIdx >= 0 && over && pend == 0) {
             if (kCount) cnt->rayMax = max(cnt->rayMax, cnt->nodes - cnt->rayStart);
             if (kAny) {
-                out[rayIdx].w = 0.0F;
+                out[rayIdx].w = occ ? 1.0F : 0.0F;
+                occ = false;
             } else {
                 for (int j = 0; j < s.nLights; ++j) {  // Shader.cpp:166-171
                     const float4* l = s.lights + 4 * j;
@@ -282,10 +338,10 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             rayIdx = -1;
         }
         // ---- refill lanes without a ray (one atomic per wave and cursor) ----
-        bool need = rayIdx < 0 && !exhausted;
+        bool need = rayIdx == -1 && !exhausted;
         uint64_t needMask = __ballot(need);
         // refill only once enough lanes are idle (fewer, larger fetches), or when none is busy
-        if (__popcll(needMask) < kWalkRefill && __ballot(rayIdx >= 0) != 0) {
+        if (__popcll(needMask) < s.refill && __ballot(rayIdx >= 0) != 0) {
             need = false;
             needMask = 0;
         }
@@ -315,7 +371,10 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             }
             if (need) {
                 rayIdx = got;
-                if (kCount) cnt->rayStart = cnt->nodes;
+                if (kCount) {
+                    cnt->rayStart = cnt->nodes;
+                    if (got >= 0) ++cnt->rays;
+                }
                 if (rayIdx < 0) {
                     exhausted = true;
                 } else {
@@ -359,13 +418,67 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 }
             }
         }
-        if (__ballot(rayIdx >= 0) == 0) {
+        // ---- a level's tail: idle lanes take the next pending subtree of a walking lane ----
+        if (donate) {
+            uint64_t idle = __ballot(rayIdx == -1 && (exhausted || segsLeft == 0));
+            if (idle != 0 && !tailMode) {  // the owners' shared words
+                tailMode = true;
+                if (rayIdx >= 0) waveBest[lane] = kAny ? 0x7FFFFFFF : __float_as_int(bt);
+            }
+            uint64_t donors = 0;
+            for (int round = 0; idle != 0 && round < 64; ++round) {
+                if (donors == 0) {
+                    donors = __ballot(rayIdx != -1 && st.sp > 0);
+                    if (donors == 0) break;
+                }
+                const int dl = __ffsll(static_cast<unsigned long long>(donors)) - 1;
+                donors &= donors - 1;  // one subtree per donor and sweep
+                int2 e = make_int2(kRefDone, 0);
+                if (lane == dl) e.x = popCulled(st, cullLimit<kCull>(fminf(bt, shT)), cull);  // its next subtree
+                const int er = __builtin_amdgcn_readlane(e.x, dl);
+                if (er == kRefDone) continue;
+                const int h = __ffsll(static_cast<unsigned long long>(idle)) - 1;
+                idle &= idle - 1;
+                const int dOwner = __builtin_amdgcn_readlane(rayIdx >= 0 ? lane : owner, dl);
+                const float ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o.x), dl));
+                const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o.y), dl));
+                const float oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o.z), dl));
+                const float dx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.x), dl));
+                const float dy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.y), dl));
+                const float dz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.z), dl));
+                const int dsrc = __builtin_amdgcn_readlane(static_cast<int>(src), dl);
+                const float dbt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bt), dl));
+                const int dbc = __builtin_amdgcn_readlane(static_cast<int>(bcode), dl);
+                if (lane == h) {
+                    rayIdx = kHelper;
+                    owner = dOwner;
+                    o = v3{ox, oy, oz};
+                    d = v3{dx, dy, dz};
+                    inv = v3{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
+                    src = static_cast<uint32_t>(dsrc);
+                    bt = dbt;
+                    bcode = static_cast<uint32_t>(dbc);
+                    shT = dbt;
+                    occ = false;
+                    st.sp = 0;
+                    if (er < 0) {  // a leaf
+                        leaf = er;
+                        ref = kRefDone;
+                    } else {
+                        leaf = 0;
+                        ref = er;
+                    }
+                }
+                if (lane == dOwner) ++pend;
+            }
+        }
+        if (__ballot(rayIdx != -1) == 0) {
             if (__ballot(!exhausted) == 0) break;
             continue;
         }
         // ---- inner nodes until every active lane holds a postponed leaf ----
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
-            const float curLim = cullLimit<kCull>(bt);
+            const float curLim = cullLimit<kCull>(fminf(bt, shT));
             const bool finite = __ballot(!finiteInv(inv)) == 0;
             ref = innerStep<kCull>(nodeBuf, ldsTop, top, ref, o, d, inv, curLim, st, cnt, kCount, finite,
                                    kAny ? s.anyOrder : 0);
@@ -400,8 +513,12 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 }
             }
             if (kAny && hit) {
-                out[rayIdx].w = 1.0F;
-                rayIdx = -1;
+                if (rayIdx >= 0 && pend == 0) {
+                    out[rayIdx].w = 1.0F;
+                    rayIdx = -1;
+                } else {  // a helper, or an owner waiting for helpers: the merge writes it
+                    occ = true;
+                }
                 st.sp = 0;
                 ref = kRefDone;
                 leaf = 0;
@@ -410,7 +527,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             leaf = 0;
             if (ref < 0) {  // the next node is a leaf too: test it now
                 leaf = ref;
-                ref = popCulled(st, cullLimit<kCull>(bt), cull);
+                ref = popCulled(st, cullLimit<kCull>(fminf(bt, shT)), cull);
             }
         }
     }

@@ -357,6 +357,40 @@ def test_binned_emission_and_shadow_order_are_invariant():
             assert outs[0][1:] == other[1:], cfg
 
 
+def test_tail_donation_matches_oracle_and_is_invariant(oracle_mod):
+    """Tail donation (tuning key 8): in a level's tail an idle lane walks the oldest pending
+    subtree of a walking lane of its wave and hands its best hit (closest) or occlusion (any-hit)
+    back.  Small frames keep most lanes idle, so nearly every ray is split: the bitmap, the ray
+    counts and the primary hits equal the oracle's and the undonated walk's in every cull mode."""
+    import mobileraytracer_amd as m
+    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+             make_cfg(128, 128, shader=1, scene="water", max_depth=4),
+             make_cfg(96, 96, shader=2, scene="water", spp=2, max_depth=4, spl=3),
+             make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3),
+             make_cfg(64, 64, shader=2, spp=3, max_depth=6))
+    for cfg in cases:
+        outs = []
+        with m.Renderer(cfg) as r:
+            for donate, cull in ((0, 1), (1, 1), (1, 0), (1, 2)):
+                r.set_tuning(8, donate)
+                r.set_tuning(2, cull)
+                assert r.get_tuning(8) == donate
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"])))
+        for other in outs[1:]:
+            assert np.array_equal(outs[0][0], other[0]), cfg
+            assert outs[0][1:] == other[1:], cfg
+    for cfg in (make_cfg(96, 96, shader=1, scene="conference"), make_cfg(128, 128, scene="teapot")):
+        ok, oi, ot = oracle_for(oracle_mod, cfg).primary_hits()
+        with m.Renderer(cfg) as r:
+            r.set_tuning(8, 1)
+            k, i, t = r.primary_hits()
+        assert np.array_equal(k, ok) and np.array_equal(i, oi)
+        assert np.array_equal(t.view(np.int32), ot.view(np.int32))
+
+
 def test_last_level_walk_skip_is_invariant():
     """The depth-capped last level shades to zero whatever its rays hit, so skipping its
     closest-hit walk (tuning key 7, default on) changes no pixel and no ray count; the walked-ray

@@ -1,5 +1,6 @@
-"""A/B of the walk tree (MOBILERT_WALK_TREE=0 reference topology, 1 SAH regrouping of the reference
-leaves) on the C4 frame: two renderers in one process, interleaved rounds, identical images."""
+"""A/B of tuning settings on the C4 frame: one renderer per setting in one process, interleaved
+rounds, no per-launch events, images compared.  VARIANTS="6=100,6=75+3=1" (key=value pairs joined
+by '+', settings separated by ','); RANKS=N renders rank 0's shard of an N-GPU frame."""
 import os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -11,18 +12,21 @@ from mobileraytracer_amd import scenes
 def main():
     o, l, c = scenes.conference()
     ranks = int(os.environ.get("RANKS", 1))
+    variants = os.environ.get("VARIANTS", "6=100,6=50").split(",")
     rs = {}
-    trees = os.environ.get("TREES", "0,1").split(",")
-    for tree in trees:
-        os.environ["MOBILERT_WALK_TREE"] = tree
+    for v in variants:
         cfg = m.Config(width=1920, height=1080, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5,
                        objFilePath=o, mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=ranks)
-        rs[tree] = m.Renderer(cfg)
-    n = max(1920 * 1080, rs[trees[0]].scene_info()["pixelSlotsMax"])
+        r = m.Renderer(cfg)
+        for kv in filter(None, v.split("+")):
+            k, val = kv.split("=")
+            r.set_tuning(int(k), int(val))
+        rs[v] = r
+    n = max(1920 * 1080, rs[variants[0]].scene_info()["pixelSlotsMax"])
     bufs = {k: torch.zeros(n, dtype=torch.int32, device="cuda") for k in rs}
     sh = torch.cuda.current_stream().cuda_stream
     res = {k: [] for k in rs}
-    for rnd in range(5):
+    for rnd in range(int(os.environ.get("ROUNDS", 5))):
         for k, r in rs.items():
             bm, pk = (bufs[k].data_ptr(), 0) if ranks == 1 else (0, bufs[k].data_ptr())
             r.render_frame_device(bm, pk, sh)
@@ -33,9 +37,9 @@ def main():
             torch.cuda.synchronize()
             res[k].append((time.perf_counter() - t0) / 5 * 1e3)
     for k in rs:
-        print(f"tree {k}: frame {np.median(res[k]):.3f} ms (min {np.min(res[k]):.3f})", flush=True)
-    for k in trees[1:]:
-        print(f"tree {k} identical image:", torch.equal(bufs[trees[0]], bufs[k]))
+        print(f"setting {k}: frame {np.median(res[k]):.3f} ms (min {np.min(res[k]):.3f})", flush=True)
+    for k in variants[1:]:
+        print(f"setting {k} identical image:", torch.equal(bufs[variants[0]], bufs[k]))
 
 
 main()
