@@ -14,6 +14,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                          \
@@ -58,6 +59,34 @@ __global__ __launch_bounds__(256, 1) void k_gather(const uint4* __restrict__ tab
     out[tid] = acc;
 }
 
+// The walk's node fetch on 64-B aligned records: three 16-B loads (the child boxes) and, with
+// kRefs, the 8-B child-reference load at +48 - what a node whose references are folded into the
+// boxes would save.
+template <bool kRefs>
+__global__ __launch_bounds__(256, 1) void k_gather_node(const uint4* __restrict__ table, uint32_t nRecords, int iters,
+                                                       uint32_t* out) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(table), static_cast<short>(0), 0x7FFFFFFF,
+                                                       0x00020000);
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t idx = mix(tid) % nRecords;
+    uint32_t acc = 0;
+    for (int i = 0; i < iters; ++i) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, idx * 64u + k * 16u, 0, 0));
+            x ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+        if (kRefs) {
+            const auto r = __builtin_amdgcn_raw_buffer_load_b64(rsrc, idx * 64u + 48u, 0, 0);
+            x ^= static_cast<uint32_t>(r[0]) ^ static_cast<uint32_t>(r[1]);
+        }
+        acc += x;
+        idx = mix(idx ^ x ^ static_cast<uint32_t>(i)) % nRecords;
+    }
+    out[tid] = acc;
+}
+
 // Quad-cooperative form of the divergent chase (64-B records): in round k the four lanes of a
 // quad fetch the four 16-B pieces of lane (4q + k)'s record with one LDS-DMA load
 // (global_load_lds_dwordx4), so one wave instruction touches 16 lines, 4 lanes each, instead of
@@ -96,7 +125,7 @@ __global__ __launch_bounds__(256, 1) void k_gather_quad(const uint4* __restrict_
     out[tid] = acc;
 }
 
-template <int kVec4, bool kCoherent, bool kQuad = false>
+template <int kVec4, bool kCoherent, bool kQuad = false, int kNode = 0>
 void run(size_t tableBytes, int blocksPerCU, const char* label) {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -116,7 +145,11 @@ void run(size_t tableBytes, int blocksPerCU, const char* label) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     auto launch = [&](int it) {
-        if (kQuad)
+        if (kNode == 1)
+            hipLaunchKernelGGL(k_gather_node<false>, dim3(blocks), dim3(256), 0, 0, table, nRecords, it, out);
+        else if (kNode == 2)
+            hipLaunchKernelGGL(k_gather_node<true>, dim3(blocks), dim3(256), 0, 0, table, nRecords, it, out);
+        else if (kQuad)
             hipLaunchKernelGGL(k_gather_quad, dim3(blocks), dim3(256), 0, 0, table, nRecords, it, out);
         else
             hipLaunchKernelGGL((k_gather<kVec4, kCoherent>), dim3(blocks), dim3(256), 0, 0, table, nRecords, it, out);
@@ -144,7 +177,14 @@ void run(size_t tableBytes, int blocksPerCU, const char* label) {
     CK(hipFree(out));
 }
 
-int main() {
+int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "node") {  // 64-B node records: 48 B vs 56 B fetched
+        for (size_t mib : {8, 16, 32}) {
+            run<4, false, false, 2>(mib << 20, 6, "node-48+8");
+            run<4, false, false, 1>(mib << 20, 6, "node-48");
+        }
+        return 0;
+    }
     // the walk: 6 workgroups of 256 threads per CU; Conference scene ~30 MB (nodes + triangles)
     for (size_t mib : {4, 32, 128}) {
         run<4, false>(mib << 20, 6, "divergent");

@@ -1,6 +1,6 @@
 """A/B of tuning settings on the C4 frame: one renderer per setting in one process, interleaved
-rounds, no per-launch events, images compared.  VARIANTS="6=100,6=75+3=1" (key=value pairs joined
-by '+', settings separated by ','); RANKS=N renders rank 0's shard of an N-GPU frame."""
+rounds, no per-launch events, images compared.  VARIANTS="6=100,6=75+3=1,W=0" (key=value pairs joined
+by '+', settings separated by ','; W sets MOBILERT_WALK_TREE for the upload); RANKS=N renders rank 0's shard of an N-GPU frame."""
 import os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -15,12 +15,21 @@ def main():
     variants = os.environ.get("VARIANTS", "6=100,6=50").split(",")
     rs = {}
     for v in variants:
+        # W=0: MOBILERT_WALK_TREE for this renderer's scene upload
+        env = {"W": "MOBILERT_WALK_TREE"}
+        for kv in filter(None, v.split("+")):
+            k, val = kv.split("=")
+            if k in env:
+                os.environ[env[k]] = val
         cfg = m.Config(width=1920, height=1080, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5,
                        objFilePath=o, mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=ranks)
         r = m.Renderer(cfg)
         for kv in filter(None, v.split("+")):
             k, val = kv.split("=")
-            r.set_tuning(int(k), int(val))
+            if k in env:
+                os.environ.pop(env[k])
+            else:
+                r.set_tuning(int(k), int(val))
         rs[v] = r
     n = max(1920 * 1080, rs[variants[0]].scene_info()["pixelSlotsMax"])
     bufs = {k: torch.zeros(n, dtype=torch.int32, device="cuda") for k in rs}
