@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmobilert_amd.so")
+# MOBILERT_LIB: another build of the library (A/B of compile-time variants, tools/build_ab.sh)
+LIB_PATH = os.environ.get("MOBILERT_LIB") or os.path.join(_HERE, "libmobilert_amd.so")
 
 # Symbols the C-ABI exports (include/mobilert_amd.h + mobilert_amd.hpp).
 EXPORTED_SYMBOLS = (

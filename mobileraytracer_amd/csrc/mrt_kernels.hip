@@ -280,7 +280,7 @@ __device__ __forceinline__ void waveLog(const TravCount& cnt, unsigned long long
 }
 
 template <bool kCount, int kVariant, int kCull>
-__global__ __launch_bounds__(kWalkThreads, 1) void k_trace(DScene s, Level lv, int* counters, int level,
+__global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, int* counters, int level,
                                                             int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kWalkThreads, 1) void k_trace(DScene s, Level lv, i
 }
 
 template <bool kCount, int kVariant, int kCull>
-__global__ __launch_bounds__(kWalkThreads, 1) void k_shadow(DScene s, Level lv, int* counters, int level,
+__global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, int* counters, int level,
                                                              int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
