@@ -391,6 +391,41 @@ def test_tail_donation_matches_oracle_and_is_invariant(oracle_mod):
         assert np.array_equal(t.view(np.int32), ot.view(np.int32))
 
 
+def test_walk_knobs_are_invariant_and_wave_log_is_consistent():
+    """The shadow walk's grid size (tuning key 6) and the walk's refill threshold (key 9) change
+    only scheduling: same bitmap and ray counts.  In counting mode the wave log holds one entry per
+    resident wave of every walk launch, and its rays add up to the frame's walked rays."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5)
+    outs = []
+    with m.Renderer(cfg) as r:
+        for key, val in ((6, 0), (6, 40), (6, 100), (9, 1), (9, 64)):
+            r.set_tuning(6, 0)
+            r.set_tuning(9, 32)
+            r.set_tuning(key, val)
+            assert r.get_tuning(key) == val
+            bm = np.zeros(cfg.width * cfg.height, np.int32)
+            r.render_frame(bm)
+            st = r.frame_stats()
+            outs.append((bm, st["rays"], st["shadowRays"]))
+        r.set_tuning(6, 0)
+        r.set_tuning(9, 32)
+        r.set_profiling(counting=True)
+        bm = np.zeros(cfg.width * cfg.height, np.int32)
+        r.render_frame(bm)
+        st = r.frame_stats()
+        log = r.wave_log().astype(np.int64)
+    for other in outs[1:]:
+        assert np.array_equal(outs[0][0], other[0])
+        assert outs[0][1:] == other[1:]
+    closest, shadow = log[0, :, :, 2].sum(), log[1, :, :, 2].sum()
+    assert closest == st["walkedRays"], (closest, st["walkedRays"])
+    assert shadow == st["shadowRays"], (shadow, st["shadowRays"])
+    ran = log[:, :, :, 1] > 0
+    assert (log[:, :, :, 1][ran] >= log[:, :, :, 0][ran]).all()
+    assert log[0, 1, :, 3].sum() > 0  # child records of level 1
+
+
 def test_last_level_walk_skip_is_invariant():
     """The depth-capped last level shades to zero whatever its rays hit, so skipping its
     closest-hit walk (tuning key 7, default on) changes no pixel and no ray count; the walked-ray
