@@ -160,7 +160,9 @@ int64_t mrt_wave_log(mrt_renderer *r, uint64_t *out);
  * key 6 = shadow walk grid, percent of its occupancy grid (1-100; 0 default: by paths per walk lane),
  * key 7 = skip the closest-hit walk of the depth-capped last level (1, default),
  * key 8 = tail donation: idle lanes of a level's tail walk subtrees of their wave's rays (0, 1 default),
- * key 9 = idle lanes before a walk wave fetches new rays (1-64, default 32) */
+ * key 9 = idle lanes before a walk wave fetches new rays (1-64, default 32),
+ * key 10 = k_shade's lean instantiation where it applies (1, default) or always the general one (0),
+ * key 11 = k_shade workgroups per CU (default 14; 0: 8) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /

@@ -119,7 +119,7 @@ class Renderer:
         of child / shadow rays, 5 = shadow-walk child order (0 near first, 1 far first),
         6 = shadow-walk grid percent (0 auto), 7 = no walk for the depth-capped last level, 8 = tail
         donation (idle lanes of a level's tail walk subtrees of their wave's rays), 9 = refill
-        threshold of the walk waves."""
+        threshold of the walk waves, 10 = lean k_shade instantiation, 11 = k_shade workgroups per CU."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 
     def get_tuning(self, key: int) -> int:

@@ -52,6 +52,7 @@ struct DScene {
     int32_t anyOrder;          // shadow walk child order (tuning key 5): 0 near first, 1 far first (default)
     int32_t tailDonate;        // idle lanes of a level's tail help walking lanes (tuning key 8, mrt_trace_ww.hpp)
     int32_t refill;            // idle lanes before a walk wave fetches new rays (tuning key 9, default 32)
+    int32_t leanShade;         // k_shade's lean instantiation where it applies (tuning key 10)
     // textures (map_Kd): scenes with a textured material only (`textured` != 0)
     const float4* triTex;      // 2 per triangle: (tA.xy, tB.xy), (tC.xy, -, -)
     const int4* texInfo;       // per texture: width, height, channels, first byte in texels

@@ -125,6 +125,9 @@ struct mrt_renderer {
     int chunkSlots = 0;
     int gdepth = 0;
     int traceThreads = 0, workGrid = 0;  // traceThreads: resident trace threads, whole device
+    int cus = 0;
+    int shadeGridPerCU = 14;             // tuning key 11: k_shade workgroups per CU (two per resident slot of
+                                         // the lean kernel; 0: workGrid)
     int32_t* dBitmap = nullptr;  // for the host-bitmap entry point
     int32_t* dBackup = nullptr;  // progressive mode: the running average before the current pass
     size_t backupN = 0;
@@ -392,6 +395,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.anyOrder = 1;
     d.tailDonate = 1;
     d.refill = 32;  // kWalkRefill
+    d.leanShade = 1;
     d.matsFinite = 1;
     for (const HMaterial& m : sc.materials) {
         for (const v3 c : {m.Kd, m.Ks, m.Kt})
@@ -561,7 +565,8 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             if (!(skipLastShade && l == nLevels)) {
-                launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, st,
+                launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa,
+                            r->shadeGridPerCU > 0 ? r->cus * r->shadeGridPerCU : r->workGrid, st,
                             skipLastShade && l + 1 == nLevels);
                 ++r->shadeLaunches;
             }
@@ -768,6 +773,7 @@ mrt_renderer* createRenderer(const mrt_config* cfg, const MemScene* mem = nullpt
     MRT_HIP(hipGetDeviceProperties(&prop, r->device));
     r->traceThreads = prop.multiProcessorCount * traceResidentThreadsPerCU();
     r->workGrid = prop.multiProcessorCount * 8;
+    r->cus = prop.multiProcessorCount;
 
     // scene (C_wrapper.cpp:68-141)
     const float ratio = static_cast<float>(cfg->width) / static_cast<float>(cfg->height);
@@ -1011,6 +1017,14 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->binMode = value;
         return 0;
     }
+    if (key == 11 && value >= 0 && value <= 64) {
+        r->shadeGridPerCU = value;
+        return 0;
+    }
+    if (key == 10 && (value == 0 || value == 1)) {
+        r->ds.leanShade = value;
+        return 0;
+    }
     if (key == 9 && value >= 1 && value <= 64) {
         r->ds.refill = value;
         return 0;
@@ -1146,6 +1160,8 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 6: *value = r->shadowGridPct; return 0;
         case 8: *value = r->ds.tailDonate; return 0;
         case 9: *value = r->ds.refill; return 0;
+        case 10: *value = r->ds.leanShade; return 0;
+        case 11: *value = r->shadeGridPerCU; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

@@ -392,16 +392,19 @@ def test_tail_donation_matches_oracle_and_is_invariant(oracle_mod):
 
 
 def test_walk_knobs_are_invariant_and_wave_log_is_consistent():
-    """The shadow walk's grid size (tuning key 6) and the walk's refill threshold (key 9) change
-    only scheduling: same bitmap and ray counts.  In counting mode the wave log holds one entry per
+    """The shadow walk's grid size (tuning key 6), the walk's refill threshold (key 9), k_shade's
+    lean or general instantiation (key 10) and its grid (key 11) change only scheduling: same
+    bitmap and ray counts.  In counting mode the wave log holds one entry per
     resident wave of every walk launch, and its rays add up to the frame's walked rays."""
     import mobileraytracer_amd as m
     cfg = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5)
     outs = []
     with m.Renderer(cfg) as r:
-        for key, val in ((6, 0), (6, 40), (6, 100), (9, 1), (9, 64)):
+        for key, val in ((6, 0), (6, 40), (6, 100), (9, 1), (9, 64), (10, 0), (11, 3)):
             r.set_tuning(6, 0)
             r.set_tuning(9, 32)
+            r.set_tuning(10, 1)
+            r.set_tuning(11, 14)
             r.set_tuning(key, val)
             assert r.get_tuning(key) == val
             bm = np.zeros(cfg.width * cfg.height, np.int32)
