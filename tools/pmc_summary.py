@@ -12,7 +12,7 @@ TA / TD busy) are averaged per kernel as they are.
 import csv, glob, json, os, re, sys
 from collections import defaultdict
 
-PRODUCT = {"k_trace": r"k_trace<false, 1, 1>", "k_shadow": r"k_shadow<false, 1, 1>", "k_shade": r"k_shade<2>"}
+PRODUCT = {"k_trace": r"k_trace<false, 1, 1>", "k_shadow": r"k_shadow<false, 1, 1>", "k_shade": r"k_shade<2, false>"}
 
 
 def rows(d):
