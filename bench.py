@@ -30,6 +30,14 @@ import os
 import sys
 import time
 
+# Hardware queues per process (read by the HIP runtime at its initialisation, so before torch is
+# imported).  HIP's default of 4 is shared by every stream of the process: with RCCL's and
+# torch's streams created, the renderer's render and shadow streams can land on one queue and the
+# shadow walk then no longer overlaps the next level (one rank's C4 shard at N = 8: 2.81 ms
+# without a process group, 3.54 ms with one at 4 queues, 2.87 ms at 8).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
@@ -168,14 +176,13 @@ def main():
     # MRT_BENCH_BACKEND=gloo (rehearsal only: several ranks sharing one GPU, gather through host
     # memory); the measured multi-GPU path is RCCL ("nccl") with one GPU per rank
     backend = os.environ.get("MRT_BENCH_BACKEND", "nccl")
-    if world > 1:
+    # MRT_BENCH_FORCE_DIST=1 (rehearsal only): the multi-GPU path (process group, packed shard,
+    # gather, unpack) even at world size 1, so a one-GPU box exercises the RCCL calls
+    dist_on = world > 1 or os.environ.get("MRT_BENCH_FORCE_DIST") == "1"
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         local = local % torch.cuda.device_count() if backend == "gloo" else local
         torch.cuda.set_device(local)
-        if backend == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     scene = scenes.conference()
@@ -183,7 +190,14 @@ def main():
                    samplesPixel=args.spp, samplesLight=1, maxDepth=args.max_depth, objFilePath=scene[0],
                    mtlFilePath=scene[1], camFilePath=scene[2], rankIndex=rank, rankCount=world,
                    device=torch.cuda.current_device())
+    # the renderer (and its two HIP streams) before the process group, so that RCCL's streams
+    # take the later hardware queues
     r = m.Renderer(cfg)
+    if dist_on:
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     r.set_tuning(3, args.overlap)
     info = r.scene_info()
     stream = torch.cuda.current_stream()
@@ -194,7 +208,7 @@ def main():
     gathered = torch.zeros((world, slots_max), dtype=torch.int32, device="cuda") if rank == 0 else None
 
     def step():
-        if world == 1:
+        if not dist_on:
             r.render_frame_device(bitmap.data_ptr(), 0, sh)
         else:
             r.render_frame_device(0, packed.data_ptr(), sh)
@@ -214,7 +228,7 @@ def main():
     kernels, per_ray = kernel_roofline(r, step)
     r.set_tuning(3, args.overlap)
 
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     rays0 = r.get_total_casted_rays()
@@ -225,12 +239,12 @@ def main():
         st = r.frame_stats()
         walked += st["walkedRays"] + st["shadowRays"]
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     rays = r.get_total_casted_rays() - rays0
 
-    if world > 1:
+    if dist_on:
         red = "cpu" if backend == "gloo" else "cuda"
         t = torch.tensor([elapsed], dtype=torch.float64, device=red)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -273,7 +287,7 @@ def main():
             "spp": args.spp, "max_depth": args.max_depth, "samples_light": 1,
             "shader": "PathTracer" if args.shader == 2 else "Whitted",
             "parallelism": (f"screen-tile shard x{world} + " + ("RCCL gather" if backend == "nccl" else "gloo gather (rehearsal)"))
-            if world > 1 else "single GPU",
+            if dist_on else "single GPU",
             "rays_walked_per_frame": walked / frames,
             "rays_built_per_frame": rays / frames,
             "mrays_per_s_built": rays / elapsed / 1e6,
@@ -309,7 +323,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args, scene)
     print(json.dumps(out), flush=True)
     r.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -293,7 +293,8 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, i
         __shared__ GNode ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, tailBest);
+        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, tailBest,
+                                              lv.rPerm);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -329,7 +330,8 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, 
         __shared__ GNode ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest);
+        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest,
+                                             lv.sPerm);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -887,13 +889,14 @@ __global__ __launch_bounds__(256) void k_accumulate(AccumArgs a, const float4* r
 }
 
 // scatter a gathered, rank-packed buffer into the bitmap (multi-GPU frame assembly)
-__global__ __launch_bounds__(256) void k_unpack(PixelMap map, int width, int nSlots, const int32_t* packed,
-                                                int32_t* bitmap) {
+// every rank's shard in one launch: blockIdx.y = rank (of the batch)
+__global__ __launch_bounds__(256) void k_unpack_ranks(UnpackArgs a, const int32_t* gathered, int32_t* bitmap) {
+    const int k = static_cast<int>(blockIdx.y);
     const int q = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
-    if (q >= nSlots) return;
+    if (q >= a.n[k]) return;
     int x, y;
-    slotToXY(map, q, &x, &y);
-    bitmap[y * width + x] = packed[q];
+    slotToXY(a.maps[k], q, &x, &y);
+    bitmap[y * a.width + x] = gathered[static_cast<size_t>(a.first + k) * static_cast<size_t>(a.stride) + q];
 }
 
 // primary-hit dump (config C2): per path slot (kind, index, t)
@@ -989,6 +992,100 @@ void launchLoadRays(const Level& lv, const float* orig, const float* dir, const 
 }
 
 // ---------------------------------------------------------------------------------------
+// Ray sorting (tuning key 12): a counting sort of one queue by a spatial key.  Rays that start
+// close together (and, keyMode 1, point into the same octant) become neighbours in the walk's
+// queue order, so a wave's refill fetches rays that share the upper part of their walk.  Only
+// the order of the walk changes, never a ray's result.
+__device__ __forceinline__ uint32_t sortKey(const DScene& s, float4 o4, float4 d4, int mode) {
+    const int bits = mode == 0 ? 4 : 3;
+    const float cells = static_cast<float>(1 << bits);
+    const float o[3] = {o4.x, o4.y, o4.z};
+    uint32_t q[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float ext = s.triRoot.bmax[a] - s.triRoot.bmin[a];
+        const float f = ext > 0.0F ? (o[a] - s.triRoot.bmin[a]) / ext * cells : 0.0F;
+        q[a] = f >= 1.0F ? static_cast<uint32_t>(fminf(f, cells - 1.0F)) : 0u;  // NaN, < 1: cell 0
+    }
+    uint32_t m = 0;
+    for (int b = 0; b < bits; ++b)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) m |= ((q[a] >> b) & 1u) << (3 * b + a);
+    if (mode == 1) m |= static_cast<uint32_t>((d4.x < 0.0F ? 1 : 0) | (d4.y < 0.0F ? 2 : 0) | (d4.z < 0.0F ? 4 : 0)) << 9;
+    return m;
+}
+
+__device__ __forceinline__ int sortCount(const Level& lv, const int* counters, int level, bool shadow) {
+    return shadow ? min(counters[cntShadows(level)], lv.shadowCap) : min(counters[cntRays(level)], lv.cap);
+}
+
+// pass 1: keys, the block's histogram in LDS, and the block's offset inside each bin
+__global__ __launch_bounds__(kSortThreads) void k_sort_keys(DScene s, Level lv, const int* counters, int level,
+                                                            int shadow, int mode, SortBufs b) {
+    __shared__ int h[kSortBins];
+    for (int i = static_cast<int>(threadIdx.x); i < kSortBins; i += kSortThreads) h[i] = 0;
+    __syncthreads();
+    const int count = sortCount(lv, counters, level, shadow != 0);
+    const float4* O = shadow != 0 ? lv.sO : lv.rO;
+    const float4* D = shadow != 0 ? lv.sD : lv.rD;
+    const int lo = static_cast<int>(static_cast<long long>(count) * blockIdx.x / gridDim.x);
+    const int hi = static_cast<int>(static_cast<long long>(count) * (blockIdx.x + 1) / gridDim.x);
+    for (int i = lo + static_cast<int>(threadIdx.x); i < hi; i += kSortThreads) {
+        const uint32_t k = sortKey(s, O[i], D[i], mode);
+        b.keys[i] = static_cast<uint16_t>(k);
+        atomicAdd(&h[k], 1);
+    }
+    __syncthreads();
+    int* off = b.blockOff + static_cast<size_t>(blockIdx.x) * kSortBins;
+    for (int k = static_cast<int>(threadIdx.x); k < kSortBins; k += kSortThreads) {
+        const int c = h[k];
+        off[k] = c > 0 ? atomicAdd(b.hist + k, c) : 0;
+    }
+}
+
+// pass 2 (one block): bin starts; clears the histogram for the next sort
+__global__ __launch_bounds__(kSortThreads) void k_sort_scan(SortBufs b) {
+    constexpr int kPer = kSortBins / kSortThreads;
+    __shared__ int waveSum[kSortThreads / 64];
+    const int t = static_cast<int>(threadIdx.x);
+    int v[kPer], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        v[j] = b.hist[t * kPer + j];
+        b.hist[t * kPer + j] = 0;
+        sum += v[j];
+    }
+    int total;
+    const int excl = waveExclusiveScan(sum, &total);
+    if (laneId() == 0) waveSum[t >> 6] = total;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < (t >> 6); ++w) base += waveSum[w];
+    int run = base + excl;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        b.start[t * kPer + j] = run;
+        run += v[j];
+    }
+}
+
+// pass 3: every ray's position; perm[position] = ray (order inside a bin is arbitrary)
+__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Level lv, const int* counters, int level, int shadow,
+                                                               SortBufs b) {
+    __shared__ int cur[kSortBins];
+    const int* off = b.blockOff + static_cast<size_t>(blockIdx.x) * kSortBins;
+    for (int k = static_cast<int>(threadIdx.x); k < kSortBins; k += kSortThreads) cur[k] = b.start[k] + off[k];
+    __syncthreads();
+    const int count = sortCount(lv, counters, level, shadow != 0);
+    const int lo = static_cast<int>(static_cast<long long>(count) * blockIdx.x / gridDim.x);
+    const int hi = static_cast<int>(static_cast<long long>(count) * (blockIdx.x + 1) / gridDim.x);
+    for (int i = lo + static_cast<int>(threadIdx.x); i < hi; i += kSortThreads) {
+        const int pos = atomicAdd(&cur[b.keys[i]], 1);
+        b.perm[pos] = i;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // launch wrappers
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st) {
     const int blocks = (a.nPaths + 255) / 256;
@@ -1078,6 +1175,14 @@ void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, 
     }
 }
 
+void launchSort(const DScene& s, const Level& lv, int* counters, int level, bool shadow, int keyMode,
+                const SortBufs& b, hipStream_t st) {
+    const int sh = shadow ? 1 : 0;
+    hipLaunchKernelGGL(k_sort_keys, dim3(kSortBlocks), dim3(kSortThreads), 0, st, s, lv, counters, level, sh, keyMode, b);
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kSortThreads), 0, st, b);
+    hipLaunchKernelGGL(k_sort_scatter, dim3(kSortBlocks), dim3(kSortThreads), 0, st, lv, counters, level, sh, b);
+}
+
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                    const ShadeArgs& a, int grid, hipStream_t st, bool deadChildren) {
     const int dead = deadChildren ? 1 : 0;
@@ -1100,9 +1205,11 @@ void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, in
     hipLaunchKernelGGL(k_accumulate, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, a, res, bitmap, packed);
 }
 
-void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st) {
-    const int blocks = (nSlots + 255) / 256;
-    hipLaunchKernelGGL(k_unpack, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, map, width, nSlots, packed, bitmap);
+void launchUnpackRanks(const UnpackArgs& a, int ranks, int maxN, const int32_t* gathered, int32_t* bitmap,
+                       hipStream_t st) {
+    const int blocks = (maxN + 255) / 256;
+    if (ranks <= 0 || blocks <= 0) return;
+    hipLaunchKernelGGL(k_unpack_ranks, dim3(blocks, ranks), dim3(256), 0, st, a, gathered, bitmap);
 }
 
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st) {

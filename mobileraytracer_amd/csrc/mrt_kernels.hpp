@@ -67,6 +67,10 @@ struct Level {
     // material index, -1 none), and the last such write in the vertex's subtree (Shader.cpp:112-120)
     float4* kd;
     float4* last;
+    // ray sorting (tuning key 12, never changes results): queue position q of the closest-hit /
+    // shadow walk takes ray rPerm[q] / sPerm[q] (null: ray q)
+    const int* rPerm;
+    const int* sPerm;
     int cap;
     int shadowCap;
 };
@@ -117,6 +121,24 @@ struct AccumArgs {
     int pad;
 };
 
+// Ray sorting (tuning key 12): a counting sort of a level's closest-hit or shadow queue by a
+// spatial key into a permutation the walk reads its rays through (rPerm / sPerm).  Buffers of
+// one stream: keys and perm (queue capacity), hist / start (kSortBins), blockOff (kSortBlocks x
+// kSortBins).  keyMode 0: Morton code of the origin (4 bits per axis); 1: direction octant +
+// origin Morton (3 bits per axis).
+constexpr int kSortBins = 4096;
+constexpr int kSortBlocks = 256;
+constexpr int kSortThreads = 1024;
+struct SortBufs {
+    uint16_t* keys;
+    int* perm;
+    int* hist;   // zero between sorts (the scan clears it)
+    int* start;
+    int* blockOff;
+};
+void launchSort(const DScene& s, const Level& lv, int* counters, int level, bool shadow, int keyMode,
+                const SortBufs& b, hipStream_t st);
+
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                  unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
@@ -130,7 +152,19 @@ void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, 
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                    const ShadeArgs& a, int grid, hipStream_t st, bool deadChildren = false);
 void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, int32_t* packed, hipStream_t st);
-void launchUnpack(const PixelMap& map, int width, int nSlots, const int32_t* packed, int32_t* bitmap, hipStream_t st);
+// rank 0's frame assembly: up to kUnpackRanks shards per launch (rank first + k reads row first + k
+// of the gathered array, stride entries apart)
+constexpr int kUnpackRanks = 16;
+struct UnpackArgs {
+    PixelMap maps[kUnpackRanks];
+    int n[kUnpackRanks];
+    int width;
+    int first;
+    int stride;
+    int pad;
+};
+void launchUnpackRanks(const UnpackArgs& a, int ranks, int maxN, const int32_t* gathered, int32_t* bitmap,
+                       hipStream_t st);
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);
 void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel = 0);
 // known-answer kernels (device slab / triangle tests) and arbitrary-ray loading for tests

@@ -121,6 +121,7 @@ struct mrt_renderer {
         std::vector<hipEvent_t> syncPool;    // ordering events between the streams
         std::vector<hipEvent_t> evPool;      // profiling: 5 timing events per level and chunk
         size_t evCount = 0;
+        mrt::SortBufs sortR{}, sortS{};      // ray sorting (tuning key 12): closest-hit / shadow stream
     } pipe;
     int chunkSlots = 0;
     int gdepth = 0;
@@ -136,6 +137,9 @@ struct mrt_renderer {
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
     int binMode = 0;                     // tuning key 4: binned emission of child / shadow rays (ShadeArgs::binMode)
     int shadowGridPct = 0;               // tuning key 6: shadow walk grid, percent of its occupancy grid (0 auto)
+    int sortMode = 0;                    // tuning key 12: sort queues before their walk (1 shadow, 2 closest hit of levels >= 2)
+    int sortKeyShadow = 0;               // tuning key 13: sort key of shadow queues (launchSort keyMode)
+    int sortKeyRay = 1;                  // tuning key 14: sort key of closest-hit queues
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
 
@@ -462,10 +466,30 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
         lv.kd = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
         lv.last = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
     }
+    pp.sortR = SortBufs{};  // allocated on first use (ensureSortBufs)
+    pp.sortS = SortBufs{};
     pp.counters = r->queueMem.alloc<int>(kNumCounters);
     pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats + kWaveLogEntries);
     pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
     pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
+}
+
+// Sort buffers of both streams, sized for the largest queue of the current allocation.
+void ensureSortBufs(mrt_renderer* r, hipStream_t st) {
+    using namespace mrt;
+    mrt_renderer::Pipe& pp = r->pipe;
+    if (pp.sortR.keys != nullptr) return;
+    size_t n = 1;
+    for (int l = 1; l <= r->nLevels && l < kMaxLevels; ++l)
+        n = std::max({n, static_cast<size_t>(pp.levels[l].cap), static_cast<size_t>(pp.levels[l].shadowCap)});
+    for (SortBufs* b : {&pp.sortR, &pp.sortS}) {
+        b->keys = r->queueMem.alloc<uint16_t>(n);
+        b->perm = r->queueMem.alloc<int>(n);
+        b->hist = r->queueMem.alloc<int>(kSortBins);
+        b->start = r->queueMem.alloc<int>(kSortBins);
+        b->blockOff = r->queueMem.alloc<int>(static_cast<size_t>(kSortBlocks) * kSortBins);
+        MRT_HIP(hipMemsetAsync(b->hist, 0, sizeof(int) * kSortBins, st));
+    }
 }
 
 // Chunk size: every slot of the shard in one pass, within the path budget.
@@ -529,6 +553,9 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     // every material is finite (Ks * 0 and Kd * 0 added to sums that start at +0), and the
     // parents write no payload for them (only their count)
     const bool skipLastShade = skipLast && nLevels >= 2 && r->ds.matsFinite != 0;
+    // ray sorting applies to the while-while BVH walk (the only one that reads the permutation)
+    const int sortMode = r->ds.accel == kAccBVH && r->ds.variant == 1 ? r->sortMode : 0;
+    if (sortMode != 0) ensureSortBufs(r, st);  // the shadow stream waits on st before its first launch
     for (int slot0 = 0; slot0 < r->nSlots && !r->stopFlag.load(); slot0 += r->chunkSlots) {
         const int nChunk = std::min(r->chunkSlots, r->nSlots - slot0);
         MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
@@ -560,8 +587,14 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         }
         for (int l = 1; l <= nLevels; ++l) {
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-            if (!(skipLast && l == nLevels))
-                launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, st);
+            if (!(skipLast && l == nLevels)) {
+                Level lt = pp.levels[l];
+                if ((sortMode & 2) != 0 && l >= 2) {
+                    launchSort(r->ds, lt, pp.counters, l, false, r->sortKeyRay, pp.sortR, st);
+                    lt.rPerm = pp.sortR.perm;
+                }
+                launchTrace(r->ds, lt, pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, st);
+            }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             if (!(skipLastShade && l == nLevels)) {
@@ -579,7 +612,12 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
             // the last level (depth > RayDepthMax) shades nothing: no shadow rays
             if (l < nLevels) {
-                launchShadow(r->ds, pp.levels[l], pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
+                Level ls = pp.levels[l];
+                if ((sortMode & 1) != 0) {
+                    launchSort(r->ds, ls, pp.counters, l, true, r->sortKeyShadow, pp.sortS, sb);
+                    ls.sPerm = pp.sortS.perm;
+                }
+                launchShadow(r->ds, ls, pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
                              r->traceThreads, sb, shadowPct);
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
@@ -938,15 +976,24 @@ int mrt_render_frame_device(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked,
 int mrt_unpack_gathered(mrt_renderer* r, const int32_t* dGathered, int32_t* dBitmap, void* stream) {
     return guarded([&] {
         hipStream_t st = stream != nullptr ? static_cast<hipStream_t>(stream) : r->stream;
-        for (int k = 0; k < r->rankCount; ++k) {
-            const auto& pre = r->prefixByRank[static_cast<size_t>(k)];
-            const auto& un = r->unitsByRank[static_cast<size_t>(k)];
-            int n = 0;
-            if (!un.empty()) n = pre.back() + un.back().z * un.back().w;
-            mrt::launchUnpack(r->mapByRank[static_cast<size_t>(k)], r->cfg.width, n,
-                              dGathered + static_cast<size_t>(k) * static_cast<size_t>(r->maxSlots), dBitmap, st);
+        // one launch per kUnpackRanks shards (a launch per shard cost ~8 us each at N = 8)
+        for (int k0 = 0; k0 < r->rankCount; k0 += mrt::kUnpackRanks) {
+            mrt::UnpackArgs a{};
+            a.width = r->cfg.width;
+            a.first = k0;
+            a.stride = r->maxSlots;
+            const int ranks = std::min(mrt::kUnpackRanks, r->rankCount - k0);
+            int maxN = 0;
+            for (int j = 0; j < ranks; ++j) {
+                const auto k = static_cast<size_t>(k0 + j);
+                const auto& pre = r->prefixByRank[k];
+                const auto& un = r->unitsByRank[k];
+                a.maps[j] = r->mapByRank[k];
+                a.n[j] = un.empty() ? 0 : pre.back() + un.back().z * un.back().w;
+                maxN = std::max(maxN, a.n[j]);
+            }
+            mrt::launchUnpackRanks(a, ranks, maxN, dGathered, dBitmap, st);
         }
-        MRT_HIP(hipStreamSynchronize(st));
     });
 }
 
@@ -1031,6 +1078,18 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
     }
     if (key == 8 && (value == 0 || value == 1)) {
         r->ds.tailDonate = value;
+        return 0;
+    }
+    if (key == 12 && value >= 0 && value <= 3) {
+        r->sortMode = value;
+        return 0;
+    }
+    if (key == 13 && (value == 0 || value == 1)) {
+        r->sortKeyShadow = value;
+        return 0;
+    }
+    if (key == 14 && (value == 0 || value == 1)) {
+        r->sortKeyRay = value;
         return 0;
     }
     if (key == 6 && value >= 0 && value <= 100) {
@@ -1162,6 +1221,9 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 9: *value = r->ds.refill; return 0;
         case 10: *value = r->ds.leanShade; return 0;
         case 11: *value = r->shadeGridPerCU; return 0;
+        case 12: *value = r->sortMode; return 0;
+        case 13: *value = r->sortKeyShadow; return 0;
+        case 14: *value = r->sortKeyRay; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

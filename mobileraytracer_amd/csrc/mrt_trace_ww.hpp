@@ -229,11 +229,12 @@ __device__ __forceinline__ void stageTop(const DScene& s, GNode* ldsTop) {
 
 // kAny = false: closest hit -> out[i] = (t, u, v, primitive code);
 // kAny = true:  shadow any-hit -> out[i].w = occluded flag.
-// fetch: kWalkShards cursors, kFetchStride ints apart.
+// fetch: kWalkShards cursors, kFetchStride ints apart.  perm (or null): queue position -> ray.
 template <bool kAny, bool kCount, int kCull>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                TStack& st, TravCount* cnt, const GNode* ldsTop, int* tailBest) {
+                                                TStack& st, TravCount* cnt, const GNode* ldsTop, int* tailBest,
+                                                const int* __restrict__ perm) {
     constexpr int kHelper = -2;  // rayIdx of a lane walking a subtree given by another lane
     const bool donate = s.tailDonate != 0;
     const int top = min(kWalkTop, s.triTop);
@@ -370,7 +371,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 }
             }
             if (need) {
-                rayIdx = got;
+                rayIdx = got >= 0 && perm != nullptr ? perm[got] : got;  // sorted queues: through the permutation
                 if (kCount) {
                     cnt->rayStart = cnt->nodes;
                     if (got >= 0) ++cnt->rays;

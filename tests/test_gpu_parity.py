@@ -357,6 +357,36 @@ def test_binned_emission_and_shadow_order_are_invariant():
             assert outs[0][1:] == other[1:], cfg
 
 
+def test_ray_sorting_is_invariant():
+    """Sorting a queue by a spatial key before its walk (tuning key 12: 1 shadow queues, 2
+    closest-hit queues of levels >= 2; keys 13 / 14: origin Morton, or octant + Morton) changes
+    only the order in which the walk takes the rays: same bitmap and ray counts, over Whitted
+    (3-child vertices), PathTracer, several light samples, textures and chunked passes."""
+    import mobileraytracer_amd as m
+    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+             make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5, maxPathsPerPass=4096),
+             make_cfg(128, 128, shader=1, scene="water", max_depth=4),
+             make_cfg(96, 96, shader=2, scene="water", spp=2, max_depth=4, spl=3),
+             make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3),
+             make_cfg(64, 64, shader=2, spp=3, max_depth=6))
+    for cfg in cases:
+        outs = []
+        with m.Renderer(cfg) as r:
+            for mode, ks, kr, ov in ((0, 0, 1, 1), (3, 0, 1, 1), (3, 1, 0, 1), (1, 1, 1, 0), (2, 0, 0, 0)):
+                r.set_tuning(12, mode)
+                r.set_tuning(13, ks)
+                r.set_tuning(14, kr)
+                r.set_tuning(3, ov)
+                assert (r.get_tuning(12), r.get_tuning(13), r.get_tuning(14)) == (mode, ks, kr)
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"])))
+        for other in outs[1:]:
+            assert np.array_equal(outs[0][0], other[0]), cfg
+            assert outs[0][1:] == other[1:], cfg
+
+
 def test_tail_donation_matches_oracle_and_is_invariant(oracle_mod):
     """Tail donation (tuning key 8): in a level's tail an idle lane walks the oldest pending
     subtree of a walking lane of its wave and hands its best hit (closest) or occlusion (any-hit)
@@ -489,6 +519,15 @@ def test_shard_assembly_is_identical_to_single_gpu():
         # the numpy restatement of pack/unpack used by the CPU distributed tests agrees
         ref = np.full(1920 * 1080, SENTINEL, np.int32)
         assert np.array_equal(sharding.unpack(gathered, 1920, 1080, world, ref), single)
+
+
+def test_shard_assembly_over_many_ranks():
+    """More shards than one unpack launch takes (kUnpackRanks = 16): 17 ranks of a small frame
+    assemble to the single-GPU image."""
+    kw = dict(width=320, height=192, shader=2, scene="conference", spp=2, max_depth=5)
+    single, rays, _ = gpu_render(make_cfg(**kw))
+    img, _, srays = _render_shards(kw, 17)
+    assert np.array_equal(img, single) and srays == rays
 
 
 def test_c5_4k_8spp_shards():
