@@ -168,6 +168,21 @@ struct alignas(16) GNode {
 };
 static_assert(sizeof(GNode) == 64, "GNode must be 64 bytes");
 
+// Walk-tree node ("quantized walk tree"): both children's boxes as 16-bit
+// coordinates on one scene-wide grid (real value origin + q * step per axis), rounded OUTWARD by
+// one extra grid step, and the child references: 32 bytes, two 16-byte loads per visit instead
+// of four.  q[0] = Lminx | Lminy << 16, q[1] = Lminz | Lmaxx << 16, q[2] = Lmaxy | Lmaxz << 16,
+// q[3..5] the same for the right child.
+struct alignas(16) QNode {
+    uint32_t q[6];
+    int32_t refL, refR;
+};
+static_assert(sizeof(QNode) == 32, "QNode must be 32 bytes");
+struct QGrid {
+    float origin[3];
+    float step[3];
+};
+
 // Cull word of a BVH2 child (GNode::coneL / coneR): what bounds the
 // Moller-Trumbore t of every triangle below the child.  bits 0-17: the normal-line axis a
 // (octahedral, 9 + 9 bits), bits 18-24: q = sin(psi) in 1/126 steps, rounded up, where every

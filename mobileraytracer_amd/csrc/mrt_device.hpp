@@ -22,7 +22,11 @@ constexpr int kLdsStackMin = 8;     // per-thread stack entries (8 bytes) in LDS
 struct DScene {
     const float4* triGeom;     // 3 per triangle (BVH order): A, AB, AC  (xyz)
     const float4* triShade;    // 3 per triangle: nA (w = material index bits), nB, nC
-    const GNode* triNodes;
+    const GNode* triNodes;     // the reference tree (triRootRef)
+    const QNode* triQNodes;    // the walk tree (triRoot), quantized (QNode)
+    // the reference box of the leaf whose first triangle is t: [2t] = min xyz, max x; [2t+1].xy =
+    // max yz (walk-tree leaves are tested exactly before their triangles)
+    const float4* leafBoxes;
     const float4* planes;      // 2 per plane: normal (w = material bits), point
     const GNode* planeNodes;
     const float4* spheres;     // 2 per sphere: center (w = sqRadius), (x = material bits)
@@ -39,15 +43,18 @@ struct DScene {
     // table instead of 16 MB (the same values, relocated)
     const float4* vertexDraws;
     const float2* jitterDraws;  // per block: the pixel sampler's two draws (tree code 0, RaygenArgs::jitter)
-    // triRoot: the walk tree (the reference leaves regrouped, rebuildOverLeaves); triRootRef: the
-    // reference tree (BVH.hpp), in the same node array - for rays with a non-finite 1/d, whose slab
-    // NaNs break the leaf-box reachability argument, and for the per-wave reference walk
+    // triRoot: the walk tree (the reference leaves regrouped, rebuildOverLeaves, quantized);
+    // triRootRef: the reference tree (BVH.hpp) - for rays outside the quantized grid's error bound
+    // (a non-finite or extreme 1/d, whose slab NaNs or roundings break the leaf-box reachability
+    // argument), for the certified cull and for the per-wave reference walk
     GRoot triRoot, triRootRef, planeRoot, sphereRoot;
+    QGrid qgrid;               // the walk tree's quantization grid
+    int32_t qEnabled;          // 0: every ray walks the reference tree (a non-finite scene box)
     int32_t nLights;
     int32_t nMats;
     int32_t cull;              // walk 1's cull mode: 0 none, 1 fast, 2 certified (mrt_trace_ww.hpp)
     int32_t variant;           // trace walk: 0 per-wave reference walk, 1 persistent while-while
-    int32_t triTop;            // triNodes[0, triTop) are the breadth-first top of the tree
+    int32_t triTop;            // triQNodes[0, triTop) are the breadth-first top of the walk tree
     int32_t matsFinite;        // every material's Kd / Ks / Kt component is finite
     int32_t anyOrder;          // shadow walk child order (tuning key 5): 0 near first, 1 far first (default)
     int32_t tailDonate;        // idle lanes of a level's tail help walking lanes (tuning key 8, mrt_trace_ww.hpp)

@@ -260,18 +260,23 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     DScene& d = r->ds;
     // cull words (certified mode) for the reference tree only: that mode walks it for every ray
     const std::vector<uint32_t> conesRef = triangleConeWords(tn, sc.triangles);
-    toDeviceBVH(wn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop, regroup ? nullptr : &conesRef);
-    d.triRootRef = d.triRoot;
-    if (regroup) {
-        std::vector<GNode> gr;
-        toDeviceBVH(tn, sc.triangles.size(), &gr, &d.triRootRef, 0, nullptr, &conesRef);
-        const int32_t off = static_cast<int32_t>(g.size());
-        for (GNode& n : gr) {
-            if (n.refL >= 0) n.refL += off;
-            if (n.refR >= 0) n.refR += off;
+    // the walk tree, numbered (top breadth-first), then quantized; the reference tree in its own
+    // GNode array
+    toDeviceBVH(wn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop, nullptr);
+    std::vector<QNode> qn;
+    d.qEnabled = toQuantizedBVH(g, d.triRoot, &d.qgrid, &qn) ? 1 : 0;
+    if (d.qEnabled == 0 || qn.empty()) qn.resize(1);  // (a leaf or empty root: no inner node)
+    d.triQNodes = r->sceneMem.upload(qn, st);
+    toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRootRef, 0, nullptr, &conesRef);
+    {
+        std::vector<float4> lb(std::max<size_t>(1, 2 * sc.triangles.size()), make_float4(0.0F, 0.0F, 0.0F, 0.0F));
+        for (const HBVHNode& n : tn) {
+            if (n.numPrimitives <= 0) continue;
+            const size_t f = static_cast<size_t>(n.indexOffset);
+            lb[2 * f] = make_float4(n.box.mn.x, n.box.mn.y, n.box.mn.z, n.box.mx.x);
+            lb[2 * f + 1] = make_float4(n.box.mx.y, n.box.mx.z, 0.0F, 0.0F);
         }
-        if (d.triRootRef.ref >= 0 && d.triRootRef.count > 0) d.triRootRef.ref += off;
-        g.insert(g.end(), gr.begin(), gr.end());
+        d.leafBoxes = r->sceneMem.upload(lb, st);
     }
     d.triNodes = r->sceneMem.upload(g, st);
     toDeviceBVH(pn, sc.planes.size(), &g, &d.planeRoot);

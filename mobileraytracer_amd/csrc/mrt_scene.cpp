@@ -2,6 +2,7 @@
 #include "mrt_scene.hpp"
 
 #include <algorithm>
+#include <limits>
 #include <array>
 #include <atomic>
 #include <cmath>
@@ -961,6 +962,70 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
         g.coneR = cones != nullptr ? (*cones)[static_cast<size_t>(l + 1)] : kConeNever;
         (*out)[k] = g;
     }
+}
+
+// Outward 16-bit quantization of the walk tree.  The kernel evaluates a
+// plane as t = fma(q, fl(step * inv), fl(fl(origin - o) * inv)); for a ray whose origin lies
+// within 4 grid extents of the origin and whose 1/d components are in [2^-40, 2^90] that value is
+// within S |1/d| 2^-19 (S = the grid extent on that axis) of (origin + q step - o) / d, and the
+// reference's (b - o) * inv of an exact box b within as much of (b - o) / d.  A margin of one
+// grid step (S / 65535 > S 2^-19) on each side therefore keeps every computed slab interval of a
+// node around the computed interval of every reference leaf box below it.
+bool toQuantizedBVH(const std::vector<GNode>& nodes, const GRoot& root, QGrid* grid, std::vector<QNode>* out) {
+    out->clear();
+    double lo[3], ext[3], emax = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = root.bmin[a];
+        ext[a] = static_cast<double>(root.bmax[a]) - root.bmin[a];
+        if (!std::isfinite(lo[a]) || !std::isfinite(ext[a]) || ext[a] < 0.0) return false;
+        emax = std::max(emax, ext[a]);
+    }
+    double step[3], org[3];
+    for (int a = 0; a < 3; ++a) {
+        const double e = std::max({ext[a], emax * 0x1p-10, 0x1p-20});
+        // 65535 steps from origin = min - 2 step must reach max + 2 step: step >= e / 65531
+        const float sf = std::nextafter(static_cast<float>(e / 65528.0), std::numeric_limits<float>::infinity());
+        const float of = std::nextafter(static_cast<float>(lo[a] - 2.0 * sf), -std::numeric_limits<float>::infinity());
+        if (!std::isfinite(sf) || !std::isfinite(of) || !(sf > 0.0F)) return false;
+        step[a] = sf;
+        org[a] = of;
+        grid->step[a] = sf;
+        grid->origin[a] = of;
+    }
+    auto qlo = [&](float b, int a) -> uint32_t {  // largest q with origin + q step <= b - step
+        double q = std::floor((static_cast<double>(b) - org[a]) / step[a]) - 1.0;
+        q = std::min(std::max(q, 0.0), 65535.0);
+        while (q > 0.0 && org[a] + q * step[a] > static_cast<double>(b) - step[a]) q -= 1.0;
+        return static_cast<uint32_t>(q);
+    };
+    auto qhi = [&](float b, int a) -> uint32_t {  // smallest q with origin + q step >= b + step
+        double q = std::ceil((static_cast<double>(b) - org[a]) / step[a]) + 1.0;
+        q = std::min(std::max(q, 0.0), 65535.0);
+        while (q < 65535.0 && org[a] + q * step[a] < static_cast<double>(b) + step[a]) q += 1.0;
+        return static_cast<uint32_t>(q);
+    };
+    out->resize(nodes.size());
+    for (size_t k = 0; k < nodes.size(); ++k) {
+        const GNode& g = nodes[k];
+        const float b[12] = {g.lminx, g.lminy, g.lminz, g.lmaxx, g.lmaxy, g.lmaxz,
+                             g.rminx, g.rminy, g.rminz, g.rmaxx, g.rmaxy, g.rmaxz};
+        for (float v : b)
+            if (!std::isfinite(v)) {
+                out->clear();
+                return false;
+            }
+        uint32_t q[12];
+        for (int c = 0; c < 2; ++c)
+            for (int a = 0; a < 3; ++a) {
+                q[6 * c + a] = qlo(b[6 * c + a], a);
+                q[6 * c + 3 + a] = qhi(b[6 * c + 3 + a], a);
+            }
+        QNode& n = (*out)[k];
+        for (int w = 0; w < 6; ++w) n.q[w] = q[2 * w] | (q[2 * w + 1] << 16);
+        n.refL = g.refL;
+        n.refR = g.refR;
+    }
+    return true;
 }
 
 namespace {

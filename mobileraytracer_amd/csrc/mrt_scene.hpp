@@ -146,6 +146,9 @@ std::vector<HBVHNode> buildBVH(std::vector<T>* prims, std::vector<int32_t>* orde
 // cones: the cull word of every reference node (triangleConeWords), or null (never culled).
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
                  int topCount = 0, int* topPlaced = nullptr, const std::vector<uint32_t>* cones = nullptr);
+// The walk tree's GNodes (numbered by toDeviceBVH) as QNodes on a grid over the root box; false
+// (nothing written) when a box or the grid is not finite.
+bool toQuantizedBVH(const std::vector<GNode>& nodes, const GRoot& root, QGrid* grid, std::vector<QNode>* out);
 // A tree over the same leaves (primitive ranges and boxes) as the reference tree `ref`, grouped
 // by a full-sweep SAH; its inner boxes are exact unions of the leaf boxes (reference numbering:
 // node 0 the root, an inner node's children at indexOffset and indexOffset + 1).

@@ -153,33 +153,23 @@ __device__ __forceinline__ float cullLimit(float best) {
 }
 
 // One BVH2 inner-node visit: returns the next node (near child, or a popped entry).
-// Nodes [0, top) are read from the LDS copy ldsTop (the breadth-first top of the tree).
+// Reference-tree nodes (GNode, exact boxes, from global memory).
 // finite: wave-uniform, every active lane's 1/d is finite (slabFinite applies; otherwise the
 // exact slab, and the certified mode does not cull)
 template <int kCull>
-__device__ __forceinline__ int innerStep(BufRes nodes, const GNode* ldsTop, int top, int ref, v3 o, v3 d, v3 inv,
-                                         float lim, TStack& st, TravCount* cnt, bool count, bool finite,
-                                         int order) {
+__device__ __forceinline__ int innerStep(BufRes nodes, int ref, v3 o, v3 d, v3 inv, float lim, TStack& st,
+                                         TravCount* cnt, bool count, bool finite, int order) {
     constexpr bool cull = kCull != kCullNone;
-    float4 n0, n1, n2;
+    const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(GNode));
+    const float4 n0 = bload4(nodes, off);
+    const float4 n1 = bload4(nodes, off + 16u);
+    const float4 n2 = bload4(nodes, off + 32u);
     int4 n3;
-    if (ref < top) {
-        const float4* np = reinterpret_cast<const float4*>(ldsTop + ref);
-        n0 = np[0];
-        n1 = np[1];
-        n2 = np[2];
-        n3 = reinterpret_cast<const int4*>(np)[3];
+    if (kCull == kCullCertified) {
+        n3 = bload4i(nodes, off + 48u);  // child refs and cull words
     } else {
-        const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(GNode));
-        n0 = bload4(nodes, off);
-        n1 = bload4(nodes, off + 16u);
-        n2 = bload4(nodes, off + 32u);
-        if (kCull == kCullCertified) {
-            n3 = bload4i(nodes, off + 48u);  // child refs and cull words
-        } else {
-            const int2 r = bload2i(nodes, off + 48u);  // child refs
-            n3 = make_int4(r.x, r.y, 0, 0);
-        }
+        const int2 r = bload2i(nodes, off + 48u);  // child refs
+        n3 = make_int4(r.x, r.y, 0, 0);
     }
     if (count) cnt->nodes += 2;
     float tl, tr, kl = 0.0F, kr = 0.0F;
@@ -217,11 +207,70 @@ __device__ __forceinline__ int innerStep(BufRes nodes, const GNode* ldsTop, int 
     return chooseChildren(hl, hr, tl, tr, kl, kr, n3.x, n3.y, lim, cull, st, rightFirst);
 }
 
-// Copies the BVH2 top into LDS (all threads; ends with a barrier).
+// The quantized walk tree's planes: t = fma(q, qa, qb) with qa = step / d, qb = (origin - o) / d
+// per axis (rounded as toQuantizedBVH's bound assumes); the slab logic of slabFinite.
+__device__ __forceinline__ float qlo(uint32_t w) { return static_cast<float>(w & 0xFFFFu); }
+__device__ __forceinline__ float qhi(uint32_t w) { return static_cast<float>(w >> 16); }
+__device__ __forceinline__ bool qslab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, v3 qa, v3 qb,
+                                      float* tEntry) {
+    const float t1x = fmaf(mnx, qa.x, qb.x), t2x = fmaf(mxx, qa.x, qb.x);
+    const float t1y = fmaf(mny, qa.y, qb.y), t2y = fmaf(mxy, qa.y, qb.y);
+    const float t1z = fmaf(mnz, qa.z, qb.z), t2z = fmaf(mxz, qa.z, qb.z);
+    const float e = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fmaxf(fminf(t1z, t2z), 0.0F));
+    const float tMax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+    *tEntry = e;
+    return tMax >= e;
+}
+
+// One walk-tree visit (QNode: two 16-byte loads, or LDS for the top nodes).  Every box holds the
+// reference leaf boxes below it with the margin of toQuantizedBVH, so for the rays admitted to this
+// tree a node passes whenever a leaf below passes the reference test, and its entry is at most
+// that leaf's: the visit set is a superset of the reference's, and the leaves are tested exactly
+// before their triangles (traceWhileWhile).
+template <int kCull>
+__device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode* ldsTop, int top, int ref, v3 qa, v3 qb,
+                                          float lim, TStack& st, TravCount* cnt, bool count, int order) {
+    constexpr bool cull = kCull != kCullNone;
+    int4 a, b;
+    if (ref < top) {
+        const int4* np = reinterpret_cast<const int4*>(ldsTop + ref);
+        a = np[0];
+        b = np[1];
+    } else {
+        const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(QNode));
+        a = bload4i(qnodes, off);
+        b = bload4i(qnodes, off + 16u);
+    }
+    if (count) cnt->nodes += 2;
+    const uint32_t w0 = static_cast<uint32_t>(a.x), w1 = static_cast<uint32_t>(a.y), w2 = static_cast<uint32_t>(a.z),
+                   w3 = static_cast<uint32_t>(a.w), w4 = static_cast<uint32_t>(b.x), w5 = static_cast<uint32_t>(b.y);
+    float tl, tr;
+    const bool hl = qslab(qlo(w0), qhi(w0), qlo(w1), qhi(w1), qlo(w2), qhi(w2), qa, qb, &tl);
+    const bool hr = qslab(qlo(w3), qhi(w3), qlo(w4), qhi(w4), qlo(w5), qhi(w5), qa, qb, &tr);
+    const bool rightFirst = order == 0 ? tr < tl : !(tr < tl);
+    return chooseChildren(hl, hr, tl, tr, tl, tr, b.z, b.w, lim, cull, st, rightFirst);
+}
+
+// A ray may walk the quantized tree when the bound of toQuantizedBVH holds for it: every 1/d
+// component in [2^-40, 2^90] and the origin within 4 grid extents of the grid origin per axis.
+__device__ __forceinline__ bool quantOK(const DScene& s, v3 o, v3 inv) {
+    if (s.qEnabled == 0) return false;
+    const float ov[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float ai = fabsf(iv[a]);
+        ok = ok && ai >= 0x1p-40F && ai <= 0x1p90F &&
+             fabsf(ov[a] - s.qgrid.origin[a]) <= 4.0F * 65535.0F * s.qgrid.step[a];
+    }
+    return ok;
+}
+
+// Copies the walk tree's top into LDS (all threads; ends with a barrier).
 template <int kThreads>
-__device__ __forceinline__ void stageTop(const DScene& s, GNode* ldsTop) {
-    const int n = min(kWalkTop, s.triTop) * static_cast<int>(sizeof(GNode) / sizeof(float4));
-    const float4* src = reinterpret_cast<const float4*>(s.triNodes);
+__device__ __forceinline__ void stageTop(const DScene& s, QNode* ldsTop) {
+    const int n = min(kWalkTop, s.triTop) * static_cast<int>(sizeof(QNode) / sizeof(float4));
+    const float4* src = reinterpret_cast<const float4*>(s.triQNodes);
     float4* dst = reinterpret_cast<float4*>(ldsTop);
     for (int i = static_cast<int>(threadIdx.x); i < n; i += kThreads) dst[i] = src[i];
     __syncthreads();
@@ -233,18 +282,22 @@ __device__ __forceinline__ void stageTop(const DScene& s, GNode* ldsTop) {
 template <bool kAny, bool kCount, int kCull>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                TStack& st, TravCount* cnt, const GNode* ldsTop, int* tailBest,
+                                                TStack& st, TravCount* cnt, const QNode* ldsTop, int* tailBest,
                                                 const int* __restrict__ perm) {
     constexpr int kHelper = -2;  // rayIdx of a lane walking a subtree given by another lane
     const bool donate = s.tailDonate != 0;
     const int top = min(kWalkTop, s.triTop);
     const BufRes nodeBuf = bufferOf(s.triNodes);
+    const BufRes qBuf = bufferOf(s.triQNodes);
     const BufRes triBuf = bufferOf(s.triGeom);
+    const BufRes leafBuf = bufferOf(s.leafBoxes);
     constexpr bool cull = kCull != kCullNone;
     const int lane = static_cast<int>(threadIdx.x & 63u);
     int rayIdx = -1;
     bool exhausted = false;
     v3 o{0, 0, 0}, d{0, 0, 0}, inv{0, 0, 0};
+    v3 qa{0, 0, 0}, qb{0, 0, 0};  // quantized walk tree: t = fma(q, qa, qb) (innerStepQ)
+    bool refTree = true;          // this lane walks the reference tree (GNode) instead
     uint32_t src = 0;
     // closest hit so far: t and primitive code only; u, v are recomputed for the winner at
     // the end (same inputs -> same bits), which keeps two registers out of the walk
@@ -405,11 +458,18 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     if (rayIdx >= 0) {
                         float te;
                         const GRoot& r = s.triRoot;  // both trees have the same root box
+                        // rays outside the quantized tree's error bound (a non-finite or extreme
+                        // 1/d, a far origin) and the certified cull (its bounds are the reference
+                        // nodes') walk the reference tree (DScene::triRootRef)
+                        refTree = kCull == kCullCertified || !quantOK(s, o, inv);
+                        if (!refTree) {
+                            qa = v3{s.qgrid.step[0] * inv.x, s.qgrid.step[1] * inv.y, s.qgrid.step[2] * inv.z};
+                            qb = v3{(s.qgrid.origin[0] - o.x) * inv.x, (s.qgrid.origin[1] - o.y) * inv.y,
+                                    (s.qgrid.origin[2] - o.z) * inv.z};
+                        }
                         if (r.count > 0 &&
                             slab(r.bmin[0], r.bmin[1], r.bmin[2], r.bmax[0], r.bmax[1], r.bmax[2], o, inv, &te)) {
-                            // a non-finite 1/d, and the certified cull (its bounds are the
-                            // reference nodes'), walk the reference tree (DScene::triRootRef)
-                            ref = finiteInv(inv) && kCull != kCullCertified ? r.ref : s.triRootRef.ref;
+                            ref = refTree ? s.triRootRef.ref : r.ref;
                             if (ref < 0) {  // the root is a leaf
                                 leaf = ref;
                                 ref = kRefDone;
@@ -448,6 +508,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 const float dy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.y), dl));
                 const float dz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.z), dl));
                 const int dsrc = __builtin_amdgcn_readlane(static_cast<int>(src), dl);
+                const int dref = __builtin_amdgcn_readlane(refTree ? 1 : 0, dl);
                 const float dbt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bt), dl));
                 const int dbc = __builtin_amdgcn_readlane(static_cast<int>(bcode), dl);
                 if (lane == h) {
@@ -456,6 +517,12 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     o = v3{ox, oy, oz};
                     d = v3{dx, dy, dz};
                     inv = v3{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
+                    refTree = dref != 0;
+                    if (!refTree) {  // the donor's values (same inputs, same roundings)
+                        qa = v3{s.qgrid.step[0] * inv.x, s.qgrid.step[1] * inv.y, s.qgrid.step[2] * inv.z};
+                        qb = v3{(s.qgrid.origin[0] - o.x) * inv.x, (s.qgrid.origin[1] - o.y) * inv.y,
+                                (s.qgrid.origin[2] - o.z) * inv.z};
+                    }
                     src = static_cast<uint32_t>(dsrc);
                     bt = dbt;
                     bcode = static_cast<uint32_t>(dbc);
@@ -481,8 +548,9 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
             const float curLim = cullLimit<kCull>(fminf(bt, shT));
             const bool finite = __ballot(!finiteInv(inv)) == 0;
-            ref = innerStep<kCull>(nodeBuf, ldsTop, top, ref, o, d, inv, curLim, st, cnt, kCount, finite,
-                                   kAny ? s.anyOrder : 0);
+            const int order = kAny ? s.anyOrder : 0;
+            ref = refTree ? innerStep<kCull>(nodeBuf, ref, o, d, inv, curLim, st, cnt, kCount, finite, order)
+                          : innerStepQ<kCull>(qBuf, ldsTop, top, ref, qa, qb, curLim, st, cnt, kCount, order);
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
                 ref = popCulled(st, curLim, cull);
@@ -491,7 +559,18 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         }
         // ---- leaves ----
         while (leaf < 0) {
-            const int first = leafFirst(leaf), nprim = leafCount(leaf);
+            const int first = leafFirst(leaf);
+            int nprim = leafCount(leaf);
+            if (!refTree) {
+                // a walk-tree leaf passed a quantized (outward) box: the reference's own test of
+                // its exact box, and the cull against that box's entry, decide (BVH.hpp:357-363)
+                const uint32_t lo = static_cast<uint32_t>(first) * 32u;
+                const float4 b0 = bload4(leafBuf, lo);
+                const int2 b1 = bload2i(leafBuf, lo + 16u);
+                float te;
+                const bool in = slabFinite(b0.x, b0.y, b0.z, b0.w, __int_as_float(b1.x), __int_as_float(b1.y), o, inv, &te);
+                if (!in || (cull && te > cullLimit<kCull>(fminf(bt, shT)))) nprim = 0;
+            }
             bool hit = false;
             for (int k = 0; k < nprim; ++k) {
                 const int j = first + k;
