@@ -23,7 +23,7 @@ struct DScene {
     const float4* triGeom;     // 3 per triangle (BVH order): A, AB, AC  (xyz)
     const float4* triShade;    // 3 per triangle: nA (w = material index bits), nB, nC
     const GNode* triNodes;     // the reference tree (triRootRef)
-    const QNode* triQNodes;    // the walk tree (triRoot), quantized (QNode)
+    const QNode4* triQNodes;   // the walk tree (triRoot), 4-wide and quantized (QNode4)
     // the reference box of the leaf whose first triangle is t: [2t] = min xyz, max x; [2t+1].xy =
     // max yz (walk-tree leaves are tested exactly before their triangles)
     const float4* leafBoxes;

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, i
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
     if (kVariant == 1) {
-        __shared__ QNode ldsTop[kWalkTop];
+        __shared__ QNode4 ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
         traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, tailBest,
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, 
     int* fetch = counters + kCntFetchShards + (kMaxLevels + level) * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
     if (kVariant == 1) {
-        __shared__ QNode ldsTop[kWalkTop];
+        __shared__ QNode4 ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
         traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest,

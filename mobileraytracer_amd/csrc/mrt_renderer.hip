@@ -262,11 +262,24 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     const std::vector<uint32_t> conesRef = triangleConeWords(tn, sc.triangles);
     // the walk tree, numbered (top breadth-first), then quantized; the reference tree in its own
     // GNode array
-    toDeviceBVH(wn, sc.triangles.size(), &g, &d.triRoot, kTopNodesMax, &d.triTop, nullptr);
-    std::vector<QNode> qn;
-    d.qEnabled = toQuantizedBVH(g, d.triRoot, &d.qgrid, &qn) ? 1 : 0;
+    std::vector<QNode4> qn;
+    d.qEnabled = toQuantizedBVH4(wn, sc.triangles.size(), &d.triRoot, kTopNodesMax, &d.triTop, &d.qgrid, &qn) ? 1 : 0;
     if (d.qEnabled == 0 || qn.empty()) qn.resize(1);  // (a leaf or empty root: no inner node)
     d.triQNodes = r->sceneMem.upload(qn, st);
+    // a 4-wide visit pushes up to three entries: the walk's stack holds 3 per level
+    {
+        int depth4 = 0;
+        std::vector<std::pair<int32_t, int>> w;
+        if (d.qEnabled != 0 && d.triRoot.count > 0 && d.triRoot.ref >= 0) w.push_back({d.triRoot.ref, 1});
+        while (!w.empty()) {
+            const auto [i, dep] = w.back();
+            w.pop_back();
+            depth4 = std::max(depth4, dep);
+            for (int32_t c : qn[static_cast<size_t>(i)].ref)
+                if (c >= 0 && c != kEmptyChild) w.push_back({c, dep + 1});
+        }
+        r->stackNeed = std::max(r->stackNeed, 3 * depth4 + 2);
+    }
     toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRootRef, 0, nullptr, &conesRef);
     {
         std::vector<float4> lb(std::max<size_t>(1, 2 * sc.triangles.size()), make_float4(0.0F, 0.0F, 0.0F, 0.0F));

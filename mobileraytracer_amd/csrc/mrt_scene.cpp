@@ -971,60 +971,184 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
 // reference's (b - o) * inv of an exact box b within as much of (b - o) / d.  A margin of one
 // grid step (S / 65535 > S 2^-19) on each side therefore keeps every computed slab interval of a
 // node around the computed interval of every reference leaf box below it.
-bool toQuantizedBVH(const std::vector<GNode>& nodes, const GRoot& root, QGrid* grid, std::vector<QNode>* out) {
-    out->clear();
-    double lo[3], ext[3], emax = 0.0;
-    for (int a = 0; a < 3; ++a) {
-        lo[a] = root.bmin[a];
-        ext[a] = static_cast<double>(root.bmax[a]) - root.bmin[a];
-        if (!std::isfinite(lo[a]) || !std::isfinite(ext[a]) || ext[a] < 0.0) return false;
-        emax = std::max(emax, ext[a]);
+namespace {
+// the grid of toQuantizedBVH over a root box, and the outward rounding of one coordinate
+struct Quantizer {
+    double step[3] = {}, org[3] = {};
+    bool init(const float* bmin, const float* bmax, QGrid* grid) {
+        double lo[3], ext[3], emax = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = bmin[a];
+            ext[a] = static_cast<double>(bmax[a]) - bmin[a];
+            if (!std::isfinite(lo[a]) || !std::isfinite(ext[a]) || ext[a] < 0.0) return false;
+            emax = std::max(emax, ext[a]);
+        }
+        for (int a = 0; a < 3; ++a) {
+            const double e = std::max({ext[a], emax * 0x1p-10, 0x1p-20});
+            // 65535 steps from origin = min - 2 step must reach max + 2 step: step >= e / 65531
+            const float sf = std::nextafter(static_cast<float>(e / 65528.0), std::numeric_limits<float>::infinity());
+            const float of = std::nextafter(static_cast<float>(lo[a] - 2.0 * sf), -std::numeric_limits<float>::infinity());
+            if (!std::isfinite(sf) || !std::isfinite(of) || !(sf > 0.0F)) return false;
+            step[a] = sf;
+            org[a] = of;
+            grid->step[a] = sf;
+            grid->origin[a] = of;
+        }
+        return true;
     }
-    double step[3], org[3];
-    for (int a = 0; a < 3; ++a) {
-        const double e = std::max({ext[a], emax * 0x1p-10, 0x1p-20});
-        // 65535 steps from origin = min - 2 step must reach max + 2 step: step >= e / 65531
-        const float sf = std::nextafter(static_cast<float>(e / 65528.0), std::numeric_limits<float>::infinity());
-        const float of = std::nextafter(static_cast<float>(lo[a] - 2.0 * sf), -std::numeric_limits<float>::infinity());
-        if (!std::isfinite(sf) || !std::isfinite(of) || !(sf > 0.0F)) return false;
-        step[a] = sf;
-        org[a] = of;
-        grid->step[a] = sf;
-        grid->origin[a] = of;
-    }
-    auto qlo = [&](float b, int a) -> uint32_t {  // largest q with origin + q step <= b - step
+    uint32_t lo(float b, int a) const {  // largest q with origin + q step <= b - step
         double q = std::floor((static_cast<double>(b) - org[a]) / step[a]) - 1.0;
         q = std::min(std::max(q, 0.0), 65535.0);
         while (q > 0.0 && org[a] + q * step[a] > static_cast<double>(b) - step[a]) q -= 1.0;
         return static_cast<uint32_t>(q);
-    };
-    auto qhi = [&](float b, int a) -> uint32_t {  // smallest q with origin + q step >= b + step
+    }
+    uint32_t hi(float b, int a) const {  // smallest q with origin + q step >= b + step
         double q = std::ceil((static_cast<double>(b) - org[a]) / step[a]) + 1.0;
         q = std::min(std::max(q, 0.0), 65535.0);
         while (q < 65535.0 && org[a] + q * step[a] < static_cast<double>(b) + step[a]) q += 1.0;
         return static_cast<uint32_t>(q);
-    };
+    }
+    // one box as three words: minx | miny << 16, minz | maxx << 16, maxy | maxz << 16
+    bool box(const float* mn, const float* mx, uint32_t* w) const {
+        for (int a = 0; a < 3; ++a)
+            if (!std::isfinite(mn[a]) || !std::isfinite(mx[a])) return false;
+        const uint32_t q[6] = {lo(mn[0], 0), lo(mn[1], 1), lo(mn[2], 2), hi(mx[0], 0), hi(mx[1], 1), hi(mx[2], 2)};
+        for (int k = 0; k < 3; ++k) w[k] = q[2 * k] | (q[2 * k + 1] << 16);
+        return true;
+    }
+};
+}  // namespace
+
+bool toQuantizedBVH(const std::vector<GNode>& nodes, const GRoot& root, QGrid* grid, std::vector<QNode>* out) {
+    out->clear();
+    Quantizer qz;
+    if (!qz.init(root.bmin, root.bmax, grid)) return false;
     out->resize(nodes.size());
     for (size_t k = 0; k < nodes.size(); ++k) {
         const GNode& g = nodes[k];
-        const float b[12] = {g.lminx, g.lminy, g.lminz, g.lmaxx, g.lmaxy, g.lmaxz,
-                             g.rminx, g.rminy, g.rminz, g.rmaxx, g.rmaxy, g.rmaxz};
-        for (float v : b)
-            if (!std::isfinite(v)) {
-                out->clear();
-                return false;
-            }
-        uint32_t q[12];
-        for (int c = 0; c < 2; ++c)
-            for (int a = 0; a < 3; ++a) {
-                q[6 * c + a] = qlo(b[6 * c + a], a);
-                q[6 * c + 3 + a] = qhi(b[6 * c + 3 + a], a);
-            }
+        const float lmn[3] = {g.lminx, g.lminy, g.lminz}, lmx[3] = {g.lmaxx, g.lmaxy, g.lmaxz};
+        const float rmn[3] = {g.rminx, g.rminy, g.rminz}, rmx[3] = {g.rmaxx, g.rmaxy, g.rmaxz};
         QNode& n = (*out)[k];
-        for (int w = 0; w < 6; ++w) n.q[w] = q[2 * w] | (q[2 * w + 1] << 16);
+        if (!qz.box(lmn, lmx, n.q) || !qz.box(rmn, rmx, n.q + 3)) {
+            out->clear();
+            return false;
+        }
         n.refL = g.refL;
         n.refR = g.refR;
     }
+    return true;
+}
+
+bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
+                     QGrid* grid, std::vector<QNode4>* out) {
+    out->clear();
+    if (topPlaced != nullptr) *topPlaced = 0;
+    const HBVHNode& r = nodes[0];
+    const float rmn[3] = {r.box.mn.x, r.box.mn.y, r.box.mn.z}, rmx[3] = {r.box.mx.x, r.box.mx.y, r.box.mx.z};
+    for (int a = 0; a < 3; ++a) {
+        root->bmin[a] = rmn[a];
+        root->bmax[a] = rmx[a];
+    }
+    root->count = static_cast<int32_t>(numPrims);
+    root->ref = 0;
+    Quantizer qz;
+    const bool gridOK = qz.init(rmn, rmx, grid);
+    if (numPrims == 0) return gridOK;
+    if (r.numPrimitives > 0) {
+        root->ref = leafRef(r.indexOffset, r.numPrimitives);
+        return gridOK;
+    }
+    if (!gridOK) return false;
+    auto inner = [&](int32_t i) { return nodes[static_cast<size_t>(i)].numPrimitives == 0; };
+    auto area = [&](int32_t i) {
+        const HAABB& b = nodes[static_cast<size_t>(i)].box;
+        const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,
+                     dz = static_cast<double>(b.mx.z) - b.mn.z;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    // collapse: the 4-wide node of BVH2 node i has up to four BVH2 descendants as children
+    std::vector<std::array<int32_t, 4>> kids;  // per 4-wide node: BVH2 indices (-1: none)
+    std::vector<int32_t> node4Of(nodes.size(), -1);
+    std::vector<int32_t> work{0};
+    node4Of[0] = 0;
+    kids.push_back({-1, -1, -1, -1});
+    while (!work.empty()) {
+        const int32_t i = work.back();
+        work.pop_back();
+        const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
+        std::vector<int32_t> c{l, l + 1};
+        while (c.size() < 4) {
+            int best = -1;
+            double ba = -1.0;
+            for (size_t k = 0; k < c.size(); ++k)
+                if (inner(c[k]) && area(c[k]) > ba) {
+                    ba = area(c[k]);
+                    best = static_cast<int>(k);
+                }
+            if (best < 0) break;
+            const int32_t cl = nodes[static_cast<size_t>(c[static_cast<size_t>(best)])].indexOffset;
+            c[static_cast<size_t>(best)] = cl;
+            c.insert(c.begin() + best + 1, cl + 1);
+        }
+        std::array<int32_t, 4> k4{-1, -1, -1, -1};
+        for (size_t k = 0; k < c.size(); ++k) {
+            k4[k] = c[k];
+            if (inner(c[k])) {
+                node4Of[static_cast<size_t>(c[k])] = static_cast<int32_t>(kids.size());
+                kids.push_back({-1, -1, -1, -1});
+                work.push_back(c[k]);
+            }
+        }
+        kids[static_cast<size_t>(node4Of[static_cast<size_t>(i)])] = k4;
+    }
+    // numbering: the first topCount breadth-first, the rest depth-first pre-order
+    const size_t n4 = kids.size();
+    std::vector<int32_t> newIdx(n4, -1), order;
+    std::deque<int32_t> bfs{0};
+    while (!bfs.empty() && static_cast<int>(order.size()) < topCount) {
+        const int32_t j = bfs.front();
+        bfs.pop_front();
+        newIdx[static_cast<size_t>(j)] = static_cast<int32_t>(order.size());
+        order.push_back(j);
+        for (int32_t c : kids[static_cast<size_t>(j)])
+            if (c >= 0 && inner(c)) bfs.push_back(node4Of[static_cast<size_t>(c)]);
+    }
+    if (topPlaced != nullptr) *topPlaced = static_cast<int>(order.size());
+    std::vector<int32_t> dfs{0};
+    while (!dfs.empty()) {
+        const int32_t j = dfs.back();
+        dfs.pop_back();
+        if (newIdx[static_cast<size_t>(j)] < 0) {
+            newIdx[static_cast<size_t>(j)] = static_cast<int32_t>(order.size());
+            order.push_back(j);
+        }
+        const auto& k4 = kids[static_cast<size_t>(j)];
+        for (int k = 3; k >= 0; --k)
+            if (k4[static_cast<size_t>(k)] >= 0 && inner(k4[static_cast<size_t>(k)]))
+                dfs.push_back(node4Of[static_cast<size_t>(k4[static_cast<size_t>(k)])]);
+    }
+    out->resize(n4);
+    for (size_t k = 0; k < n4; ++k) {
+        const auto& k4 = kids[static_cast<size_t>(order[k])];
+        QNode4& q = (*out)[k];
+        for (int c = 0; c < 4; ++c) {
+            const int32_t b = k4[static_cast<size_t>(c)];
+            if (b < 0) {
+                q.q[3 * c] = q.q[3 * c + 1] = q.q[3 * c + 2] = 0u;
+                q.ref[c] = kEmptyChild;
+                continue;
+            }
+            const HBVHNode& bn = nodes[static_cast<size_t>(b)];
+            const float mn[3] = {bn.box.mn.x, bn.box.mn.y, bn.box.mn.z}, mx[3] = {bn.box.mx.x, bn.box.mx.y, bn.box.mx.z};
+            if (!qz.box(mn, mx, q.q + 3 * c)) {
+                out->clear();
+                return false;
+            }
+            q.ref[c] = bn.numPrimitives > 0 ? leafRef(bn.indexOffset, bn.numPrimitives)
+                                             : newIdx[static_cast<size_t>(node4Of[static_cast<size_t>(b)])];
+        }
+    }
+    root->ref = 0;
     return true;
 }
 

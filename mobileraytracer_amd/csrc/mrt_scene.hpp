@@ -149,6 +149,12 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
 // The walk tree's GNodes (numbered by toDeviceBVH) as QNodes on a grid over the root box; false
 // (nothing written) when a box or the grid is not finite.
 bool toQuantizedBVH(const std::vector<GNode>& nodes, const GRoot& root, QGrid* grid, std::vector<QNode>* out);
+// The walk tree collapsed to 4-wide nodes (each node's children: its BVH2 children, the inner one
+// of largest area replaced by its own children while fewer than four), quantized like
+// toQuantizedBVH and numbered as toDeviceBVH numbers (the first topCount breadth-first).  Fills
+// root (box of nodes[0], reference into out); false when a box or the grid is not finite.
+bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
+                     QGrid* grid, std::vector<QNode4>* out);
 // A tree over the same leaves (primitive ranges and boxes) as the reference tree `ref`, grouped
 // by a full-sweep SAH; its inner boxes are exact unions of the leaf boxes (reference numbering:
 // node 0 the root, an inner node's children at indexOffset and indexOffset + 1).

@@ -222,33 +222,72 @@ __device__ __forceinline__ bool qslab(float mnx, float mny, float mnz, float mxx
     return tMax >= e;
 }
 
-// One walk-tree visit (QNode: two 16-byte loads, or LDS for the top nodes).  Every box holds the
-// reference leaf boxes below it with the margin of toQuantizedBVH, so for the rays admitted to this
-// tree a node passes whenever a leaf below passes the reference test, and its entry is at most
-// that leaf's: the visit set is a superset of the reference's, and the leaves are tested exactly
-// before their triangles (traceWhileWhile).
+// compare-exchange of two (sort key, reference) pairs: ascending keys
+__device__ __forceinline__ void cex(float& ka, int& ra, float& kb, int& rb) {
+    const bool sw = kb < ka;
+    const float k = sw ? kb : ka;
+    const int r = sw ? rb : ra;
+    kb = sw ? ka : kb;
+    rb = sw ? ra : rb;
+    ka = k;
+    ra = r;
+}
+
+// One walk-tree visit (QNode4: four 16-byte loads, or LDS for the top nodes).  Every child box
+// holds the reference leaf boxes below it with the margin of toQuantizedBVH, so for the rays
+// admitted to this tree a child passes whenever a leaf below passes the reference test, and its
+// entry is at most that leaf's: the visit set is a superset of the reference's, and the leaves are
+// tested exactly before their triangles (traceWhileWhile).  The hit children are visited in order
+// of entry (order 0: nearest first; 1: farthest first): the first now, the others pushed.
 template <int kCull>
-__device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode* ldsTop, int top, int ref, v3 qa, v3 qb,
+__device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, int top, int ref, v3 qa, v3 qb,
                                           float lim, TStack& st, TravCount* cnt, bool count, int order) {
     constexpr bool cull = kCull != kCullNone;
-    int4 a, b;
+    int4 a, b, c, e;
     if (ref < top) {
         const int4* np = reinterpret_cast<const int4*>(ldsTop + ref);
         a = np[0];
         b = np[1];
+        c = np[2];
+        e = np[3];
     } else {
-        const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(QNode));
+        const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(QNode4));
         a = bload4i(qnodes, off);
         b = bload4i(qnodes, off + 16u);
+        c = bload4i(qnodes, off + 32u);
+        e = bload4i(qnodes, off + 48u);
     }
-    if (count) cnt->nodes += 2;
-    const uint32_t w0 = static_cast<uint32_t>(a.x), w1 = static_cast<uint32_t>(a.y), w2 = static_cast<uint32_t>(a.z),
-                   w3 = static_cast<uint32_t>(a.w), w4 = static_cast<uint32_t>(b.x), w5 = static_cast<uint32_t>(b.y);
-    float tl, tr;
-    const bool hl = qslab(qlo(w0), qhi(w0), qlo(w1), qhi(w1), qlo(w2), qhi(w2), qa, qb, &tl);
-    const bool hr = qslab(qlo(w3), qhi(w3), qlo(w4), qhi(w4), qlo(w5), qhi(w5), qa, qb, &tr);
-    const bool rightFirst = order == 0 ? tr < tl : !(tr < tl);
-    return chooseChildren(hl, hr, tl, tr, tl, tr, b.z, b.w, lim, cull, st, rightFirst);
+    const bool v0 = e.x != kEmptyChild, v1 = e.y != kEmptyChild, v2 = e.z != kEmptyChild, v3c = e.w != kEmptyChild;
+    if (count) cnt->nodes += static_cast<uint32_t>(v0) + v1 + v2 + v3c;
+    const auto u = [](int w) { return static_cast<uint32_t>(w); };
+    float t0, t1, t2, t3;
+    bool h0 = qslab(qlo(u(a.x)), qhi(u(a.x)), qlo(u(a.y)), qhi(u(a.y)), qlo(u(a.z)), qhi(u(a.z)), qa, qb, &t0) && v0;
+    bool h1 = qslab(qlo(u(a.w)), qhi(u(a.w)), qlo(u(b.x)), qhi(u(b.x)), qlo(u(b.y)), qhi(u(b.y)), qa, qb, &t1) && v1;
+    bool h2 = qslab(qlo(u(b.z)), qhi(u(b.z)), qlo(u(b.w)), qhi(u(b.w)), qlo(u(c.x)), qhi(u(c.x)), qa, qb, &t2) && v2;
+    bool h3 = qslab(qlo(u(c.y)), qhi(u(c.y)), qlo(u(c.z)), qhi(u(c.z)), qlo(u(c.w)), qhi(u(c.w)), qa, qb, &t3) && v3c;
+    if (cull) {
+        h0 = h0 && !(t0 > lim);
+        h1 = h1 && !(t1 > lim);
+        h2 = h2 && !(t2 > lim);
+        h3 = h3 && !(t3 > lim);
+    }
+    const int n = static_cast<int>(h0) + h1 + h2 + h3;
+    if (n == 0) return popCulled(st, lim, cull);
+    // sort keys: the entry (nearest first) or its negation (farthest first); misses last
+    constexpr float kInf = __builtin_inff();
+    const float sg = order == 0 ? 1.0F : -1.0F;
+    float k0 = h0 ? sg * t0 : kInf, k1 = h1 ? sg * t1 : kInf, k2 = h2 ? sg * t2 : kInf, k3 = h3 ? sg * t3 : kInf;
+    int r0 = e.x, r1 = e.y, r2 = e.z, r3 = e.w;
+    cex(k0, r0, k1, r1);
+    cex(k2, r2, k3, r3);
+    cex(k0, r0, k2, r2);
+    cex(k1, r1, k3, r3);
+    cex(k1, r1, k2, r2);
+    // push the others farthest-in-order first (the stack's key is the entry, for popCulled)
+    if (n > 3) st.push(r3, sg * k3);
+    if (n > 2) st.push(r2, sg * k2);
+    if (n > 1) st.push(r1, sg * k1);
+    return r0;
 }
 
 // A ray may walk the quantized tree when the bound of toQuantizedBVH holds for it: every 1/d
@@ -268,8 +307,8 @@ __device__ __forceinline__ bool quantOK(const DScene& s, v3 o, v3 inv) {
 
 // Copies the walk tree's top into LDS (all threads; ends with a barrier).
 template <int kThreads>
-__device__ __forceinline__ void stageTop(const DScene& s, QNode* ldsTop) {
-    const int n = min(kWalkTop, s.triTop) * static_cast<int>(sizeof(QNode) / sizeof(float4));
+__device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
+    const int n = min(kWalkTop, s.triTop) * static_cast<int>(sizeof(QNode4) / sizeof(float4));
     const float4* src = reinterpret_cast<const float4*>(s.triQNodes);
     float4* dst = reinterpret_cast<float4*>(ldsTop);
     for (int i = static_cast<int>(threadIdx.x); i < n; i += kThreads) dst[i] = src[i];
@@ -282,7 +321,7 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode* ldsTop) {
 template <bool kAny, bool kCount, int kCull>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                TStack& st, TravCount* cnt, const QNode* ldsTop, int* tailBest,
+                                                TStack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest,
                                                 const int* __restrict__ perm) {
     constexpr int kHelper = -2;  // rayIdx of a lane walking a subtree given by another lane
     const bool donate = s.tailDonate != 0;
