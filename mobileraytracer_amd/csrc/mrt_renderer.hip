@@ -137,6 +137,7 @@ struct mrt_renderer {
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
     int binMode = 0;                     // tuning key 4: binned emission of child / shadow rays (ShadeArgs::binMode)
     int shadowGridPct = 0;               // tuning key 6: shadow walk grid, percent of its occupancy grid (0 auto)
+    int refill = 0;                      // tuning key 9: walk refill threshold (0 auto: by paths per lane)
     int sortMode = 0;                    // tuning key 12: sort queues before their walk (1 shadow, 2 closest hit of levels >= 2)
     int sortKeyShadow = 0;               // tuning key 13: sort key of shadow queues (launchSort keyMode)
     int sortKeyRay = 1;                  // tuning key 14: sort key of closest-hit queues
@@ -596,6 +597,10 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // full grid is 2.6 % faster).  Results do not depend on the grid.
         const double pathsPerLane = static_cast<double>(ra.nPaths) / std::max(1, r->traceThreads);
         const int shadowPct = r->shadowGridPct > 0 ? r->shadowGridPct : pathsPerLane < 4.0 ? 60 : pathsPerLane < 8.0 ? 75 : 100;
+        // refill threshold: larger batches where a lane sees few paths (a small shard: the tail
+        // dominates; C4 shard at N = 8: 24 / 32 / 40 -> 2.68 / 2.64 / 2.61 ms), smaller where it
+        // sees many (N = 1: 13.77 / 13.86 / 13.88 ms)
+        r->ds.refill = r->refill > 0 ? r->refill : pathsPerLane < 4.0 ? 40 : 24;
         size_t sync = 0;
         hipEvent_t shadowDone[kMaxLevels] = {};
         if (sb != st) {
@@ -1090,8 +1095,8 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.leanShade = value;
         return 0;
     }
-    if (key == 9 && value >= 1 && value <= 64) {
-        r->ds.refill = value;
+    if (key == 9 && value >= 0 && value <= 64) {
+        r->refill = value;
         return 0;
     }
     if (key == 8 && (value == 0 || value == 1)) {
@@ -1236,7 +1241,7 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 5: *value = r->ds.anyOrder; return 0;
         case 6: *value = r->shadowGridPct; return 0;
         case 8: *value = r->ds.tailDonate; return 0;
-        case 9: *value = r->ds.refill; return 0;
+        case 9: *value = r->refill; return 0;
         case 10: *value = r->ds.leanShade; return 0;
         case 11: *value = r->shadeGridPerCU; return 0;
         case 12: *value = r->sortMode; return 0;

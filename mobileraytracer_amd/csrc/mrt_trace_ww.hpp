@@ -27,7 +27,7 @@
 namespace mrt {
 
 constexpr int kRefDone = 0x7FFFFFFF;  // sentinel: no node (never a valid inner index)
-constexpr int kWalkRefill = 32;       // idle lanes before a wave fetches new rays (DScene::refill default)
+constexpr int kWalkRefill = 32;       // idle lanes before a wave fetches new rays (DScene::refill at upload; frames set it by paths per lane)
 constexpr int kWalkShards = 8;        // work cursors per level (one per XCD group of workgroups)
 constexpr int kWalkStack = kLdsStackMin;  // LDS stack entries per thread (deeper ones spill)
 constexpr int kWalkTop = kTopNodesMax;
