@@ -183,6 +183,23 @@ class Renderer:
         self.close()
 
 
+def walk_tree(config: Config):
+    """Host-side quantized 4-wide walk tree of the configured scene (no GPU): nodes (N, 16) uint32
+    (12 box words, 4 child references), grid (6,) float32 (origin xyz, step xyz), root (2,) int32
+    (reference, triangle count) - DESIGN.md section 3.1."""
+    lib = _native.lib()
+    c = config.to_c()
+    n = lib.mrt_walk_tree(ctypes.byref(c), None, None, None)
+    if n < 0:
+        raise RuntimeError(lib.mrt_last_error().decode())
+    nodes = np.empty((n, 16), np.uint32)
+    grid = np.empty(6, np.float32)
+    root = np.empty(2, np.int32)
+    if lib.mrt_walk_tree(ctypes.byref(c), _ptr(nodes), _ptr(grid), _ptr(root)) != n:
+        raise RuntimeError(lib.mrt_last_error().decode())
+    return nodes, grid, root
+
+
 def triangle_bvh(config: Config):
     """Host-side triangle BVH of the configured scene (no GPU): boxes (N, 6), offsets, counts,
     order - the layout of the reference's BVHNode array (BVH.hpp:56-60)."""

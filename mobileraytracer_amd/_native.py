@@ -17,7 +17,7 @@ EXPORTED_SYMBOLS = (
     "mrt_last_error", "mrt_create", "mrt_destroy", "mrt_render_frame", "mrt_render_frame_device",
     "mrt_unpack_gathered", "mrt_stop_render", "mrt_get_sample", "mrt_get_total_casted_rays",
     "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits", "mrt_set_tuning",
-    "mrt_get_tuning", "mrt_triangle_bvh", "mrt_decode_texture", "mrt_kat_slab", "mrt_kat_triangle",
+    "mrt_get_tuning", "mrt_triangle_bvh", "mrt_walk_tree", "mrt_decode_texture", "mrt_kat_slab", "mrt_kat_triangle",
     "mrt_trace_rays", "mrt_sample_tables", "mrt_regular_grid", "mrt_grid_box_test", "mrt_create_from_memory",
     "mrt_preview_arrays", "mrt_wave_log",
     "mrt_android_read_file", "mrt_android_initialize", "mrt_android_render_into_bitmap", "mrt_android_start_render",
@@ -112,6 +112,7 @@ def load_library(path=LIB_PATH):
         "mrt_set_tuning": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32]),
         "mrt_get_tuning": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
         "mrt_triangle_bvh": (ctypes.c_int64, [vp, vp, vp, vp, vp]),
+        "mrt_walk_tree": (ctypes.c_int64, [vp, vp, vp, vp]),
         "mrt_decode_texture": (ctypes.c_int64, [ctypes.c_char_p, vp, vp]),
         "mrt_regular_grid": (ctypes.c_int64, [vp, ctypes.c_int32, vp, vp, vp]),
         "mrt_grid_box_test": (ctypes.c_int, [ctypes.c_int32, vp, vp]),

@@ -1152,6 +1152,44 @@ int64_t mrt_triangle_bvh(const mrt_config* cfg, float* boxes, int32_t* offsets, 
     return rc == 0 ? n : -1;
 }
 
+int64_t mrt_walk_tree(const mrt_config* cfg, uint32_t* nodes, float* grid, int32_t* root) {
+    using namespace mrt;
+    int64_t n = -1;
+    const int rc = guarded([&] {
+        HScene sc;
+        if (cfg->sceneIndex >= 0 && cfg->sceneIndex <= 3) {
+            sc = builtinScene(cfg->sceneIndex);
+        } else {
+            std::string err;
+            if (!loadObjScene(cfg->objFilePath ? cfg->objFilePath : "", cfg->mtlFilePath ? cfg->mtlFilePath : "", &sc,
+                              &err))
+                throw std::runtime_error(err);
+        }
+        std::vector<int32_t> perm;
+        const std::vector<HBVHNode> tn = buildBVH(&sc.triangles, &perm);
+        const char* walkTree = std::getenv("MOBILERT_WALK_TREE");
+        const bool regroup = walkTree == nullptr || std::atoi(walkTree) != 0;
+        const std::vector<HBVHNode> wn = regroup ? rebuildOverLeaves(tn, 2) : tn;
+        GRoot r{};
+        QGrid g{};
+        std::vector<QNode4> qn;
+        int top = 0;
+        if (!toQuantizedBVH4(wn, sc.triangles.size(), &r, kTopNodesMax, &top, &g, &qn))
+            throw std::runtime_error("walk tree not quantizable (non-finite boxes)");
+        n = static_cast<int64_t>(qn.size());
+        if (nodes != nullptr) std::memcpy(nodes, qn.data(), qn.size() * sizeof(QNode4));
+        if (grid != nullptr) {
+            std::memcpy(grid, g.origin, sizeof(g.origin));
+            std::memcpy(grid + 3, g.step, sizeof(g.step));
+        }
+        if (root != nullptr) {
+            root[0] = r.ref;
+            root[1] = r.count;
+        }
+    });
+    return rc == 0 ? n : -1;
+}
+
 int mrt_grid_box_test(int32_t kind, const float* prim, const float* box) {
     using namespace mrt;
     const HAABB b{v3{box[0], box[1], box[2]}, v3{box[3], box[4], box[5]}};

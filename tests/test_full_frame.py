@@ -204,3 +204,78 @@ def test_walk_tree_is_invariant():
         finally:
             del os.environ["MOBILERT_WALK_TREE"]
     assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1:] == outs[1][1:]
+
+
+def test_quantized_walk_tree_boundary_rays(oracle_mod):
+    """The walk tree's boxes are 16-bit grid coordinates rounded outward by one step, under an
+    error bound that holds for 1/d components in [2^-40, 2^90] and origins within 4 grid extents
+    (DESIGN.md section 3.1); walk-tree leaves are tested exactly.  Rays built to sit on that
+    argument's edges - aimed at leaf-box corners, edges and faces (tangent to exact leaf boxes),
+    starting on leaf-box faces, with direction components of 1e-27 / 1e-29 (1/d just inside /
+    outside 2^90), from 3.9 and 4.1 grid extents away - give the reference walk's closest hits and
+    shadow tests in every cull mode, and a sample equals the oracle."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, shader=1, scene="conference")
+    boxes, off, cnt, _ = m.triangle_bvh(cfg)
+    lo, hi = boxes[0, :3].astype(np.float64), boxes[0, 3:].astype(np.float64)
+    ext = hi - lo
+    leaf = boxes[cnt > 0].astype(np.float64)
+    rng = np.random.default_rng(11)
+    parts = []
+    n = 200_000
+    # aimed at a corner / an edge point / a face point of a random leaf box
+    o, _ = random_rays(3 * n, 12, lo, hi)
+    o = o.astype(np.float64)
+    b = leaf[rng.integers(0, len(leaf), 3 * n)]
+    t = b[:, :3] + rng.random((3 * n, 3)) * (b[:, 3:] - b[:, :3])
+    corner = np.where(rng.random((3 * n, 3)) < 0.5, b[:, :3], b[:, 3:])
+    t[:n] = corner[:n]                                   # corners
+    ax = rng.integers(0, 3, (3 * n, 2))
+    idx = np.arange(3 * n)
+    t[n:2 * n, :][np.arange(n), ax[n:2 * n, 0]] = corner[n:2 * n][np.arange(n), ax[n:2 * n, 0]]
+    t[n:2 * n, :][np.arange(n), ax[n:2 * n, 1]] = corner[n:2 * n][np.arange(n), ax[n:2 * n, 1]]  # edges
+    t[2 * n:, :][np.arange(n), ax[2 * n:, 0]] = corner[2 * n:][np.arange(n), ax[2 * n:, 0]]      # faces
+    parts.append((o, t - o))
+    # starting on a leaf-box face, random directions
+    o2 = leaf[rng.integers(0, len(leaf), n)]
+    p = o2[:, :3] + rng.random((n, 3)) * (o2[:, 3:] - o2[:, :3])
+    a = rng.integers(0, 3, n)
+    p[np.arange(n), a] = np.where(rng.random(n) < 0.5, o2[np.arange(n), a], o2[np.arange(n), 3 + a])
+    parts.append((p, rng.normal(size=(n, 3))))
+    # tiny direction components around the 2^90 bound on 1/d, and far origins around 4 extents
+    k = 20_000
+    o3, d3 = random_rays(k, 13, lo, hi)
+    d3 = d3.astype(np.float64)
+    d3[: k // 2, rng.integers(0, 3)] = rng.choice([1e-27, -1e-27])
+    d3[k // 2:, rng.integers(0, 3)] = rng.choice([1e-29, -1e-29])
+    parts.append((o3.astype(np.float64), d3))
+    c = (lo + hi) / 2
+    for f in (3.9, 4.1):
+        dirn = rng.normal(size=(k, 3))
+        dirn /= np.linalg.norm(dirn, axis=1, keepdims=True)
+        far = c - dirn * (f * ext.max() + np.linalg.norm(ext))
+        tgt = lo + rng.random((k, 3)) * ext
+        parts.append((far, tgt - far))
+    o = np.concatenate([q[0] for q in parts]).astype(np.float32)
+    d = np.concatenate([q[1] for q in parts])
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    dist = (rng.random(len(o)) * np.linalg.norm(ext) * 2).astype(np.float32)
+    res = {}
+    with m.Renderer(cfg) as r:
+        for walk, cull in ((0, 0), (1, 0), (1, 1), (1, 2)):
+            r.set_tuning(1, walk)
+            r.set_tuning(2, cull)
+            res[(walk, cull)] = (r.trace_rays(o, d), r.trace_rays(o, d, dist=dist, any_hit=True)[0])
+    ref_hits, ref_occ = res[(0, 0)]
+    assert (ref_hits[0] == 3).mean() > 0.3
+    for key, (hits, occ) in res.items():
+        assert all(np.array_equal(x, y) for x, y in zip(hits, ref_hits)), key
+        assert np.array_equal(occ, ref_occ), key
+    o_ = oracle_for(oracle_mod, cfg)
+    sel = np.concatenate([np.arange(0, 4 * n, 100), np.arange(4 * n, len(o), 10)])
+    ok, oi, ot = o_.trace_rays(o[sel], d[sel])
+    occ = o_.trace_rays(o[sel], d[sel], dist=dist[sel], any_hit=True)[0]
+    o_.close()
+    assert np.array_equal(ok, ref_hits[0][sel]) and np.array_equal(oi, ref_hits[1][sel])
+    assert np.array_equal(ot.view(np.int32), ref_hits[2][sel].view(np.int32))
+    assert np.array_equal(occ, ref_occ[sel])

@@ -1,0 +1,71 @@
+"""CPU: the quantized 4-wide walk tree by construction.  The GPU walk is
+exact because (1) its leaves are exactly the reference BVH's leaves (BVH.hpp:161-283), each once,
+and (2) every child box holds the exact box of every reference leaf below it with a margin of at
+least one grid step on every side - the margin that covers the rounding of the kernel's
+fma(q, step/d, (origin - o)/d) and of the reference's (b - o) * inv.  Both are checked here on the
+host build the renderer uploads (mrt_walk_tree), in float64."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import make_cfg
+
+EMPTY = 0x7FFFFFFE
+
+
+def _leaf_key(ref):
+    v = -ref - 1
+    return v >> 3, v & 7
+
+
+@pytest.mark.parametrize("case", [dict(scene="conference"), dict(scene="water"), dict(scene="teapot"),
+                                  dict(sceneIndex=2), dict(sceneIndex=3)])
+def test_walk_tree_holds_reference_leaves_with_margin(case):
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, **case)
+    boxes, off, cnt, _ = m.triangle_bvh(cfg)
+    leaves = {(int(off[i]), int(cnt[i])): boxes[i].astype(np.float64) for i in range(len(cnt)) if cnt[i] > 0}
+    nodes, grid, root = m.walk_tree(cfg)
+    refs = nodes[:, 12:].view(np.int32)
+    org, step = grid[:3].astype(np.float64), grid[3:].astype(np.float64)
+    if not leaves:  # no triangles: nothing to walk
+        assert int(root[1]) == 0
+        return
+    assert np.all(step > 0) and int(root[1]) == sum(c for _, c in leaves)
+    if int(root[0]) < 0:  # the root is a leaf: no inner node
+        assert _leaf_key(int(root[0])) in leaves
+        return
+    seen = []
+    union = {}  # node -> exact union box of the reference leaves below (float64)
+
+    def child_box(ref):
+        if ref < 0:
+            key = _leaf_key(ref)
+            seen.append(key)
+            return leaves[key]
+        return union[ref]
+
+    # post-order over the 4-wide nodes
+    order, stack = [], [int(root[0])]
+    while stack:
+        i = stack.pop()
+        order.append(i)
+        stack.extend(int(r) for r in refs[i] if 0 <= int(r) != EMPTY)
+    for i in reversed(order):
+        w = nodes[i, :12].astype(np.int64)
+        u = None
+        for c in range(4):
+            ref = int(refs[i, c])
+            if ref == EMPTY:
+                continue
+            exact = child_box(ref)
+            q = np.array([w[3 * c] & 0xFFFF, w[3 * c] >> 16, w[3 * c + 1] & 0xFFFF,
+                          w[3 * c + 1] >> 16, w[3 * c + 2] & 0xFFFF, w[3 * c + 2] >> 16], np.float64)
+            qmin, qmax = org + q[:3] * step, org + q[3:] * step
+            assert np.all(qmin <= exact[:3] - step), (i, c)
+            assert np.all(qmax >= exact[3:] + step), (i, c)
+            u = exact.copy() if u is None else np.concatenate([np.minimum(u[:3], exact[:3]), np.maximum(u[3:], exact[3:])])
+        union[i] = u
+    # every reference leaf exactly once, nothing else
+    assert sorted(seen) == sorted(leaves.keys())
+    # the root's union is the reference root box
+    assert np.array_equal(union[int(root[0])].astype(np.float32), boxes[0])
