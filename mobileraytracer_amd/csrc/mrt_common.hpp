@@ -168,19 +168,11 @@ struct alignas(16) GNode {
 };
 static_assert(sizeof(GNode) == 64, "GNode must be 64 bytes");
 
-// Walk-tree node ("quantized walk tree"): both children's boxes as 16-bit
-// coordinates on one scene-wide grid (real value origin + q * step per axis), rounded OUTWARD by
-// one extra grid step, and the child references: 32 bytes, two 16-byte loads per visit instead
-// of four.  q[0] = Lminx | Lminy << 16, q[1] = Lminz | Lmaxx << 16, q[2] = Lmaxy | Lmaxz << 16,
-// q[3..5] the same for the right child.
-struct alignas(16) QNode {
-    uint32_t q[6];
-    int32_t refL, refR;
-};
-static_assert(sizeof(QNode) == 32, "QNode must be 32 bytes");
-// 4-wide walk-tree node: the same 16-bit boxes for up to four children (q[3c .. 3c+2] = child c's
-// minx | miny << 16, minz | maxx << 16, maxy | maxz << 16) and their references (kEmptyChild:
-// no child): 64 bytes, four 16-byte loads per visit, about half the dependent visits of BVH2.
+// Walk-tree node ("quantized walk tree"): up to four children, each
+// child's box as 16-bit coordinates on one scene-wide grid (real value origin + q * step per axis)
+// rounded OUTWARD by one extra grid step (q[3c .. 3c+2] = child c's minx | miny << 16,
+// minz | maxx << 16, maxy | maxz << 16), and their references (kEmptyChild: no child): 64 bytes,
+// four 16-byte loads per visit, about half the dependent visits of a BVH2.
 constexpr int32_t kEmptyChild = 0x7FFFFFFE;
 struct alignas(16) QNode4 {
     uint32_t q[12];

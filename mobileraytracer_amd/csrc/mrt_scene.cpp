@@ -972,7 +972,7 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
 // grid step (S / 65535 > S 2^-19) on each side therefore keeps every computed slab interval of a
 // node around the computed interval of every reference leaf box below it.
 namespace {
-// the grid of toQuantizedBVH over a root box, and the outward rounding of one coordinate
+// the walk tree's grid over a root box, and the outward rounding of one coordinate
 struct Quantizer {
     double step[3] = {}, org[3] = {};
     bool init(const float* bmin, const float* bmax, QGrid* grid) {
@@ -1018,26 +1018,6 @@ struct Quantizer {
     }
 };
 }  // namespace
-
-bool toQuantizedBVH(const std::vector<GNode>& nodes, const GRoot& root, QGrid* grid, std::vector<QNode>* out) {
-    out->clear();
-    Quantizer qz;
-    if (!qz.init(root.bmin, root.bmax, grid)) return false;
-    out->resize(nodes.size());
-    for (size_t k = 0; k < nodes.size(); ++k) {
-        const GNode& g = nodes[k];
-        const float lmn[3] = {g.lminx, g.lminy, g.lminz}, lmx[3] = {g.lmaxx, g.lmaxy, g.lmaxz};
-        const float rmn[3] = {g.rminx, g.rminy, g.rminz}, rmx[3] = {g.rmaxx, g.rmaxy, g.rmaxz};
-        QNode& n = (*out)[k];
-        if (!qz.box(lmn, lmx, n.q) || !qz.box(rmn, rmx, n.q + 3)) {
-            out->clear();
-            return false;
-        }
-        n.refL = g.refL;
-        n.refR = g.refR;
-    }
-    return true;
-}
 
 bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
                      QGrid* grid, std::vector<QNode4>* out) {

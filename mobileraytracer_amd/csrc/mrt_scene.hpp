@@ -146,12 +146,9 @@ std::vector<HBVHNode> buildBVH(std::vector<T>* prims, std::vector<int32_t>* orde
 // cones: the cull word of every reference node (triangleConeWords), or null (never culled).
 void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vector<GNode>* out, GRoot* root,
                  int topCount = 0, int* topPlaced = nullptr, const std::vector<uint32_t>* cones = nullptr);
-// The walk tree's GNodes (numbered by toDeviceBVH) as QNodes on a grid over the root box; false
-// (nothing written) when a box or the grid is not finite.
-bool toQuantizedBVH(const std::vector<GNode>& nodes, const GRoot& root, QGrid* grid, std::vector<QNode>* out);
 // The walk tree collapsed to 4-wide nodes (each node's children: its BVH2 children, the inner one
 // of largest area replaced by its own children while fewer than four), quantized like
-// toQuantizedBVH and numbered as toDeviceBVH numbers (the first topCount breadth-first).  Fills
+// Quantizer (mrt_scene.cpp) and numbered as toDeviceBVH numbers (the first topCount breadth-first).  Fills
 // root (box of nodes[0], reference into out); false when a box or the grid is not finite.
 bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
                      QGrid* grid, std::vector<QNode4>* out);

@@ -208,7 +208,7 @@ __device__ __forceinline__ int innerStep(BufRes nodes, int ref, v3 o, v3 d, v3 i
 }
 
 // The quantized walk tree's planes: t = fma(q, qa, qb) with qa = step / d, qb = (origin - o) / d
-// per axis (rounded as toQuantizedBVH's bound assumes); the slab logic of slabFinite.
+// per axis (rounded as the Quantizer's bound in mrt_scene.cpp assumes); the slab logic of slabFinite.
 __device__ __forceinline__ float qlo(uint32_t w) { return static_cast<float>(w & 0xFFFFu); }
 __device__ __forceinline__ float qhi(uint32_t w) { return static_cast<float>(w >> 16); }
 __device__ __forceinline__ bool qslab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, v3 qa, v3 qb,
@@ -234,7 +234,7 @@ __device__ __forceinline__ void cex(float& ka, int& ra, float& kb, int& rb) {
 }
 
 // One walk-tree visit (QNode4: four 16-byte loads, or LDS for the top nodes).  Every child box
-// holds the reference leaf boxes below it with the margin of toQuantizedBVH, so for the rays
+// holds the reference leaf boxes below it with the Quantizer's margin (mrt_scene.cpp), so for the rays
 // admitted to this tree a child passes whenever a leaf below passes the reference test, and its
 // entry is at most that leaf's: the visit set is a superset of the reference's, and the leaves are
 // tested exactly before their triangles (traceWhileWhile).  The hit children are visited in order
@@ -290,7 +290,7 @@ __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, i
     return r0;
 }
 
-// A ray may walk the quantized tree when the bound of toQuantizedBVH holds for it: every 1/d
+// A ray may walk the quantized tree when the Quantizer's bound (mrt_scene.cpp) holds for it: every 1/d
 // component in [2^-40, 2^90] and the origin within 4 grid extents of the grid origin per axis.
 __device__ __forceinline__ bool quantOK(const DScene& s, v3 o, v3 inv) {
     if (s.qEnabled == 0) return false;
