@@ -174,9 +174,10 @@ int mrt_primary_hits(mrt_renderer *r, int32_t *kind, int32_t *index, float *t);
  * (min xyz, max xyz), offsets[N] / counts[N] (BVHNode::indexOffset / numPrimitives) and
  * order[triangles] (input index of each triangle in BVH order). */
 int64_t mrt_triangle_bvh(const mrt_config *cfg, float *boxes, int32_t *offsets, int32_t *counts, int32_t *order);
-/* Host only: the quantized 4-wide walk tree the BVH walk traverses:
- * returns the node count or -1; with non-NULL outputs fills nodes (count x 16 uint32: 12 box
- * words, 4 child references), grid[6] (origin xyz, step xyz) and root[2] (reference, triangles). */
+/* Host only: the quantized wide walk tree the BVH walk traverses:
+ * returns the node count or -1; with non-NULL outputs fills nodes (count x 4W uint32: 3W box
+ * words, W child references; W = the walk width, root[2]), grid[6] (origin xyz, step xyz) and
+ * root[3] (reference, triangles, W). */
 int64_t mrt_walk_tree(const mrt_config *cfg, uint32_t *nodes, float *grid, int32_t *root);
 /* Host only: the RegularGrid accelerator's build (RegularGrid.hpp:112-289, gridSize 32) for one
  * primitive kind of the scene cfg names (kind 0 planes, 1 spheres, 2 triangles).  Returns the

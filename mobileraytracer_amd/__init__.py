@@ -184,17 +184,19 @@ class Renderer:
 
 
 def walk_tree(config: Config):
-    """Host-side quantized 4-wide walk tree of the configured scene (no GPU): nodes (N, 16) uint32
-    (12 box words, 4 child references), grid (6,) float32 (origin xyz, step xyz), root (2,) int32
-    (reference, triangle count) - DESIGN.md section 3.1."""
+    """Host-side quantized wide walk tree of the configured scene (no GPU): nodes (N, 4W) uint32
+    (3W box words, W child references), grid (6,) float32 (origin xyz, step xyz), root (3,) int32
+    (reference, triangle count, width W) - DESIGN.md section 3.1."""
     lib = _native.lib()
     c = config.to_c()
     n = lib.mrt_walk_tree(ctypes.byref(c), None, None, None)
     if n < 0:
         raise RuntimeError(lib.mrt_last_error().decode())
-    nodes = np.empty((n, 16), np.uint32)
+    # the width first (a node is 4 * width words), then the nodes
     grid = np.empty(6, np.float32)
-    root = np.empty(2, np.int32)
+    root = np.empty(3, np.int32)
+    lib.mrt_walk_tree(ctypes.byref(c), None, _ptr(grid), _ptr(root))
+    nodes = np.empty((n, 4 * int(root[2])), np.uint32)
     if lib.mrt_walk_tree(ctypes.byref(c), _ptr(nodes), _ptr(grid), _ptr(root)) != n:
         raise RuntimeError(lib.mrt_last_error().decode())
     return nodes, grid, root

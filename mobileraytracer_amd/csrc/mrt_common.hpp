@@ -174,11 +174,16 @@ static_assert(sizeof(GNode) == 64, "GNode must be 64 bytes");
 // minz | maxx << 16, maxy | maxz << 16), and their references (kEmptyChild: no child): 64 bytes,
 // four 16-byte loads per visit, about half the dependent visits of a BVH2.
 constexpr int32_t kEmptyChild = 0x7FFFFFFE;
+#ifndef MRT_WALK_WIDTH
+#define MRT_WALK_WIDTH 4
+#endif
+constexpr int kWalkWidth = MRT_WALK_WIDTH;  // children per walk-tree node (4 or 8)
+static_assert(kWalkWidth == 4 || kWalkWidth == 8, "walk width");
 struct alignas(16) QNode4 {
-    uint32_t q[12];
-    int32_t ref[4];
+    uint32_t q[3 * kWalkWidth];
+    int32_t ref[kWalkWidth];
 };
-static_assert(sizeof(QNode4) == 64, "QNode4 must be 64 bytes");
+static_assert(sizeof(QNode4) == 16 * kWalkWidth, "QNode4: 16 bytes per child");
 struct QGrid {
     float origin[3];
     float step[3];

@@ -16,7 +16,7 @@ constexpr int kDefaultTraceVariant = 1;
 constexpr int kAccNaive = 1;  // Shader::Accelerator (Shader.hpp:20-24)
 constexpr int kAccGrid = 2;
 constexpr int kAccBVH = 3;
-constexpr int kTopNodesMax = 64;         // walk-tree nodes numbered breadth-first (staged in LDS by the walk)
+constexpr int kTopNodesMax = 64 * 4 / kWalkWidth;  // walk-tree nodes numbered breadth-first (4 KB staged in LDS by the walk)
 
 // Device counters (ints).  Pair l = {rays of level l+1, shadow rays of level l} sits on two
 // adjacent ints so k_shade allocates both with one 64-bit atomic per block.

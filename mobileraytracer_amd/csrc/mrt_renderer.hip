@@ -267,7 +267,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.qEnabled = toQuantizedBVH4(wn, sc.triangles.size(), &d.triRoot, kTopNodesMax, &d.triTop, &d.qgrid, &qn) ? 1 : 0;
     if (d.qEnabled == 0 || qn.empty()) qn.resize(1);  // (a leaf or empty root: no inner node)
     d.triQNodes = r->sceneMem.upload(qn, st);
-    // a 4-wide visit pushes up to three entries: the walk's stack holds 3 per level
+    // a visit pushes up to kWalkWidth - 1 entries: the walk's stack holds that many per level
     {
         int depth4 = 0;
         std::vector<std::pair<int32_t, int>> w;
@@ -279,7 +279,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
             for (int32_t c : qn[static_cast<size_t>(i)].ref)
                 if (c >= 0 && c != kEmptyChild) w.push_back({c, dep + 1});
         }
-        r->stackNeed = std::max(r->stackNeed, 3 * depth4 + 2);
+        r->stackNeed = std::max(r->stackNeed, (kWalkWidth - 1) * depth4 + 2);
     }
     toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRootRef, 0, nullptr, &conesRef);
     {
@@ -1185,6 +1185,7 @@ int64_t mrt_walk_tree(const mrt_config* cfg, uint32_t* nodes, float* grid, int32
         if (root != nullptr) {
             root[0] = r.ref;
             root[1] = r.count;
+            root[2] = kWalkWidth;
         }
     });
     return rc == 0 ? n : -1;

@@ -1047,17 +1047,18 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
         return dx * dy + dy * dz + dz * dx;
     };
     // collapse: the 4-wide node of BVH2 node i has up to four BVH2 descendants as children
-    std::vector<std::array<int32_t, 4>> kids;  // per 4-wide node: BVH2 indices (-1: none)
+    std::vector<std::array<int32_t, kWalkWidth>> kids;  // per walk node: BVH2 indices (-1: none)
     std::vector<int32_t> node4Of(nodes.size(), -1);
     std::vector<int32_t> work{0};
     node4Of[0] = 0;
-    kids.push_back({-1, -1, -1, -1});
+    kids.emplace_back();
+    kids.back().fill(-1);
     while (!work.empty()) {
         const int32_t i = work.back();
         work.pop_back();
         const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
         std::vector<int32_t> c{l, l + 1};
-        while (c.size() < 4) {
+        while (c.size() < static_cast<size_t>(kWalkWidth)) {
             int best = -1;
             double ba = -1.0;
             for (size_t k = 0; k < c.size(); ++k)
@@ -1070,12 +1071,14 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
             c[static_cast<size_t>(best)] = cl;
             c.insert(c.begin() + best + 1, cl + 1);
         }
-        std::array<int32_t, 4> k4{-1, -1, -1, -1};
+        std::array<int32_t, kWalkWidth> k4;
+        k4.fill(-1);
         for (size_t k = 0; k < c.size(); ++k) {
             k4[k] = c[k];
             if (inner(c[k])) {
                 node4Of[static_cast<size_t>(c[k])] = static_cast<int32_t>(kids.size());
-                kids.push_back({-1, -1, -1, -1});
+                kids.emplace_back();
+                kids.back().fill(-1);
                 work.push_back(c[k]);
             }
         }
@@ -1103,7 +1106,7 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
             order.push_back(j);
         }
         const auto& k4 = kids[static_cast<size_t>(j)];
-        for (int k = 3; k >= 0; --k)
+        for (int k = kWalkWidth - 1; k >= 0; --k)
             if (k4[static_cast<size_t>(k)] >= 0 && inner(k4[static_cast<size_t>(k)]))
                 dfs.push_back(node4Of[static_cast<size_t>(k4[static_cast<size_t>(k)])]);
     }
@@ -1111,7 +1114,7 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
     for (size_t k = 0; k < n4; ++k) {
         const auto& k4 = kids[static_cast<size_t>(order[k])];
         QNode4& q = (*out)[k];
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < kWalkWidth; ++c) {
             const int32_t b = k4[static_cast<size_t>(c)];
             if (b < 0) {
                 q.q[3 * c] = q.q[3 * c + 1] = q.q[3 * c + 2] = 0u;

@@ -233,61 +233,74 @@ __device__ __forceinline__ void cex(float& ka, int& ra, float& kb, int& rb) {
     ra = r;
 }
 
-// One walk-tree visit (QNode4: four 16-byte loads, or LDS for the top nodes).  Every child box
-// holds the reference leaf boxes below it with the Quantizer's margin (mrt_scene.cpp), so for the rays
-// admitted to this tree a child passes whenever a leaf below passes the reference test, and its
-// entry is at most that leaf's: the visit set is a superset of the reference's, and the leaves are
-// tested exactly before their triangles (traceWhileWhile).  The hit children are visited in order
-// of entry (order 0: nearest first; 1: farthest first): the first now, the others pushed.
+// ascending sort of kWalkWidth (key, reference) pairs: Batcher's odd-even merge networks
+template <int W>
+__device__ __forceinline__ void sortChildren(float* k, int* r) {
+    if (W == 4) {
+        cex(k[0], r[0], k[1], r[1]);
+        cex(k[2], r[2], k[3], r[3]);
+        cex(k[0], r[0], k[2], r[2]);
+        cex(k[1], r[1], k[3], r[3]);
+        cex(k[1], r[1], k[2], r[2]);
+    } else {
+        constexpr int net[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {1, 2}, {5, 6},
+                                    {0, 4}, {1, 5}, {2, 6}, {3, 7}, {2, 4}, {3, 5}, {1, 2}, {3, 4}, {5, 6}};
+#pragma unroll
+        for (int c = 0; c < 19; ++c) cex(k[net[c][0]], r[net[c][0]], k[net[c][1]], r[net[c][1]]);
+    }
+}
+
+// One walk-tree visit (QNode4: kWalkWidth 16-byte loads, or LDS for the top nodes).  Every child
+// box holds the reference leaf boxes below it with the Quantizer's margin (mrt_scene.cpp), so for
+// the rays admitted to this tree a child passes whenever a leaf below passes the reference test,
+// and its entry is at most that leaf's: the visit set is a superset of the reference's, and the
+// leaves are tested exactly before their triangles (traceWhileWhile).  The hit children are
+// visited in order of entry (order 0: nearest first; 1: farthest first): the first now, the
+// others pushed.
 template <int kCull>
 __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, int top, int ref, v3 qa, v3 qb,
                                           float lim, TStack& st, TravCount* cnt, bool count, int order) {
+    constexpr int W = kWalkWidth;
     constexpr bool cull = kCull != kCullNone;
-    int4 a, b, c, e;
+    int4 raw[W];
     if (ref < top) {
         const int4* np = reinterpret_cast<const int4*>(ldsTop + ref);
-        a = np[0];
-        b = np[1];
-        c = np[2];
-        e = np[3];
+#pragma unroll
+        for (int j = 0; j < W; ++j) raw[j] = np[j];
     } else {
         const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(QNode4));
-        a = bload4i(qnodes, off);
-        b = bload4i(qnodes, off + 16u);
-        c = bload4i(qnodes, off + 32u);
-        e = bload4i(qnodes, off + 48u);
+#pragma unroll
+        for (int j = 0; j < W; ++j) raw[j] = bload4i(qnodes, off + 16u * static_cast<uint32_t>(j));
     }
-    const bool v0 = e.x != kEmptyChild, v1 = e.y != kEmptyChild, v2 = e.z != kEmptyChild, v3c = e.w != kEmptyChild;
-    if (count) cnt->nodes += static_cast<uint32_t>(v0) + v1 + v2 + v3c;
-    const auto u = [](int w) { return static_cast<uint32_t>(w); };
-    float t0, t1, t2, t3;
-    bool h0 = qslab(qlo(u(a.x)), qhi(u(a.x)), qlo(u(a.y)), qhi(u(a.y)), qlo(u(a.z)), qhi(u(a.z)), qa, qb, &t0) && v0;
-    bool h1 = qslab(qlo(u(a.w)), qhi(u(a.w)), qlo(u(b.x)), qhi(u(b.x)), qlo(u(b.y)), qhi(u(b.y)), qa, qb, &t1) && v1;
-    bool h2 = qslab(qlo(u(b.z)), qhi(u(b.z)), qlo(u(b.w)), qhi(u(b.w)), qlo(u(c.x)), qhi(u(c.x)), qa, qb, &t2) && v2;
-    bool h3 = qslab(qlo(u(c.y)), qhi(u(c.y)), qlo(u(c.z)), qhi(u(c.z)), qlo(u(c.w)), qhi(u(c.w)), qa, qb, &t3) && v3c;
-    if (cull) {
-        h0 = h0 && !(t0 > lim);
-        h1 = h1 && !(t1 > lim);
-        h2 = h2 && !(t2 > lim);
-        h3 = h3 && !(t3 > lim);
-    }
-    const int n = static_cast<int>(h0) + h1 + h2 + h3;
-    if (n == 0) return popCulled(st, lim, cull);
-    // sort keys: the entry (nearest first) or its negation (farthest first); misses last
+    const auto word = [&](int i) -> uint32_t {  // word i of the node (i a compile-time constant after unrolling)
+        const int4 v = raw[i >> 2];
+        const int c = i & 3;
+        return static_cast<uint32_t>(c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w);
+    };
     constexpr float kInf = __builtin_inff();
-    const float sg = order == 0 ? 1.0F : -1.0F;
-    float k0 = h0 ? sg * t0 : kInf, k1 = h1 ? sg * t1 : kInf, k2 = h2 ? sg * t2 : kInf, k3 = h3 ? sg * t3 : kInf;
-    int r0 = e.x, r1 = e.y, r2 = e.z, r3 = e.w;
-    cex(k0, r0, k1, r1);
-    cex(k2, r2, k3, r3);
-    cex(k0, r0, k2, r2);
-    cex(k1, r1, k3, r3);
-    cex(k1, r1, k2, r2);
+    const float sg = order == 0 ? 1.0F : -1.0F;  // sort keys: the entry (nearest first) or its negation
+    float key[W];
+    int rf[W];
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+        const uint32_t w0 = word(3 * c), w1 = word(3 * c + 1), w2 = word(3 * c + 2);
+        rf[c] = static_cast<int>(word(3 * W + c));
+        const bool used = rf[c] != kEmptyChild;
+        if (count) cnt->nodes += used ? 1u : 0u;
+        float t;
+        bool h = qslab(qlo(w0), qhi(w0), qlo(w1), qhi(w1), qlo(w2), qhi(w2), qa, qb, &t) && used;
+        if (cull) h = h && !(t > lim);
+        n += h ? 1 : 0;
+        key[c] = h ? sg * t : kInf;  // misses last
+    }
+    if (n == 0) return popCulled(st, lim, cull);
+    sortChildren<W>(key, rf);
     // push the others farthest-in-order first (the stack's key is the entry, for popCulled)
-    if (n > 3) st.push(r3, sg * k3);
-    if (n > 2) st.push(r2, sg * k2);
-    if (n > 1) st.push(r1, sg * k1);
-    return r0;
+#pragma unroll
+    for (int k = W - 1; k >= 1; --k)
+        if (k < n) st.push(rf[k], sg * key[k]);
+    return rf[0];
 }
 
 // A ray may walk the quantized tree when the Quantizer's bound (mrt_scene.cpp) holds for it: every 1/d

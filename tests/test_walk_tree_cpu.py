@@ -25,7 +25,9 @@ def test_walk_tree_holds_reference_leaves_with_margin(case):
     boxes, off, cnt, _ = m.triangle_bvh(cfg)
     leaves = {(int(off[i]), int(cnt[i])): boxes[i].astype(np.float64) for i in range(len(cnt)) if cnt[i] > 0}
     nodes, grid, root = m.walk_tree(cfg)
-    refs = nodes[:, 12:].view(np.int32)
+    width = int(root[2])
+    assert width in (4, 8) and nodes.shape[1] == 4 * width
+    refs = nodes[:, 3 * width:].view(np.int32)
     org, step = grid[:3].astype(np.float64), grid[3:].astype(np.float64)
     if not leaves:  # no triangles: nothing to walk
         assert int(root[1]) == 0
@@ -51,9 +53,9 @@ def test_walk_tree_holds_reference_leaves_with_margin(case):
         order.append(i)
         stack.extend(int(r) for r in refs[i] if 0 <= int(r) != EMPTY)
     for i in reversed(order):
-        w = nodes[i, :12].astype(np.int64)
+        w = nodes[i, :3 * width].astype(np.int64)
         u = None
-        for c in range(4):
+        for c in range(width):
             ref = int(refs[i, c])
             if ref == EMPTY:
                 continue
