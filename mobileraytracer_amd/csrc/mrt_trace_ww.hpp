@@ -613,6 +613,9 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         while (leaf < 0) {
             const int first = leafFirst(leaf);
             int nprim = leafCount(leaf);
+            // the first triangle's loads go out with the leaf box's (one round trip, not two)
+            const uint32_t off0 = static_cast<uint32_t>(first) * 48u;
+            const float4 a0 = bload3(triBuf, off0), b0t = bload3(triBuf, off0 + 16u), c0 = bload3(triBuf, off0 + 32u);
             if (!refTree) {
                 // a walk-tree leaf passed a quantized (outward) box: the reference's own test of
                 // its exact box, and the cull against that box's entry, decide (BVH.hpp:357-363)
@@ -631,7 +634,9 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 const uint32_t off = static_cast<uint32_t>(j) * 48u;
                 float t, u, v;
                 if (kCount) ++cnt->tris;
-                if (!triTest(bload3(triBuf, off), bload3(triBuf, off + 16u), bload3(triBuf, off + 32u), o, d, &t, &u, &v))
+                const bool f = k == 0;
+                if (!triTest(f ? a0 : bload3(triBuf, off), f ? b0t : bload3(triBuf, off + 16u),
+                             f ? c0 : bload3(triBuf, off + 32u), o, d, &t, &u, &v))
                     continue;
                 if (t < kEpsilon) continue;
                 if (kAny) {
