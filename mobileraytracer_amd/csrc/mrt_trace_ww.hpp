@@ -414,7 +414,17 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             }
         }
         // ---- lanes whose triangle walk is over: lights (closest only), write the result ----
-        if (rayIdx >= 0 && over && pend == 0) {
+        // Closest hit: the lights' test and the winner's u, v cost the wave dependent loads, so
+        // finished lanes wait (idle, like lanes waiting for a refill) and are completed together
+        // once they and the idle lanes would trigger a refill, no lane is still walking, or the
+        // queue has run dry.
+        const bool doneLane = rayIdx >= 0 && over && pend == 0;
+        bool runDone = true;
+        if (!kAny) {
+            const int nReady = __popcll(__ballot(doneLane || (rayIdx == -1 && !exhausted)));
+            runDone = nReady >= s.refill || __ballot(rayIdx >= 0 && !doneLane) == 0 || __ballot(exhausted) != 0;
+        }
+        if (doneLane && runDone) {
             if (kCount) cnt->rayMax = max(cnt->rayMax, cnt->nodes - cnt->rayStart);
             if (kAny) {
                 out[rayIdx].w = occ ? 1.0F : 0.0F;
