@@ -162,7 +162,11 @@ int64_t mrt_wave_log(mrt_renderer *r, uint64_t *out);
  * key 8 = tail donation: idle lanes of a level's tail walk subtrees of their wave's rays (0, 1 default),
  * key 9 = idle lanes before a walk wave fetches new rays (1-64, default 32),
  * key 10 = k_shade's lean instantiation where it applies (1, default) or always the general one (0),
- * key 11 = k_shade workgroups per CU (default 14; 0: 8) */
+ * key 11 = k_shade workgroups per CU (default 14; 0: 8),
+ * key 12 = sort queues before their walk (0 default, 1 shadow, 2 closest hit, 3 both),
+ * key 13 / 14 = sort key of shadow / closest-hit queues,
+ * key 15 = replay a one-chunk pass from a captured HIP graph (1) or launch it (0, default;
+ *          the replay measured slower) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /
