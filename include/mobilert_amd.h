@@ -157,12 +157,12 @@ int64_t mrt_wave_log(mrt_renderer *r, uint64_t *out);
  * key 3 = shadow rays on the same stream (0) or their own stream (1, default),
  * key 4 = binned emission of child / shadow rays (0 default, 1),
  * key 5 = shadow walk child order: 0 near first, 1 far first (default),
- * key 6 = shadow walk grid, percent of its occupancy grid (1-100; 0 default: by paths per walk lane),
+ * key 6 = shadow walk grid, percent of its occupancy grid (1-100; 0 default: 50-75 by paths per walk lane),
  * key 7 = skip the closest-hit walk of the depth-capped last level (1, default),
  * key 8 = tail donation: idle lanes of a level's tail walk subtrees of their wave's rays (0, 1 default),
  * key 9 = idle lanes before a walk wave fetches new rays (1-64, default 32),
  * key 10 = k_shade's lean instantiation where it applies (1, default) or always the general one (0),
- * key 11 = k_shade workgroups per CU (default 14; 0: 8),
+ * key 11 = k_shade workgroups per CU (-1 default: 14 below 4 paths per walk lane, else 28; 0: 8),
  * key 12 = sort queues before their walk (0 default, 1 shadow, 2 closest hit, 3 both),
  * key 13 / 14 = sort key of shadow / closest-hit queues,
  * key 15 = replay a one-chunk pass from a captured HIP graph (1) or launch it (0, default;

@@ -127,8 +127,8 @@ struct mrt_renderer {
     int gdepth = 0;
     int traceThreads = 0, workGrid = 0;  // traceThreads: resident trace threads, whole device
     int cus = 0;
-    int shadeGridPerCU = 14;             // tuning key 11: k_shade workgroups per CU (two per resident slot of
-                                         // the lean kernel; 0: workGrid)
+    int shadeGridPerCU = -1;             // tuning key 11: k_shade workgroups per CU (14: two per resident slot
+                                         // of the lean kernel; 0: workGrid; -1 auto: by paths per lane)
     int32_t* dBitmap = nullptr;  // for the host-bitmap entry point
     int32_t* dBackup = nullptr;  // progressive mode: the running average before the current pass
     size_t backupN = 0;
@@ -162,6 +162,7 @@ struct mrt_renderer {
     GraphKey graphKey{}, graphSeen{};   // the captured pass; the last pass run directly
     hipGraphExec_t graphExec = nullptr;
     hipEvent_t graphIn = nullptr, graphOut = nullptr;
+    unsigned long long* hostStats = nullptr;  // pinned: the per-pass statistics read back by DMA
 
     // host copies for the GL preview of the Android front end (mrt_preview_arrays; kept only for
     // renderers made by mrt_create_from_memory): triangles in BVH order and the materials
@@ -178,6 +179,7 @@ struct mrt_renderer {
 
     ~mrt_renderer() {
         if (graphExec != nullptr) (void)hipGraphExecDestroy(graphExec);
+        if (hostStats != nullptr) (void)hipHostFree(hostStats);
         if (graphIn != nullptr) (void)hipEventDestroy(graphIn);
         if (graphOut != nullptr) (void)hipEventDestroy(graphOut);
         for (hipEvent_t e : pipe.evPool) (void)hipEventDestroy(e);
@@ -619,7 +621,13 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // a narrower shadow grid leaves them room (C4 shard at N = 8: 2.92 -> 2.83 ms; at N = 1 the
         // full grid is 2.6 % faster).  Results do not depend on the grid.
         const double pathsPerLane = static_cast<double>(ra.nPaths) / std::max(1, r->traceThreads);
-        const int shadowPct = r->shadowGridPct > 0 ? r->shadowGridPct : pathsPerLane < 4.0 ? 60 : pathsPerLane < 8.0 ? 75 : 100;
+        // (round 2, 4-wide walk tree: C4 shard at N = 8 60 / 50 % -> 2.55 / 2.50 ms; N = 1 100 / 80 /
+        // 70 % with 28 shading workgroups per CU -> 13.48 / 13.34 / 13.34 ms)
+        const int shadowPct = r->shadowGridPct > 0 ? r->shadowGridPct : pathsPerLane < 4.0 ? 50 : pathsPerLane < 8.0 ? 75 : 70;
+        // k_shade's grid: where a lane sees many paths a deeper grid hides the shading's gathers
+        // beside the concurrent shadow walk (14 / 28 per CU: N = 1 13.55 / 13.48 ms, N = 4 shard
+        // 4.10 / 4.07 ms); the smallest shards keep 14 (N = 8: 2.55 / 2.56 ms)
+        const int shadePerCU = r->shadeGridPerCU >= 0 ? r->shadeGridPerCU : pathsPerLane < 4.0 ? 14 : 28;
         // refill threshold: larger batches where a lane sees few paths (a small shard: the tail
         // dominates; C4 shard at N = 8: 24 / 32 / 40 -> 2.68 / 2.64 / 2.61 ms), smaller where it
         // sees many (N = 1: 13.77 / 13.86 / 13.88 ms)
@@ -645,7 +653,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             if (!(skipLastShade && l == nLevels)) {
                 launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa,
-                            r->shadeGridPerCU > 0 ? r->cus * r->shadeGridPerCU : r->workGrid, st,
+                            shadePerCU > 0 ? r->cus * shadePerCU : r->workGrid, st,
                             skipLastShade && l + 1 == nLevels);
                 ++r->shadeLaunches;
             }
@@ -752,9 +760,11 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     using namespace mrt;
     const auto t0 = std::chrono::steady_clock::now();
     renderPassGraphed(r, dBitmap, dPacked, st, sampleBase, spp);
-    unsigned long long hs[kNumStats] = {};
-    MRT_HIP(hipMemcpyAsync(hs, r->pipe.stats, sizeof(unsigned long long) * kNumStats, hipMemcpyDeviceToHost, st));
+    if (r->hostStats == nullptr) MRT_HIP(hipHostMalloc(&r->hostStats, sizeof(unsigned long long) * kNumStats));
+    MRT_HIP(hipMemcpyAsync(r->hostStats, r->pipe.stats, sizeof(unsigned long long) * kNumStats, hipMemcpyDeviceToHost, st));
     MRT_HIP(hipStreamSynchronize(st));
+    unsigned long long hs[kNumStats];
+    std::memcpy(hs, r->hostStats, sizeof(hs));
     const auto t1 = std::chrono::steady_clock::now();
     if (hs[kStatOverflow] != 0) return false;
     fs->rays += hs[kStatRays];
@@ -1172,7 +1182,7 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->binMode = value;
         return 0;
     }
-    if (key == 11 && value >= 0 && value <= 64) {
+    if (key == 11 && value >= -1 && value <= 64) {
         r->shadeGridPerCU = value;
         return 0;
     }

@@ -430,11 +430,11 @@ def test_walk_knobs_are_invariant_and_wave_log_is_consistent():
     cfg = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5)
     outs = []
     with m.Renderer(cfg) as r:
-        for key, val in ((6, 0), (6, 40), (6, 100), (9, 1), (9, 64), (10, 0), (11, 3)):
+        for key, val in ((6, 0), (6, 40), (6, 100), (9, 1), (9, 64), (10, 0), (11, 3), (11, 14), (11, 28)):
             r.set_tuning(6, 0)
             r.set_tuning(9, 32)
             r.set_tuning(10, 1)
-            r.set_tuning(11, 14)
+            r.set_tuning(11, -1)
             r.set_tuning(key, val)
             assert r.get_tuning(key) == val
             bm = np.zeros(cfg.width * cfg.height, np.int32)
