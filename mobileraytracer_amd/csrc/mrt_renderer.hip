@@ -622,8 +622,13 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // full grid is 2.6 % faster).  Results do not depend on the grid.
         const double pathsPerLane = static_cast<double>(ra.nPaths) / std::max(1, r->traceThreads);
         // (round 2, 4-wide walk tree: C4 shard at N = 8 60 / 50 % -> 2.55 / 2.50 ms; N = 1 100 / 80 /
-        // 70 % with 28 shading workgroups per CU -> 13.48 / 13.34 / 13.34 ms)
-        const int shadowPct = r->shadowGridPct > 0 ? r->shadowGridPct : pathsPerLane < 4.0 ? 50 : pathsPerLane < 8.0 ? 75 : 70;
+        // 70 % with 28 shading workgroups per CU -> 13.48 / 13.34 / 13.34 ms).  With shadow rays on
+        // the render stream (key 3 = 0) nothing runs beside the shadow walk: full grid.
+        const int shadowPct = r->shadowGridPct > 0 ? r->shadowGridPct
+                              : sb == st            ? 100
+                              : pathsPerLane < 4.0  ? 50
+                              : pathsPerLane < 8.0  ? 75
+                                                    : 70;
         // k_shade's grid: where a lane sees many paths a deeper grid hides the shading's gathers
         // beside the concurrent shadow walk (14 / 28 per CU: N = 1 13.55 / 13.48 ms, N = 4 shard
         // 4.10 / 4.07 ms); the smallest shards keep 14 (N = 8: 2.55 / 2.56 ms)
