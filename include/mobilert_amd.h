@@ -57,10 +57,14 @@ typedef struct mrt_config {
     int32_t rankCount;    /* number of shards (GPUs); <= 0 -> 1 */
     int32_t device;       /* HIP device ordinal, -1 = current device */
     int32_t cull;         /* near-first traversal with t-culling of the triangle BVH:
-                           * 0 none (the reference's visit set), 1 (default) fast: a box whose
-                           * entry exceeds best * (1 + 2^-10) is skipped, 2 certified: skipped
-                           * only on a rigorous bound of Moller-Trumbore's rounding (exact for
-                           * every input, slower).  See DESIGN.md section 3. */
+                           * 0 none (the reference's visit set; exact), 1 fast: a box whose entry
+                           * exceeds best * (1 + 2^-10) is skipped (NOT exact for every input:
+                           * a grazing Moller-Trumbore hit can lie before its box), 2 certified:
+                           * every box skipped only on a rigorous bound of Moller-Trumbore's
+                           * rounding (exact, slow), 3 exact (recommended; RayTrace, the Android
+                           * session and the Python Config use it): inner boxes never skipped,
+                           * leaves skipped on the certified bound of their own triangles.  See
+                           * DESIGN.md section 3. */
     int32_t maxPathsPerPass; /* <= 0 -> automatic chunk size */
     int32_t progressive;  /* 1: one pass per sample; bitmap and mrt_get_sample() updated after
                            * each (Renderer.cpp:53-88).  0: all samples in flight at once.
@@ -153,7 +157,7 @@ int64_t mrt_wave_log(mrt_renderer *r, uint64_t *out);
 /* tuning knobs for A/B measurement (results are identical for every value):
  * key 1 = trace walk: 0 per-wave 64-ray batches with the plain DFS of BVH.hpp:327-384,
  *         1 persistent while-while walk (default),
- * key 2 = cull mode of walk 1: 0 none, 1 fast (default), 2 certified (mrt_config.cull),
+ * key 2 = cull mode of walk 1: 0 none, 1 fast (inexact), 2 certified, 3 exact (mrt_config.cull),
  * key 3 = shadow rays on the same stream (0) or their own stream (1, default),
  * key 4 = binned emission of child / shadow rays (0 default, 1),
  * key 5 = shadow walk child order: 0 near first, 1 far first (default),

@@ -51,7 +51,7 @@ typedef struct mrt_android_config {
 /* readFile: the bytes of one file picked by the user.  ".obj", ".mtl", ".cam" are kept as the scene
  * definition for the next initialize; anything else is a texture, cached by its file name. */
 void mrt_android_read_file(const char *path, const uint8_t *bytes, int64_t size);
-/* rtInitialize: builds the renderer (built-in scenes 0-3, else the OBJ read before, whose
+/* rtInitialize: cancels a render still running and waits for its thread, then builds the renderer (built-in scenes 0-3, else the OBJ read before, whose
  * definitions are then dropped).  Returns triangles + spheres + planes, or -1 (out of memory or
  * the OBJ could not be processed), -2 (any other error; message in mrt_last_error), -3. */
 int32_t mrt_android_initialize(const mrt_android_config *config);
@@ -59,6 +59,13 @@ int32_t mrt_android_initialize(const mrt_android_config *config);
  * until the state leaves BUSY) on a detached thread while the state is BUSY (one frame), updating
  * fps / sample, then FINISHED unless stopped, then IDLE.  nThreads is the reference's and unused. */
 void mrt_android_render_into_bitmap(int32_t *pixels, int32_t nThreads);
+/* The same, and done(user) is called on the render thread once its last frame has returned, i.e.
+ * once nothing writes pixels any more (the JNI layer unlocks the Android bitmap there, as the
+ * reference's render thread does, JNI_layer.cpp:850-854). */
+typedef void (*mrt_android_done_fn)(void *user);
+void mrt_android_render_into_bitmap_cb(int32_t *pixels, int32_t nThreads, mrt_android_done_fn done, void *user);
+/* Blocks until no render thread is running (every pixels buffer handed over is released). */
+void mrt_android_wait_render(void);
 /* rtStartRender: with wait, blocks until the previous render finished; state BUSY. */
 void mrt_android_start_render(int32_t wait);
 /* rtStopRender: state STOPPED, the renderer's cooperative cancel. */
@@ -77,7 +84,8 @@ int32_t mrt_android_resize(int32_t size);
 int64_t mrt_android_vertices(float *out);
 int64_t mrt_android_colors(float *out);
 int64_t mrt_android_camera(float *out);
-/* drops the renderer and every cached file (JNI_OnUnload) */
+/* drops the renderer (after cancelling and waiting for a running render) and every cached file
+ * (JNI_OnUnload) */
 void mrt_android_reset(void);
 
 #ifdef __cplusplus

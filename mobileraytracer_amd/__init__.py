@@ -49,7 +49,7 @@ class Config:
     rankIndex: int = 0
     rankCount: int = 1
     device: int = -1
-    cull: int = 1
+    cull: int = 3
     maxPathsPerPass: int = 0
     progressive: int = 0
 

@@ -20,7 +20,8 @@ EXPORTED_SYMBOLS = (
     "mrt_get_tuning", "mrt_triangle_bvh", "mrt_walk_tree", "mrt_decode_texture", "mrt_kat_slab", "mrt_kat_triangle",
     "mrt_trace_rays", "mrt_sample_tables", "mrt_regular_grid", "mrt_grid_box_test", "mrt_create_from_memory",
     "mrt_preview_arrays", "mrt_wave_log",
-    "mrt_android_read_file", "mrt_android_initialize", "mrt_android_render_into_bitmap", "mrt_android_start_render",
+    "mrt_android_read_file", "mrt_android_initialize", "mrt_android_render_into_bitmap",
+    "mrt_android_render_into_bitmap_cb", "mrt_android_wait_render", "mrt_android_start_render",
     "mrt_android_stop_render", "mrt_android_finish_render", "mrt_android_state", "mrt_android_fps",
     "mrt_android_time_renderer", "mrt_android_sample", "mrt_android_number_of_lights", "mrt_android_resize",
     "mrt_android_vertices", "mrt_android_colors", "mrt_android_camera", "mrt_android_reset",
@@ -123,6 +124,8 @@ def load_library(path=LIB_PATH):
         "mrt_android_read_file": (None, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
         "mrt_android_initialize": (ctypes.c_int32, [P(MrtAndroidConfig)]),
         "mrt_android_render_into_bitmap": (None, [vp, ctypes.c_int32]),
+        "mrt_android_render_into_bitmap_cb": (None, [vp, ctypes.c_int32, vp, vp]),
+        "mrt_android_wait_render": (None, []),
         "mrt_android_start_render": (None, [ctypes.c_int32]),
         "mrt_android_stop_render": (None, [ctypes.c_int32]),
         "mrt_android_finish_render": (None, []),

@@ -22,7 +22,16 @@ from . import _native
 
 IDLE, BUSY, FINISHED, STOPPED = 0, 1, 2, 3  # JNI_layer.hpp:12-13
 
-_pixels = None  # the bitmap a render thread writes: kept alive here, as the locked Android bitmap is
+# The bitmaps render threads still write, kept alive as the locked Android bitmap is: each is
+# released by its render thread's done callback, once that thread's last frame has returned.
+_live = {}
+_token = [0]
+_DONE = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+
+@_DONE
+def _release(user):
+    _live.pop(int(user or 0), None)
 
 
 def _lib():
@@ -44,10 +53,20 @@ def initialize(scene: int, shader: int, accelerator: int, width: int, height: in
 
 
 def render_into_bitmap(pixels: np.ndarray, n_threads: int = 1) -> None:
-    global _pixels
     assert pixels.dtype == np.int32 and pixels.flags["C_CONTIGUOUS"]
-    _pixels = pixels
-    _lib().mrt_android_render_into_bitmap(ctypes.c_void_p(pixels.ctypes.data), n_threads)
+    _token[0] += 1
+    _live[_token[0]] = pixels
+    _lib().mrt_android_render_into_bitmap_cb(ctypes.c_void_p(pixels.ctypes.data), n_threads,
+                                             ctypes.cast(_release, ctypes.c_void_p), ctypes.c_void_p(_token[0]))
+
+
+def wait_render() -> None:
+    """Blocks until no render thread is running (every bitmap handed over is released)."""
+    _lib().mrt_android_wait_render()
+
+
+def bitmaps_in_use() -> int:
+    return len(_live)
 
 
 def start_render(wait: bool = False) -> None:

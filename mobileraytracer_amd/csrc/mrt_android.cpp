@@ -27,6 +27,8 @@ namespace {
 
 std::mutex gMutex;                    // guards the renderer and the cached files (JNI_layer.cpp:64)
 std::condition_variable gRendered;    // :79
+std::condition_variable gIdle;        // a render thread ended (gActive dropped)
+int32_t gActive = 0;                  // render threads still running (guarded by gMutex)
 std::atomic<int32_t> gState{MRT_STATE_IDLE};
 std::atomic<bool> gFinished{true};    // finishedRendering_ (:84)
 std::atomic<float> gFps{0.0F};
@@ -60,6 +62,15 @@ std::shared_ptr<mrt_renderer> current() {
     return gRenderer;
 }
 
+// Cancels the render in flight and waits for its thread to end (the lock is released while
+// waiting): the renderer and the caller's pixels may be replaced or freed only after that, since
+// the thread's last mrt_render_frame writes the pixels until it returns.
+void stopAndWait(std::unique_lock<std::mutex>& lock) {
+    if (gActive == 0) return;
+    if (gRenderer != nullptr) mrt_stop_render(gRenderer.get());
+    gIdle.wait(lock, [] { return gActive == 0; });
+}
+
 }  // namespace
 
 extern "C" {
@@ -83,7 +94,8 @@ void mrt_android_read_file(const char* path, const uint8_t* bytes, int64_t size)
 
 int32_t mrt_android_initialize(const mrt_android_config* config) {
     try {
-        std::lock_guard<std::mutex> lock(gMutex);
+        std::unique_lock<std::mutex> lock(gMutex);
+        stopAndWait(lock);
         gRenderer.reset();
         mrt_config c{};
         c.width = config->width;
@@ -100,7 +112,7 @@ int32_t mrt_android_initialize(const mrt_android_config* config) {
         c.camFilePath = "";
         c.rankCount = 1;
         c.device = -1;
-        c.cull = 1;
+        c.cull = 3;  // exact for every input
         c.progressive = 1;  // the bitmap fills sample by sample while RenderTask polls it
         const bool builtin = config->scene >= 0 && config->scene <= 3;
         mrt_renderer* r = nullptr;
@@ -146,24 +158,43 @@ int32_t mrt_android_initialize(const mrt_android_config* config) {
     }
 }
 
-void mrt_android_render_into_bitmap(int32_t* pixels, int32_t nThreads) {
+void mrt_android_render_into_bitmap_cb(int32_t* pixels, int32_t nThreads, mrt_android_done_fn done, void* user) {
     (void)nThreads;  // Renderer::renderFrame's thread count: the GPU path does not use it
-    std::shared_ptr<mrt_renderer> r = current();
-    std::thread([r, pixels] {  // detached render thread (:883-889)
+    std::shared_ptr<mrt_renderer> r;
+    {
+        std::lock_guard<std::mutex> lock(gMutex);
+        r = gRenderer;
+        ++gActive;  // before the thread starts: an initialize / reset right after this call waits for it
+    }
+    std::thread([r, pixels, done, user] {  // detached render thread (:883-889)
         int32_t rep = 1;
         while (gState == MRT_STATE_BUSY && rep > 0) {
             if (r != nullptr) (void)mrt_render_frame(r.get(), pixels);
             updateFps();
             rep--;
         }
+        // the last frame has returned: the caller may release the pixels now (the reference unlocks
+        // the Android bitmap here, in the render thread, :850-854)
+        if (done != nullptr) done(user);
         gFinished = true;
         gRendered.notify_all();
         {
             std::lock_guard<std::mutex> lock(gMutex);
             if (gState != MRT_STATE_STOPPED) gState = MRT_STATE_FINISHED;
+            --gActive;
         }
+        gIdle.notify_all();
         gState = MRT_STATE_IDLE;
     }).detach();
+}
+
+void mrt_android_render_into_bitmap(int32_t* pixels, int32_t nThreads) {
+    mrt_android_render_into_bitmap_cb(pixels, nThreads, nullptr, nullptr);
+}
+
+void mrt_android_wait_render(void) {
+    std::unique_lock<std::mutex> lock(gMutex);
+    gIdle.wait(lock, [] { return gActive == 0; });
 }
 
 void mrt_android_start_render(int32_t wait) {  // :406-426
@@ -236,8 +267,8 @@ int64_t mrt_android_camera(float* out) {
 }
 
 void mrt_android_reset(void) {
-    std::lock_guard<std::mutex> lock(gMutex);
-    if (gRenderer != nullptr) mrt_stop_render(gRenderer.get());
+    std::unique_lock<std::mutex> lock(gMutex);
+    stopAndWait(lock);
     gRenderer.reset();
     gObj.clear();
     gMtl.clear();

@@ -24,8 +24,9 @@ struct DScene {
     const float4* triShade;    // 3 per triangle: nA (w = material index bits), nB, nC
     const GNode* triNodes;     // the reference tree (triRootRef)
     const QNode4* triQNodes;   // the walk tree (triRoot), 4-wide and quantized (QNode4)
-    // the reference box of the leaf whose first triangle is t: [2t] = min xyz, max x; [2t+1].xy =
-    // max yz (walk-tree leaves are tested exactly before their triangles)
+    // per leaf, indexed by its first triangle t (48 B): [3t] = min xyz, max x; [3t+1].xy = max yz
+    // (walk-tree leaves are tested exactly before their triangles); [3t+1].zw, [3t+2] = the leaf's
+    // certified-cull record (mrt_scene.cpp leafCullRecord; the exact cull mode)
     const float4* leafBoxes;
     const float4* planes;      // 2 per plane: normal (w = material bits), point
     const GNode* planeNodes;
@@ -52,7 +53,7 @@ struct DScene {
     int32_t qEnabled;          // 0: every ray walks the reference tree (a non-finite scene box)
     int32_t nLights;
     int32_t nMats;
-    int32_t cull;              // walk 1's cull mode: 0 none, 1 fast, 2 certified (mrt_trace_ww.hpp)
+    int32_t cull;              // walk 1's cull mode: 0 none, 1 fast, 2 certified, 3 exact (mrt_trace_ww.hpp)
     int32_t variant;           // trace walk: 0 per-wave reference walk, 1 persistent while-while
     int32_t triTop;            // triQNodes[0, triTop) are the breadth-first top of the walk tree
     int32_t matsFinite;        // every material's Kd / Ks / Kt component is finite

@@ -1124,6 +1124,7 @@ int persistentGrid(K kernel, int slot, int maxThreads) {
         if (s.variant == 0) MRT_LAUNCH_ONE(KERNEL, 0, kCullNone, SLOT);                                        \
         else if (s.cull == kCullFast) MRT_LAUNCH_ONE(KERNEL, 1, kCullFast, SLOT + 1);                          \
         else if (s.cull == kCullCertified) MRT_LAUNCH_ONE(KERNEL, 1, kCullCertified, SLOT + 2);                \
+        else if (s.cull == kCullExact) MRT_LAUNCH_ONE(KERNEL, 1, kCullExact, SLOT + 4);                        \
         else MRT_LAUNCH_ONE(KERNEL, 1, kCullNone, SLOT + 3);                                                   \
     } while (0)
 
@@ -1143,7 +1144,7 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
         hipLaunchKernelGGL((k_trace_other<true>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }
-    MRT_LAUNCH_WALK(k_shadow, 4);
+    MRT_LAUNCH_WALK(k_shadow, 5);
 }
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
@@ -1228,10 +1229,12 @@ int traceResidentThreadsPerCU() {
                              reinterpret_cast<const void*>(k_trace<false, 1, kCullFast>),
                              reinterpret_cast<const void*>(k_trace<false, 1, kCullCertified>),
                              reinterpret_cast<const void*>(k_trace<false, 1, kCullNone>),
+                             reinterpret_cast<const void*>(k_trace<false, 1, kCullExact>),
                              reinterpret_cast<const void*>(k_shadow<false, 0, kCullNone>),
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullFast>),
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullCertified>),
-                             reinterpret_cast<const void*>(k_shadow<false, 1, kCullNone>)};
+                             reinterpret_cast<const void*>(k_shadow<false, 1, kCullNone>),
+                             reinterpret_cast<const void*>(k_shadow<false, 1, kCullExact>)};
     for (const void* k : kernels) {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWalkThreads, 0) == hipSuccess)

@@ -307,12 +307,17 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     }
     toDeviceBVH(tn, sc.triangles.size(), &g, &d.triRootRef, 0, nullptr, &conesRef);
     {
-        std::vector<float4> lb(std::max<size_t>(1, 2 * sc.triangles.size()), make_float4(0.0F, 0.0F, 0.0F, 0.0F));
+        // per leaf (indexed by its first triangle, 48 B): the exact reference box, then the
+        // certified-cull record of its own triangles (leafCullRecord) for the exact mode
+        std::vector<float4> lb(std::max<size_t>(1, 3 * sc.triangles.size()), make_float4(0.0F, 0.0F, 0.0F, 0.0F));
         for (const HBVHNode& n : tn) {
             if (n.numPrimitives <= 0) continue;
             const size_t f = static_cast<size_t>(n.indexOffset);
-            lb[2 * f] = make_float4(n.box.mn.x, n.box.mn.y, n.box.mn.z, n.box.mx.x);
-            lb[2 * f + 1] = make_float4(n.box.mx.y, n.box.mx.z, 0.0F, 0.0F);
+            float c[6];
+            leafCullRecord(sc.triangles, f, f + static_cast<size_t>(n.numPrimitives), n.box, c);
+            lb[3 * f] = make_float4(n.box.mn.x, n.box.mn.y, n.box.mn.z, n.box.mx.x);
+            lb[3 * f + 1] = make_float4(n.box.mx.y, n.box.mx.z, c[0], c[1]);
+            lb[3 * f + 2] = make_float4(c[2], c[3], c[4], c[5]);
         }
         d.leafBoxes = r->sceneMem.upload(lb, st);
     }
@@ -1170,7 +1175,7 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.variant = value;
         return 0;
     }
-    if (key == 2 && value >= 0 && value <= 2) {
+    if (key == 2 && value >= 0 && value <= 3) {
         r->ds.cull = value;
         return 0;
     }
@@ -1613,7 +1618,7 @@ void workThread(::MobileRT::Config& config) {
         const char* dev = std::getenv("MOBILERT_DEVICE");
         c.device = dev != nullptr ? std::atoi(dev) : -1;
         c.rankCount = 1;
-        c.cull = 1;
+        c.cull = 3;  // exact for every input
         c.progressive = 1;  // the UI polls config.bitmap while the frame renders
         const auto tc0 = std::chrono::steady_clock::now();
         mrt_renderer* r = createRenderer(&c);

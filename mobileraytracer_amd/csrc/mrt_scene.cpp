@@ -1020,8 +1020,9 @@ struct Quantizer {
 }  // namespace
 
 bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
-                     QGrid* grid, std::vector<QNode4>* out) {
+                     QGrid* grid, std::vector<QNode4>* out, std::vector<int32_t>* bvh2Of) {
     out->clear();
+    if (bvh2Of != nullptr) bvh2Of->clear();
     if (topPlaced != nullptr) *topPlaced = 0;
     const HBVHNode& r = nodes[0];
     const float rmn[3] = {r.box.mn.x, r.box.mn.y, r.box.mn.z}, rmx[3] = {r.box.mx.x, r.box.mx.y, r.box.mx.z};
@@ -1049,6 +1050,7 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
     // collapse: the 4-wide node of BVH2 node i has up to four BVH2 descendants as children
     std::vector<std::array<int32_t, kWalkWidth>> kids;  // per walk node: BVH2 indices (-1: none)
     std::vector<int32_t> node4Of(nodes.size(), -1);
+    std::vector<int32_t> kidsBvh2{0};  // per walk node: its BVH2 node
     std::vector<int32_t> work{0};
     node4Of[0] = 0;
     kids.emplace_back();
@@ -1077,6 +1079,7 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
             k4[k] = c[k];
             if (inner(c[k])) {
                 node4Of[static_cast<size_t>(c[k])] = static_cast<int32_t>(kids.size());
+                kidsBvh2.push_back(c[k]);
                 kids.emplace_back();
                 kids.back().fill(-1);
                 work.push_back(c[k]);
@@ -1111,6 +1114,10 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
                 dfs.push_back(node4Of[static_cast<size_t>(k4[static_cast<size_t>(k)])]);
     }
     out->resize(n4);
+    if (bvh2Of != nullptr) {
+        bvh2Of->resize(n4);
+        for (size_t k = 0; k < n4; ++k) (*bvh2Of)[k] = kidsBvh2[static_cast<size_t>(order[k])];
+    }
     for (size_t k = 0; k < n4; ++k) {
         const auto& k4 = kids[static_cast<size_t>(order[k])];
         QNode4& q = (*out)[k];
@@ -1193,6 +1200,68 @@ uint32_t coneWord(const std::vector<HTriangle>& tris, size_t lo, size_t hi) {
     return qx | (qy << 9) | (static_cast<uint32_t>(qCode) << 18) | (static_cast<uint32_t>(kCode) << 25);
 }
 }  // namespace
+
+void cullRecord(const std::vector<HTriangle>& tris, const std::vector<std::array<int32_t, 2>>& ranges,
+                const double ctr[3], double hd, float out[6]) {
+    const float never[6] = {0.0F, 0.0F, 0.0F, 1.0F, 0.0F, 0.0F};
+    std::copy(never, never + 6, out);
+    double kMax = 1.0;
+    double m[3][3] = {};  // sum of n n^T over unit normals (lines: sign-free)
+    std::vector<std::array<double, 3>> ns;
+    for (const auto& rg : ranges) {
+        for (int32_t i = rg[0]; i < rg[1]; ++i) {
+            const HTriangle& t = tris[static_cast<size_t>(i)];
+            const double ab[3] = {t.AB.x, t.AB.y, t.AB.z}, ac[3] = {t.AC.x, t.AC.y, t.AC.z};
+            const double n[3] = {ab[1] * ac[2] - ab[2] * ac[1], ab[2] * ac[0] - ab[0] * ac[2],
+                                 ab[0] * ac[1] - ab[1] * ac[0]};
+            const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+            const double l1 = (std::fabs(ab[0]) + std::fabs(ab[1]) + std::fabs(ab[2])) *
+                              (std::fabs(ac[0]) + std::fabs(ac[1]) + std::fabs(ac[2]));
+            if (!(len > 0.0) || !std::isfinite(l1)) return;
+            kMax = std::max(kMax, l1 / len);
+            const std::array<double, 3> u{n[0] / len, n[1] / len, n[2] / len};
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) m[r][c] += u[static_cast<size_t>(r)] * u[static_cast<size_t>(c)];
+            ns.push_back(u);
+        }
+    }
+    if (ns.empty()) return;
+    int col = 0;
+    for (int c = 1; c < 3; ++c)
+        if (m[c][c] > m[col][col]) col = c;
+    double a[3] = {m[0][col], m[1][col], m[2][col]};
+    for (int it = 0; it < 64; ++it) {
+        double b[3];
+        for (int r = 0; r < 3; ++r) b[r] = m[r][0] * a[0] + m[r][1] * a[1] + m[r][2] * a[2];
+        const double l = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
+        if (!(l > 0.0)) return;
+        for (int r = 0; r < 3; ++r) a[r] = b[r] / l;
+    }
+    double cosMin = 1.0;
+    for (const auto& u : ns) cosMin = std::min(cosMin, std::fabs(u[0] * a[0] + u[1] * a[1] + u[2] * a[2]));
+    // psi widened by 1e-3 rad: the float storage of a' and q, and the kernel's float evaluation
+    const double psi = std::acos(std::min(1.0, cosMin)) + 1e-3;
+    if (psi >= 1.5) return;
+    const double cq = std::cos(psi), q = std::sin(psi);
+    const double D = 2.0 * hd * 1.0002 + 0x1p-20 * (std::fabs(ctr[0]) + std::fabs(ctr[1]) + std::fabs(ctr[2]) + hd);
+    const double Kc = 0x1p-18 * kMax * 1.001;
+    auto up = [](double x) { return std::nextafter(static_cast<float>(x), std::numeric_limits<float>::infinity()); };
+    if (!std::isfinite(D) || !std::isfinite(Kc)) return;
+    out[0] = static_cast<float>(a[0] * cq);
+    out[1] = static_cast<float>(a[1] * cq);
+    out[2] = static_cast<float>(a[2] * cq);
+    out[3] = up(q);
+    out[4] = up(Kc);
+    out[5] = up(D);
+}
+
+void leafCullRecord(const std::vector<HTriangle>& tris, size_t lo, size_t hi, const HAABB& box, float out[6]) {
+    const double ctr[3] = {0.5 * (double(box.mn.x) + box.mx.x), 0.5 * (double(box.mn.y) + box.mx.y),
+                           0.5 * (double(box.mn.z) + box.mx.z)};
+    const double dx = double(box.mx.x) - box.mn.x, dy = double(box.mx.y) - box.mn.y, dz = double(box.mx.z) - box.mn.z;
+    const double hd = 0.5 * std::sqrt(dx * dx + dy * dy + dz * dz);
+    cullRecord(tris, {{static_cast<int32_t>(lo), static_cast<int32_t>(hi)}}, ctr, hd, out);
+}
 
 // A second topology over the reference tree's leaves ("walk tree").
 // Reachability of a triangle in the reference walk is its leaf box passing the slab test: every

@@ -12,6 +12,7 @@
 #include <functional>
 #include <istream>
 #include <string>
+#include <array>
 #include <vector>
 
 namespace mrt {
@@ -151,7 +152,7 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
 // Quantizer (mrt_scene.cpp) and numbered as toDeviceBVH numbers (the first topCount breadth-first).  Fills
 // root (box of nodes[0], reference into out); false when a box or the grid is not finite.
 bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
-                     QGrid* grid, std::vector<QNode4>* out);
+                     QGrid* grid, std::vector<QNode4>* out, std::vector<int32_t>* bvh2Of = nullptr);
 // A tree over the same leaves (primitive ranges and boxes) as the reference tree `ref`, grouped
 // by a full-sweep SAH; its inner boxes are exact unions of the leaf boxes (reference numbering:
 // node 0 the root, an inner node's children at indexOffset and indexOffset + 1).
@@ -159,6 +160,15 @@ std::vector<HBVHNode> rebuildOverLeaves(const std::vector<HBVHNode>& ref, int we
 // The cull word (mrt_common.hpp) of every node of a triangle BVH built by buildBVH over tris
 // (already in BVH order): the normal-line cone and the conditioning bound K of its triangles.
 std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris);
+// The certified-cull record of a set of triangles [lo, hi) inside box (the exact mode's leaf cull,
+// mrt_trace_ww.hpp leafKey): out = {a'.x, a'.y, a'.z, q, Kc, D} with a' = a cos(psi) for a normal-line
+// cone (axis a, half-angle psi) holding every triangle's normal, q >= sin(psi), Kc >= 2^-18 * 1.001 *
+// max(1, |AB|_1 |AC|_1 / |AB x AC|), D >= 2.0002 * half diagonal + 2^-20 (|centre|_1 + half diagonal).
+// No bound (degenerate triangle, cone wider than 90 degrees): {0, 0, 0, 1, 0, 0}, which never culls.
+void leafCullRecord(const std::vector<HTriangle>& tris, size_t lo, size_t hi, const HAABB& box, float out[6]);
+// The same over several triangle ranges, with D covering a box of half diagonal hd around centre ctr.
+void cullRecord(const std::vector<HTriangle>& tris, const std::vector<std::array<int32_t, 2>>& ranges,
+                const double ctr[3], double hd, float out[6]);
 
 // RegularGrid<T> build (mrt_grid.cpp): prims in BVH order, order[j] = input index of prims[j]
 struct HGrid {

@@ -112,6 +112,28 @@ __device__ __forceinline__ float cullKey(uint32_t w, float mnx, float mny, float
     return fmaxf(fmaxf(kx, ky), kz);
 }
 
+// The exact mode's certified leaf key (mode 3): the same bound as cullKey, evaluated from a leaf
+// record precomputed on the host (mrt_scene.cpp leafCullRecord: r1.zw, r2.x = a' = a cos(psi),
+// r2.y = q >= sin(psi), r2.z = Kc >= 2^-18 * 1.001 * K, r2.w = D) with cheaper, looser steps:
+//   |d . n| >= |d . a| cos psi - |d x a| sin psi >= |d . a'| - q |d|_1       (|d x a| <= |d|_1)
+//   den = that - (2e-6 + Kc / 4) |d|_1 <= smin - 2e-6 |d| - 2^-20 K |d|_1
+//   L = te |d|_1 1.0001 + D >= |o - A| for every vertex A in the box (the ray's entry point is in it)
+//   rho = L (Kc |d|_1 / den + 2^-20) 1.002 >= cullKey's rho (rcp's 1 ulp and the 2^-19 of the
+//   inflation included), key = the entry of the box inflated by rho, per axis, rounded down.
+// Every float step rounds at most a few ulps against margins of >= 2^-19 relative.  key <= te.
+__device__ __forceinline__ float leafKey(float4 r1, float4 r2, float te, float ex, float ey, float ez, v3 d, v3 inv) {
+    const float dl1 = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    const float c = fabsf(fmaf(d.z, r2.x, fmaf(d.y, r1.w, d.x * r1.z)));
+    const float den = c - dl1 * (r2.y + fmaf(0.25F, r2.z, 2e-6F));
+    if (!(den > 0.0F)) return 0.0F;
+    const float L = fmaf(te, dl1 * 1.0001F, r2.w);
+    const float rho = L * fmaf(r2.z * dl1, __builtin_amdgcn_rcpf(den), 0x1p-20F) * 1.002F;
+    const float kx = fmaf(-rho, fabsf(inv.x), fmaf(-0x1p-19F, fabsf(ex), ex));
+    const float ky = fmaf(-rho, fabsf(inv.y), fmaf(-0x1p-19F, fabsf(ey), ey));
+    const float kz = fmaf(-rho, fabsf(inv.z), fmaf(-0x1p-19F, fabsf(ez), ez));
+    return fmaxf(fmaxf(kx, ky), kz);
+}
+
 // Culling against the keys, near-first order (by box entry) and the push of the far child.
 __device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float tr, float kl, float kr, int refL,
                                               int refR, float lim, bool cull, TStack& st, bool rightFirst) {
@@ -139,17 +161,26 @@ __device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float 
 //   0  no culling: exactly the reference's visit set;
 //   1  fast: skip a box whose entry exceeds best * (1 + 2^-10).  Exact unless a triangle inside
 //      is hit at a grazing angle (|d . n| below ~1e-3) whose rounding moves Moller-Trumbore's t
-//      below the best hit (tests/cull_cases.py builds one); no such ray in any tested frame;
+//      below the best hit (tests/cull_cases.py builds one); NOT exact for every input;
 //   2  certified: the keys of cullKey (a rigorous lower bound on every acceptable t below the
-//      box), exact for every input; slower (the bound needs each child's normal cone, and the
-//      cones of closed objects hold every direction).
-constexpr int kCullNone = 0, kCullFast = 1, kCullCertified = 2;
+//      box) on every node of the reference tree, exact for every input; slow (the bound needs
+//      each child's normal cone, and the cones of closed objects hold every direction);
+//   3  exact (default): the inner nodes of the quantized 4-wide tree are never culled (mode 0's
+//      visit set), and a leaf whose exact box passes is skipped only when its certified key
+//      (cullKey over the leaf's own <= 4 triangles, whose cone is narrow) exceeds the best:
+//      exact for every input, and the triangle tests behind the best hit are mostly avoided.
+constexpr int kCullNone = 0, kCullFast = 1, kCullCertified = 2, kCullExact = 3;
 constexpr float kCullMargin = 0x1p-10f;  // cull mode 1
 
 // the limit a key is compared with: a child / stack entry is skipped iff key > limit
 template <int kCull>
 __device__ __forceinline__ float cullLimit(float best) {
     return kCull == kCullFast ? best + best * kCullMargin : best;
+}
+// modes that cull inner nodes and stack entries (mode 3 culls leaves only)
+template <int kCull>
+constexpr int innerCullMode() {
+    return (kCull == kCullFast || kCull == kCullCertified) ? kCull : kCullNone;
 }
 
 // One BVH2 inner-node visit: returns the next node (near child, or a popped entry).
@@ -343,7 +374,8 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
     const BufRes qBuf = bufferOf(s.triQNodes);
     const BufRes triBuf = bufferOf(s.triGeom);
     const BufRes leafBuf = bufferOf(s.leafBoxes);
-    constexpr bool cull = kCull != kCullNone;
+    constexpr int kInner = innerCullMode<kCull>();  // the cull mode of inner nodes and pops
+    constexpr bool cull = kInner != kCullNone;
     const int lane = static_cast<int>(threadIdx.x & 63u);
     int rayIdx = -1;
     bool exhausted = false;
@@ -557,7 +589,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 const int dl = __ffsll(static_cast<unsigned long long>(donors)) - 1;
                 donors &= donors - 1;  // one subtree per donor and sweep
                 int2 e = make_int2(kRefDone, 0);
-                if (lane == dl) e.x = popCulled(st, cullLimit<kCull>(fminf(bt, shT)), cull);  // its next subtree
+                if (lane == dl) e.x = popCulled(st, cullLimit<kInner>(fminf(bt, shT)), cull);  // its next subtree
                 const int er = __builtin_amdgcn_readlane(e.x, dl);
                 if (er == kRefDone) continue;
                 const int h = __ffsll(static_cast<unsigned long long>(idle)) - 1;
@@ -608,11 +640,11 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         }
         // ---- inner nodes until every active lane holds a postponed leaf ----
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
-            const float curLim = cullLimit<kCull>(fminf(bt, shT));
+            const float curLim = cullLimit<kInner>(fminf(bt, shT));
             const bool finite = __ballot(!finiteInv(inv)) == 0;
             const int order = kAny ? s.anyOrder : 0;
-            ref = refTree ? innerStep<kCull>(nodeBuf, ref, o, d, inv, curLim, st, cnt, kCount, finite, order)
-                          : innerStepQ<kCull>(qBuf, ldsTop, top, ref, qa, qb, curLim, st, cnt, kCount, order);
+            ref = refTree ? innerStep<kInner>(nodeBuf, ref, o, d, inv, curLim, st, cnt, kCount, finite, order)
+                          : innerStepQ<kInner>(qBuf, ldsTop, top, ref, qa, qb, curLim, st, cnt, kCount, order);
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
                 ref = popCulled(st, curLim, cull);
@@ -629,12 +661,28 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             if (!refTree) {
                 // a walk-tree leaf passed a quantized (outward) box: the reference's own test of
                 // its exact box, and the cull against that box's entry, decide (BVH.hpp:357-363)
-                const uint32_t lo = static_cast<uint32_t>(first) * 32u;
+                const uint32_t lo = static_cast<uint32_t>(first) * 48u;
                 const float4 b0 = bload4(leafBuf, lo);
-                const int2 b1 = bload2i(leafBuf, lo + 16u);
-                float te;
-                const bool in = slabFinite(b0.x, b0.y, b0.z, b0.w, __int_as_float(b1.x), __int_as_float(b1.y), o, inv, &te);
-                if (!in || (cull && te > cullLimit<kCull>(fminf(bt, shT)))) nprim = 0;
+                if (kCull == kCullExact) {
+                    const float4 b1 = bload4(leafBuf, lo + 16u);
+                    const float4 b2 = bload4(leafBuf, lo + 32u);
+                    float te, ex, ey, ez;
+                    if (!slabFiniteAxes(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv, &te, &ex, &ey, &ez)) {
+                        nprim = 0;
+                    } else {
+                        // certified leaf cull: the key never exceeds the entry, so only a leaf
+                        // entered beyond the best needs it; skipped iff every acceptable t of
+                        // its triangles exceeds the best (then no tie is possible either)
+                        const float lim = fminf(bt, shT);
+                        if (te > lim && leafKey(b1, b2, te, ex, ey, ez, d, inv) > lim) nprim = 0;
+                    }
+                } else {
+                    const int2 b1 = bload2i(leafBuf, lo + 16u);
+                    float te;
+                    const bool in =
+                        slabFinite(b0.x, b0.y, b0.z, b0.w, __int_as_float(b1.x), __int_as_float(b1.y), o, inv, &te);
+                    if (!in || (cull && te > cullLimit<kCull>(fminf(bt, shT)))) nprim = 0;
+                }
             }
             bool hit = false;
             for (int k = 0; k < nprim; ++k) {
@@ -674,7 +722,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             leaf = 0;
             if (ref < 0) {  // the next node is a leaf too: test it now
                 leaf = ref;
-                ref = popCulled(st, cullLimit<kCull>(fminf(bt, shT)), cull);
+                ref = popCulled(st, cullLimit<kInner>(fminf(bt, shT)), cull);
             }
         }
     }

@@ -21,7 +21,6 @@
 #include <new>
 #include <stdexcept>
 #include <string>
-#include <thread>
 #include <unistd.h>
 #include <vector>
 
@@ -74,6 +73,20 @@ jobject directFloats(JNIEnv* env, int64_t (*fill)(float*)) {
         throw std::runtime_error("JNIEnv::NewDirectByteBuffer failed to allocate native memory!");
     }
     return direct;
+}
+
+// The locked Android bitmap, released by the session's render thread once its last frame has
+// returned (mrt_android_render_into_bitmap_cb's callback): it attaches to the VM, unlocks the pixels
+// and drops the global reference, as the reference's render thread does after renderFrame
+// (JNI_layer.cpp:850-869).  Nothing writes the pixels after that point.
+void unlockBitmap(void* user) {
+    const jobject bitmap = static_cast<jobject>(user);
+    JNIEnv* tenv = nullptr;
+    if (javaVM_ != nullptr && javaVM_->AttachCurrentThread(&tenv, nullptr) == JNI_OK) {
+        AndroidBitmap_unlockPixels(tenv, bitmap);
+        tenv->DeleteGlobalRef(bitmap);
+        javaVM_->DetachCurrentThread();
+    }
 }
 
 }  // namespace
@@ -149,8 +162,8 @@ JNIEXPORT void JNICALL Java_puscas_mobilertapp_MainRenderer_rtFinishRender(JNIEn
     env->ExceptionClear();
 }
 
-// :743-901: the bitmap stays locked while the session's render thread writes it; a watcher thread
-// attached to the VM unlocks it once the session leaves BUSY
+// :743-901: the bitmap stays locked while the session's render thread writes it; the render
+// thread unlocks it (unlockBitmap) once its last frame has returned
 JNIEXPORT void JNICALL Java_puscas_mobilertapp_MainRenderer_rtRenderIntoBitmap(JNIEnv* env, jobject /*thiz*/,
                                                                                jobject localBitmap, jint nThreads) {
     guarded(env, [&] {
@@ -160,16 +173,7 @@ JNIEXPORT void JNICALL Java_puscas_mobilertapp_MainRenderer_rtRenderIntoBitmap(J
             env->DeleteGlobalRef(bitmap);
             throw std::runtime_error("Couldn't lock the Android bitmap pixels.");
         }
-        mrt_android_render_into_bitmap(static_cast<int32_t*>(pixels), nThreads);
-        std::thread([bitmap] {
-            while (mrt_android_state() == MRT_STATE_BUSY) usleep(1000);
-            JNIEnv* tenv = nullptr;
-            if (javaVM_ != nullptr && javaVM_->AttachCurrentThread(&tenv, nullptr) == JNI_OK) {
-                AndroidBitmap_unlockPixels(tenv, bitmap);
-                tenv->DeleteGlobalRef(bitmap);
-                javaVM_->DetachCurrentThread();
-            }
-        }).detach();
+        mrt_android_render_into_bitmap_cb(static_cast<int32_t*>(pixels), nThreads, unlockBitmap, bitmap);
         return 0;
     }, 0);
 }

@@ -186,6 +186,8 @@ def test_stop_and_finish_render():
     A.stop_render(True)
     assert A.state() in (A.STOPPED, A.IDLE)
     _wait_idle(A)
+    A.wait_render()
+    assert A.bitmaps_in_use() == 0  # released by the render thread after its last frame
     assert 1 <= A.sample() < 64
     assert len(np.unique(pixels)) > 1
     A.finish_render()
@@ -193,4 +195,29 @@ def test_stop_and_finish_render():
     A.start_render(True)  # finishedRendering_ is set: returns at once
     assert A.state() == A.BUSY
     A.finish_render()
+    A.reset()
+
+
+@pytest.mark.gpu
+def test_initialize_waits_for_running_render():
+    """rtInitialize while a long frame renders: the running thread is cancelled and waited for
+    before the renderer is replaced, so its bitmap is released (nothing writes it afterwards)."""
+    from mobileraytracer_amd import android as A
+    from mobileraytracer_amd import scenes
+    files = scenes.conference()
+    A.reset()
+    for p in files:
+        A.read_file(p)
+    assert A.initialize(-1, 2, 3, 320, 240, 64, 1, files[0]) > 0
+    pixels = np.zeros(320 * 240, np.int32)
+    A.start_render(True)
+    A.render_into_bitmap(pixels)
+    t0 = time.time()
+    while A.sample() < 1 and time.time() - t0 < 30:
+        time.sleep(0.001)
+    assert A.initialize(0, 1, 3, 32, 32) > 0  # built-in Cornell: no files needed
+    assert A.bitmaps_in_use() == 0
+    snapshot = pixels.copy()
+    time.sleep(0.2)
+    assert np.array_equal(snapshot, pixels)
     A.reset()

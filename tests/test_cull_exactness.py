@@ -37,14 +37,14 @@ def test_adversarial_case_is_what_it_claims(oracle_mod, adversarial):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("walk,cull", [
-    (1, 2), (0, 0), (1, 0),
+    (None, None), (1, 3), (1, 2), (0, 0), (1, 0),
     pytest.param(1, 1, marks=pytest.mark.xfail(strict=True, reason="the fast cull's known limit (DESIGN.md section 3)")),
 ])
 def test_adversarial_grazing_hit_gpu(oracle_mod, adversarial, walk, cull):
-    """GPU closest hit and shadow test of the adversarial ray equal the oracle's: the reference
-    walk, walk 1 without culling and walk 1 with the certified cull.  The fast cull (mode 1)
-    skips the tilted triangle's box and is expected to differ (strict xfail: the case stays
-    adversarial)."""
+    """GPU closest hit and shadow test of the adversarial ray equal the oracle's: the product's
+    DEFAULT settings (walk and cull untouched), the exact mode 3, the reference walk, walk 1
+    without culling and walk 1 with the certified cull.  The opt-in fast cull (mode 1) skips the
+    tilted triangle's box and is expected to differ (strict xfail: the case stays adversarial)."""
     import mobileraytracer_amd as m
     obj, mtl, cam = adversarial
     o = oracle_mod.Oracle(32, 32, 1, -1, obj=obj, mtl=mtl, cam=cam)
@@ -53,8 +53,11 @@ def test_adversarial_grazing_hit_gpu(oracle_mod, adversarial, walk, cull):
     orig = np.repeat(cc.ORIG[None], 3, 0)
     dirs = np.repeat(cc.DIR[None], 3, 0)
     with m.Renderer(cfg) as r:
-        r.set_tuning(1, walk)
-        r.set_tuning(2, cull)
+        if walk is None:
+            assert r.get_tuning(2) == 3 and r.get_tuning(1) == 1  # the defaults are the exact mode
+        else:
+            r.set_tuning(1, walk)
+            r.set_tuning(2, cull)
         got = r.trace_rays(orig, dirs)
         got_s = r.trace_rays(orig, dirs, dist=dists, any_hit=True)
     ref = o.trace_rays(orig, dirs)

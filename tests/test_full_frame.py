@@ -37,7 +37,7 @@ def c3_gpu():
     cfg = make_cfg(1920, 1080, shader=1, scene="conference")
     out = {}
     with m.Renderer(cfg) as r:
-        for cull in (1, 0, 2):
+        for cull in (1, 0, 2, 3):
             r.set_tuning(2, cull)
             bm = np.full(1920 * 1080, SENTINEL, np.int32)
             r.render_frame(bm)
@@ -50,7 +50,7 @@ def test_c3_primary_hits_full_frame(oracle_mod, c3_gpu):
     o = oracle_for(oracle_mod, cfg)
     ok, oi, ot = o.primary_hits()
     o.close()
-    k, i, t = out[1][2]
+    k, i, t = out[3][2]  # the default (exact) mode
     rendered = ok >= 0
     assert rendered.sum() == 1920 * 1072
     assert np.array_equal(k, ok) and np.array_equal(i, oi)
@@ -60,7 +60,7 @@ def test_c3_primary_hits_full_frame(oracle_mod, c3_gpu):
 
 def test_c3_whitted_bitmap_full_frame(oracle_mod, c3_gpu):
     cfg, out = c3_gpu
-    bm, st, _ = out[1]
+    bm, st, _ = out[3]
     ref, ref_rays = oracle_full(oracle_mod, cfg)
     rows = bm.reshape(1080, 1920)
     assert (rows[1072:] == SENTINEL).all()  # H / 16 = 67: rows 1072-1079 never rendered (Renderer.cpp:33-34)
@@ -71,8 +71,8 @@ def test_c3_whitted_bitmap_full_frame(oracle_mod, c3_gpu):
 
 def test_c3_cull_modes_identical_full_frame(c3_gpu):
     _, out = c3_gpu
-    base_bm, base_st, base_hits = out[1]
-    for cull in (0, 2):
+    base_bm, base_st, base_hits = out[3]
+    for cull in (0, 1, 2):
         bm, st, hits = out[cull]
         assert np.array_equal(bm, base_bm), cull
         assert (st["rays"], st["shadowRays"]) == (base_st["rays"], base_st["shadowRays"])
@@ -85,7 +85,7 @@ def c4_gpu():
     cfg = make_cfg(1920, 1080, shader=2, scene="conference", spp=4, max_depth=5)
     out = {}
     with m.Renderer(cfg) as r:
-        for cull in (1, 0, 2):
+        for cull in (1, 0, 2, 3):
             r.set_tuning(2, cull)
             bm = np.full(1920 * 1080, SENTINEL, np.int32)
             r.render_frame(bm)
@@ -95,7 +95,7 @@ def c4_gpu():
 
 def test_c4_pathtracer_full_frame(oracle_mod, c4_gpu):
     cfg, out = c4_gpu
-    bm, st = out[1]
+    bm, st = out[3]
     assert st["primaryRays"] == 4 * 1920 * 1072
     ref, ref_rays = oracle_full(oracle_mod, cfg)
     assert np.array_equal(bm, ref), int((bm != ref).sum())
@@ -104,8 +104,8 @@ def test_c4_pathtracer_full_frame(oracle_mod, c4_gpu):
 
 def test_c4_cull_modes_identical_full_frame(c4_gpu):
     _, out = c4_gpu
-    base_bm, base_st = out[1]
-    for cull in (0, 2):
+    base_bm, base_st = out[3]
+    for cull in (0, 1, 2):
         bm, st = out[cull]
         assert np.array_equal(bm, base_bm), (cull, int((bm != base_bm).sum()))
         assert (st["rays"], st["shadowRays"]) == (base_st["rays"], base_st["shadowRays"])
@@ -131,7 +131,7 @@ def test_random_rays_all_cull_modes(oracle_mod):
         o, d = random_rays(4_000_000, 7, lo, hi)
         dist = np.random.default_rng(8).random(len(o)).astype(np.float32) * np.float32(np.linalg.norm(hi - lo))
         res = {}
-        for walk, cull in ((0, 0), (1, 0), (1, 1), (1, 2)):
+        for walk, cull in ((0, 0), (1, 0), (1, 1), (1, 2), (1, 3)):
             r.set_tuning(1, walk)
             r.set_tuning(2, cull)
             res[(walk, cull)] = (r.trace_rays(o, d), r.trace_rays(o, d, dist=dist, any_hit=True)[0])
@@ -262,7 +262,7 @@ def test_quantized_walk_tree_boundary_rays(oracle_mod):
     dist = (rng.random(len(o)) * np.linalg.norm(ext) * 2).astype(np.float32)
     res = {}
     with m.Renderer(cfg) as r:
-        for walk, cull in ((0, 0), (1, 0), (1, 1), (1, 2)):
+        for walk, cull in ((0, 0), (1, 0), (1, 1), (1, 2), (1, 3)):
             r.set_tuning(1, walk)
             r.set_tuning(2, cull)
             res[(walk, cull)] = (r.trace_rays(o, d), r.trace_rays(o, d, dist=dist, any_hit=True)[0])
