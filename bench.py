@@ -61,6 +61,10 @@ def parse():
     p.add_argument("--shader", type=int, default=2)
     p.add_argument("--overlap", type=int, default=1, help="shadow rays on their own stream (timed frames)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    # rehearsals (not the headline line): rank 0's shard of an N-GPU frame on this one GPU (e.g.
+    # C5: --width 3840 --height 2160 --spp 8 --shard-of 8), and the final bitmap saved as .npy
+    p.add_argument("--shard-of", type=int, default=0)
+    p.add_argument("--dump-bitmap", default="")
     return p.parse_args()
 
 
@@ -107,14 +111,37 @@ def cpu_baseline(args, scene):
             "rays_counted": "built (every Ray constructed, Ray.cpp:25-28)"}
 
 
+def kernel_source_stamp():
+    """sha256 of the HIP sources the walk / shading kernels are built from: a PMC profile is
+    reported only while it was measured on this exact code."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(HERE, "mobileraytracer_amd", "csrc")
+    for name in sorted(os.listdir(d)):
+        if name.endswith((".hip", ".hpp")):
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
+PMC_PROFILE = os.path.join("profiles", "r03_pmc_traffic.json")
+
+
 def pmc_traffic():
     """Bytes beyond L2 per launch for each kernel from the committed rocprofv3 PMC summary
-    (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), if present."""
-    path = os.path.join(HERE, "profiles", "r02_pmc_traffic.json")
+    (tools/pmc_run.sh: FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md),
+    used only when its kernel-source stamp equals this build's (else stale: traffic null)."""
+    path = os.path.join(HERE, PMC_PROFILE)
     if not os.path.exists(path):
-        return {}
+        return {}, {"file": PMC_PROFILE, "status": "absent"}
     with open(path) as f:
-        return json.load(f).get("bytes_beyond_l2_per_launch", {})
+        j = json.load(f)
+    stamp = kernel_source_stamp()
+    if j.get("kernel_source_sha256") != stamp:
+        return {}, {"file": PMC_PROFILE, "status": "stale (measured on other kernel sources)",
+                    "profile_sha256": j.get("kernel_source_sha256"), "build_sha256": stamp}
+    return j.get("bytes_beyond_l2_per_launch", {}), {"file": PMC_PROFILE, "status": "current",
+                                                     "kernel_source_sha256": stamp}
 
 
 def kernel_roofline(r, step):
@@ -135,9 +162,14 @@ def kernel_roofline(r, step):
     r.set_tuning(3, 1)
     walked, shadows, shaded = c["walkedRays"], c["shadowRays"], c["shadedVertices"]
     # k_trace: per ray 32 (ray read: origin, direction) + 16 (hit write) + 32 per node record + 36 per
-    # triangle test; k_shadow: 32 (ray read) + 4 (flag write) + the same gathers
+    # triangle test; k_shadow: 32 (ray read) + 4 (flag write) + the same gathers (SURVEY.md 8(d))
     trace_b = 48.0 * walked + 32.0 * c["nodeRecords"] + 36.0 * c["triTests"]
     shadow_b = 36.0 * shadows + 32.0 * c["shadowNodeRecords"] + 36.0 * c["shadowTriTests"]
+    # the bytes the kernels' load instructions actually request: 16 per child record of the
+    # quantized 4-wide tree (a 64-B node holds four), 48 per walk-tree leaf record (exact box +
+    # certified-cull record), 36 per triangle test (three 12-B loads: A, AB, AC)
+    trace_f = 48.0 * walked + 16.0 * c["nodeRecords"] + 48.0 * c["leafRecords"] + 36.0 * c["triTests"]
+    shadow_f = 36.0 * shadows + 16.0 * c["shadowNodeRecords"] + 48.0 * c["shadowLeafRecords"] + 36.0 * c["shadowTriTests"]
     # k_shade: per vertex 52 read (origin, direction, hit, tree code) + 16
     # written (vertex or result record); per shaded hit 48 (normals, material id) + 64 (material)
     # + 64 (light) + 32 (the vertex's six draws, one compact block); per shadow ray 48 written;
@@ -148,18 +180,26 @@ def kernel_roofline(r, step):
     shade_b = 68.0 * shaded_rays + 208.0 * shaded + 48.0 * shadows + 36.0 * children
     fr = max(1, 2)
 
-    def entry(name, frame_bytes, ms, launches):
+    def entry(name, frame_bytes, ms, launches, fetched_bytes=None):
         launches_pf = launches / fr
         per_launch = frame_bytes / max(1.0, launches_pf)
         avg_ms = ms / max(1, launches)
         ach = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        return {"algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches_per_frame": launches_pf,
-                "achieved": ach, "peak": PEAK_VMEM_GBS, "unit": "GB/s", "frac": ach / PEAK_VMEM_GBS}
+        e = {"algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches_per_frame": launches_pf,
+             "achieved": ach, "peak": PEAK_VMEM_GBS, "unit": "GB/s", "frac": ach / PEAK_VMEM_GBS}
+        if fetched_bytes is not None:
+            f = fetched_bytes / max(1.0, launches_pf)
+            fa = f / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+            e.update({"fetched_bytes_per_launch": f, "achieved_fetched": fa, "frac_fetched": fa / PEAK_VMEM_GBS})
+        return e
 
     per_ray = {"nodes": c["nodeRecords"] / max(1, walked), "tris": c["triTests"] / max(1, walked),
+               "leaves": c["leafRecords"] / max(1, walked),
                "shadow_nodes": c["shadowNodeRecords"] / max(1, shadows),
-               "shadow_tris": c["shadowTriTests"] / max(1, shadows), "shaded_vertices": shaded}
-    return {"k_trace": entry("k_trace", trace_b, tr_ms, tr_n), "k_shadow": entry("k_shadow", shadow_b, sh_ms, sh_n),
+               "shadow_tris": c["shadowTriTests"] / max(1, shadows),
+               "shadow_leaves": c["shadowLeafRecords"] / max(1, shadows), "shaded_vertices": shaded}
+    return {"k_trace": entry("k_trace", trace_b, tr_ms, tr_n, trace_f),
+            "k_shadow": entry("k_shadow", shadow_b, sh_ms, sh_n, shadow_f),
             "k_shade": entry("k_shade", shade_b, sd_ms, sd_n)}, per_ray
 
 
@@ -186,10 +226,11 @@ def main():
     else:
         torch.cuda.set_device(0)
     scene = scenes.conference()
+    shard_of = args.shard_of if (args.shard_of > 1 and not dist_on) else 0
     cfg = m.Config(width=args.width, height=args.height, shader=args.shader, sceneIndex=-1,
                    samplesPixel=args.spp, samplesLight=1, maxDepth=args.max_depth, objFilePath=scene[0],
-                   mtlFilePath=scene[1], camFilePath=scene[2], rankIndex=rank, rankCount=world,
-                   device=torch.cuda.current_device())
+                   mtlFilePath=scene[1], camFilePath=scene[2], rankIndex=rank,
+                   rankCount=shard_of if shard_of else world, device=torch.cuda.current_device())
     # the renderer (and its two HIP streams) before the process group, so that RCCL's streams
     # take the later hardware queues
     r = m.Renderer(cfg)
@@ -208,7 +249,9 @@ def main():
     gathered = torch.zeros((world, slots_max), dtype=torch.int32, device="cuda") if rank == 0 else None
 
     def step():
-        if not dist_on:
+        if shard_of:
+            r.render_frame_device(0, packed.data_ptr(), sh)
+        elif not dist_on:
             r.render_frame_device(bitmap.data_ptr(), 0, sh)
         else:
             r.render_frame_device(0, packed.data_ptr(), sh)
@@ -244,6 +287,22 @@ def main():
     elapsed = time.perf_counter() - t0
     rays = r.get_total_casted_rays() - rays0
 
+    # BASELINE.md section 2's timed window ends with the bitmap in host memory: a second, shorter
+    # timed loop adds the D2H copy of the frame into pinned host memory to every frame
+    host_bm = torch.empty(bitmap.numel(), dtype=torch.int32, pin_memory=True) if rank == 0 else None
+    if dist_on:
+        dist.barrier()
+    k2 = max(1, min(args.steps, 10))
+    t2 = time.perf_counter()
+    for _ in range(k2):
+        step()
+        if rank == 0:
+            host_bm.copy_(bitmap, non_blocking=True)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    d2h_ms = (time.perf_counter() - t2) / k2 * 1e3
+
     if dist_on:
         red = "cpu" if backend == "gloo" else "cuda"
         t = torch.tensor([elapsed], dtype=torch.float64, device=red)
@@ -258,7 +317,7 @@ def main():
         return
 
     frames = max(1, args.steps)
-    traffic = pmc_traffic() if world == 1 else {}
+    traffic, traffic_src = pmc_traffic() if world == 1 else ({}, {"status": "not collected for N > 1"})
     for name, e in kernels.items():
         tb = traffic.get(name)
         e["traffic"] = tb
@@ -272,6 +331,10 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / frames * 1e3,
+        # the same frames with the bitmap copied to pinned host memory after each (the reference's
+        # timed window includes it); `value` excludes it
+        "ms_per_step_with_d2h": d2h_ms,
+        "value_with_d2h": (walked / frames) / (d2h_ms * 1e-3) / 1e6 if d2h_ms else None,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -287,7 +350,8 @@ def main():
             "spp": args.spp, "max_depth": args.max_depth, "samples_light": 1,
             "shader": "PathTracer" if args.shader == 2 else "Whitted",
             "parallelism": (f"screen-tile shard x{world} + " + ("RCCL gather" if backend == "nccl" else "gloo gather (rehearsal)"))
-            if dist_on else "single GPU",
+            if dist_on else (f"rank 0's shard of a {shard_of}-GPU frame, on one GPU (rehearsal)" if shard_of
+                             else "single GPU"),
             "rays_walked_per_frame": walked / frames,
             "rays_built_per_frame": rays / frames,
             "mrays_per_s_built": rays / elapsed / 1e6,
@@ -305,6 +369,11 @@ def main():
             "unit": "GB/s",
             "frac": dom["frac"],
             "traffic": dom["traffic"],
+            "traffic_source": traffic_src,
+            # the same launch priced at the bytes its loads request (16 B per quantized child record,
+            # 48 B per leaf record, 36 B per triangle test) instead of SURVEY 8(d)'s 32 B per record
+            "frac_fetched": dom["frac_fetched"],
+            "achieved_fetched": dom["achieved_fetched"],
             "avg_launch_ms": dom["avg_launch_ms"],
             "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
             "per_ray": per_ray,
@@ -319,9 +388,12 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not shard_of and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, scene)
     print(json.dumps(out), flush=True)
+    if args.dump_bitmap:
+        import numpy as np
+        np.save(args.dump_bitmap, bitmap.cpu().numpy())
     r.close()
     if dist_on:
         dist.destroy_process_group()

@@ -108,6 +108,9 @@ typedef struct mrt_frame_stats {
     uint64_t shadedVertices;       /* counting pass only: hits k_shade shaded (not emissive, under the
                                       depth cap) */
     int64_t shadeLaunches;         /* k_shade launches of the frame */
+    uint64_t leafRecords;          /* counting pass only: walk-tree leaf records (exact leaf boxes)
+                                      fetched by closest-hit rays */
+    uint64_t shadowLeafRecords;    /* ... and by shadow rays */
 } mrt_frame_stats;
 
 /* A named byte buffer (a map_Kd texture file handed over by the Android front end). */
@@ -159,18 +162,14 @@ int64_t mrt_wave_log(mrt_renderer *r, uint64_t *out);
  *         1 persistent while-while walk (default),
  * key 2 = cull mode of walk 1: 0 none, 1 fast (inexact), 2 certified, 3 exact (mrt_config.cull),
  * key 3 = shadow rays on the same stream (0) or their own stream (1, default),
- * key 4 = binned emission of child / shadow rays (0 default, 1),
  * key 5 = shadow walk child order: 0 near first, 1 far first (default),
  * key 6 = shadow walk grid, percent of its occupancy grid (1-100; 0 default: 50-75 by paths per walk lane),
  * key 7 = skip the closest-hit walk of the depth-capped last level (1, default),
  * key 8 = tail donation: idle lanes of a level's tail walk subtrees of their wave's rays (0, 1 default),
  * key 9 = idle lanes before a walk wave fetches new rays (1-64, default 32),
  * key 10 = k_shade's lean instantiation where it applies (1, default) or always the general one (0),
- * key 11 = k_shade workgroups per CU (-1 default: 14 below 4 paths per walk lane, else 28; 0: 8),
- * key 12 = sort queues before their walk (0 default, 1 shadow, 2 closest hit, 3 both),
- * key 13 / 14 = sort key of shadow / closest-hit queues,
- * key 15 = replay a one-chunk pass from a captured HIP graph (1) or launch it (0, default;
- *          the replay measured slower) */
+ * key 11 = k_shade workgroups per CU (-1 default: 14 below 4 paths per walk lane, else 28; 0: 8).
+ * (Keys 4, 12-15 - binned emission, queue sorting, graph replay - measured slower and were removed.) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /

@@ -114,9 +114,9 @@ class Renderer:
         _native.check(self._lib.mrt_set_profiling(self._h, int(timing) | (2 * int(counting))))
 
     def set_tuning(self, key: int, value: int) -> None:
-        """A/B knobs (identical results): 1 = trace walk (0 reference, 1 default), 2 = t-cull mode
-        (0 none, 1 fast, 2 certified), 3 = shadow rays on their own stream, 4 = binned emission
-        of child / shadow rays, 5 = shadow-walk child order (0 near first, 1 far first),
+        """A/B knobs: 1 = trace walk (0 reference, 1 default), 2 = t-cull mode (0 none, 1 fast -
+        inexact on grazing inputs, 2 certified, 3 exact: the default), 3 = shadow rays on their own
+        stream, 5 = shadow-walk child order (0 near first, 1 far first),
         6 = shadow-walk grid percent (0 auto), 7 = no walk for the depth-capped last level, 8 = tail
         donation (idle lanes of a level's tail walk subtrees of their wave's rays), 9 = refill
         threshold of the walk waves, 10 = lean k_shade instantiation, 11 = k_shade workgroups per CU."""

@@ -70,6 +70,7 @@ class MrtFrameStats(ctypes.Structure):
         ("levelTraceMs", ctypes.c_double * 16), ("levelShadowMs", ctypes.c_double * 16),
         ("maxNodeRecordsPerRay", ctypes.c_uint64),
         ("walkedRays", ctypes.c_uint64), ("shadedVertices", ctypes.c_uint64), ("shadeLaunches", ctypes.c_int64),
+        ("leafRecords", ctypes.c_uint64), ("shadowLeafRecords", ctypes.c_uint64),
     ]
 
 

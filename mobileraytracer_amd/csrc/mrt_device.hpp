@@ -282,6 +282,7 @@ __device__ __forceinline__ bool leafSpheres(const DScene& s, int first, int coun
 struct TravCount {
     uint32_t nodes;  // child records fetched (2 per inner visit)
     uint32_t tris;   // triangle tests
+    uint32_t leaves = 0;    // leaf records fetched (the walk tree's exact leaf boxes)
     uint32_t rayStart = 0;  // nodes at the current ray's fetch (per-ray maximum, counting builds)
     uint32_t rayMax = 0;
     uint32_t rays = 0;      // rays this lane fetched (the wave log of counting builds)

@@ -86,97 +86,6 @@ __device__ __forceinline__ void blockAllocPair(unsigned long long* pair, int nLo
     *baseHi = static_cast<int>(static_cast<unsigned>(e >> 32));
 }
 
-// Binned form of blockAllocPair: the block's slots stay ONE contiguous range per counter (one
-// 64-bit atomic per block), laid out bin-major, so rays with equal keys land next to each other
-// and a wave of the next launch walks rays of one direction octant from one patch of parents
-// (the north_star "sorting with ballot / prefix-sum", staged per block).
-//   lo: nLo in [0, 3] slots under key keyLo; hi: nHi in [0, 2^hiBits) slots under key keyHi;
-//   keys in [0, kEmitBins).  A lane's rank inside its (wave, bin) is a sum of ballot popcounts
-//   over the bits of its count; wave 0 scans the (bin, wave) totals.
-// lds: 2 x (2 * kWaves * kEmitBins + 2) ints, alternated by parity.
-__device__ __forceinline__ void blockAllocBinned(unsigned long long* pair, int nLo, int keyLo, int nHi, int keyHi,
-                                                 int hiBits, int* baseLo, int* baseHi, int* lds, int parity) {
-    constexpr int kWaves = kBlock / 64;
-    constexpr int kB = kEmitBins;
-    const int lane = laneId();
-    const int wave = static_cast<int>(threadIdx.x >> 6);
-    const uint64_t below = (1ull << lane) - 1ull;
-    int rankLo = 0, rankHi = 0, totLo = 0, totHi = 0;
-#pragma unroll
-    for (int b = 0; b < kB; ++b) {
-        const bool inLo = keyLo == b, inHi = keyHi == b;
-        const uint64_t l0 = __ballot(inLo && (nLo & 1) != 0);
-        const uint64_t l1 = __ballot(inLo && (nLo & 2) != 0);
-        const int rl = __popcll(l0 & below) + 2 * __popcll(l1 & below);
-        const int tl = __popcll(l0) + 2 * __popcll(l1);
-        int rh = 0, th = 0;
-        for (int k = 0; k < hiBits; ++k) {
-            const uint64_t m = __ballot(inHi && ((nHi >> k) & 1) != 0);
-            rh += __popcll(m & below) << k;
-            th += __popcll(m) << k;
-        }
-        if (inLo) rankLo = rl;
-        if (inHi) rankHi = rh;
-        if (lane == b) {
-            totLo = tl;
-            totHi = th;
-        }
-    }
-    int* buf = lds + parity * (2 * kWaves * kB + 2);
-    int* cLo = buf;                 // [wave][bin] -> count, then the exclusive offset in the block
-    int* cHi = buf + kWaves * kB;
-    if (lane < kB) {
-        cLo[wave * kB + lane] = totLo;
-        cHi[wave * kB + lane] = totHi;
-    }
-    __syncthreads();
-    if (wave == 0) {
-        // lane b < kB: bin b's total over the waves, scanned over the bins
-        unsigned long long v = 0;
-        int pl[kWaves], ph[kWaves];
-        if (lane < kB) {
-            int sl = 0, sh = 0;
-#pragma unroll
-            for (int w = 0; w < kWaves; ++w) {
-                pl[w] = sl;
-                ph[w] = sh;
-                sl += cLo[w * kB + lane];
-                sh += cHi[w * kB + lane];
-            }
-            v = (static_cast<unsigned long long>(static_cast<unsigned>(sh)) << 32) | static_cast<unsigned>(sl);
-        }
-        unsigned long long x = v;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const unsigned long long y = __shfl_up(x, off, 64);
-            if (lane >= off) x += y;
-        }
-        const unsigned long long sum = __shfl(x, 63, 64);
-        unsigned long long base = 0;
-        if (lane == 0 && sum != 0) base = atomicAdd(pair, sum);
-        base = __shfl(base, 0, 64);
-        if (lane < kB) {
-            const unsigned long long e = base + (x - v);  // bin start (both halves; no carry: counts < 2^31)
-            const int el = static_cast<int>(static_cast<unsigned>(e & 0xFFFFFFFFull));
-            const int eh = static_cast<int>(static_cast<unsigned>(e >> 32));
-#pragma unroll
-            for (int w = 0; w < kWaves; ++w) {
-                cLo[w * kB + lane] = el + pl[w];
-                cHi[w * kB + lane] = eh + ph[w];
-            }
-        }
-    }
-    __syncthreads();
-    *baseLo = cLo[wave * kB + keyLo] + rankLo;
-    *baseHi = cHi[wave * kB + keyHi] + rankHi;
-}
-
-// emission keys (binMode 1): a child run by its first ray's direction octant and lobe, shadow
-// rays by the light of their first sample
-__device__ __forceinline__ int octantKey(v3 d, bool specular) {
-    return (d.x < 0.0F ? 1 : 0) | (d.y < 0.0F ? 2 : 0) | (d.z < 0.0F ? 4 : 0) | (specular ? 8 : 0);
-}
-
 // ---------------------------------------------------------------------------------------
 // pixel mapping: path p -> (pixel slot, sample); slot -> (x, y) through the unit table
 __device__ __forceinline__ void slotToXY(const PixelMap& m, int slot, int* x, int* y) {
@@ -249,15 +158,17 @@ constexpr int kWalkThreads = 256;
 
 template <bool kCount>
 __device__ __forceinline__ void reduceCounts(const TravCount& cnt, unsigned long long* stats, int nodesStat,
-                                             int trisStat) {
-    unsigned long long n = cnt.nodes, t = cnt.tris;
+                                             int trisStat, int leavesStat) {
+    unsigned long long n = cnt.nodes, t = cnt.tris, l = cnt.leaves;
     for (int off = 32; off > 0; off >>= 1) {
         n += __shfl_down(n, off, 64);
         t += __shfl_down(t, off, 64);
+        l += __shfl_down(l, off, 64);
     }
     if (laneId() == 0) {
         atomicAdd(stats + nodesStat, n);
         atomicAdd(stats + trisStat, t);
+        atomicAdd(stats + leavesStat, l);
     }
 }
 
@@ -293,8 +204,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, i
         __shared__ QNode4 ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, tailBest,
-                                              lv.rPerm);
+        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, tailBest);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -310,7 +220,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, i
         }
     }
     if (kCount) {
-        reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris);
+        reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris, kStatLeaves);
         atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
         waveLog(cnt, stats, 0, level, t0);
     }
@@ -330,8 +240,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, 
         __shared__ QNode4 ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest,
-                                             lv.sPerm);
+        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -347,7 +256,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, 
         }
     }
     if (kCount) {
-        reduceCounts<kCount>(cnt, stats, kStatNodesShadow, kStatTrisShadow);
+        reduceCounts<kCount>(cnt, stats, kStatNodesShadow, kStatTrisShadow, kStatLeavesShadow);
         waveLog(cnt, stats, 1, level, t0);
     }
 }
@@ -523,7 +432,6 @@ struct ShadeState {
     v3 ld0, lc0;  // light sample 0 (kept in registers)
     float dist0, hcos, hsin, hemi2;
     int nShadow, nChild;
-    int light0;  // the light chosen by sample 0 (emission key of the shadow rays)
     v3 dir0;     // direction of the first child (computed before the slots are allocated)
 };
 
@@ -576,7 +484,6 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     v.direct = hasPositive(Kd) && s.nLights > 0;
     if (v.direct) {
         v.ok0 = lightSample(s, v.g, pick0, lr0, lq0, &v.ld0, &v.dist0, &v.lc0);
-        v.light0 = static_cast<int>(lightChoice(s, pick0));
         v.nShadow = static_cast<int>(v.ok0);
         for (int k = 1; k < a.samplesLight; ++k) {
             v3 ld, lc;
@@ -664,7 +571,7 @@ __device__ __forceinline__ v3 firstChildDir(const ShadeState& v) {
     return refract(v.d, v.g.N, 1.0F / v.ior);
 }
 
-// kFull: the general kernel (textures, binned emission, counting); the lean instantiation (no
+// kFull: the general kernel (textures, counting); the lean instantiation (no
 // texture, compaction only, no statistics) needs fewer registers: 65 VGPRs instead of 103, so
 // 7 waves per SIMD instead of 4
 template <int kShader, bool kFull>
@@ -675,7 +582,6 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
     auto* pair = reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1));
     static_assert(cntShadows(1) == cntRays(2) + 1, "pair layout");
     __shared__ unsigned long long allocLds[2 * (kBlock / 64 + 1)];
-    __shared__ int binLds[2 * (2 * (kBlock / 64) * kEmitBins + 2)];
     const bool dead = deadNext != 0;
     int parity = 0;
     for (int base = static_cast<int>(blockIdx.x * blockDim.x); base < count;
@@ -696,13 +602,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
         }
         int childBase, shadowBase;
         const int nC = active ? v.nChild : 0, nS = active ? v.nShadow : 0;
-        if (kFull && a.binMode == 1 && !dead) {
-            const int cKey = nC > 0 ? octantKey(v.dir0, !v.wantD) : 0;
-            const int sKey = nS > 0 ? (v.light0 & (kEmitBins - 1)) : 0;
-            blockAllocBinned(pair, nC, cKey, nS, sKey, a.shadowBits, &childBase, &shadowBase, binLds, parity);
-        } else {
-            blockAllocPair(pair, nC, nS, &childBase, &shadowBase, allocLds, parity);
-        }
+        blockAllocPair(pair, nC, nS, &childBase, &shadowBase, allocLds, parity);
         parity ^= 1;
         if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, dead);
         if (kFull && a.stats != nullptr) {  // counting pass: shaded (non-terminal) vertices
@@ -992,100 +892,6 @@ void launchLoadRays(const Level& lv, const float* orig, const float* dir, const 
 }
 
 // ---------------------------------------------------------------------------------------
-// Ray sorting (tuning key 12): a counting sort of one queue by a spatial key.  Rays that start
-// close together (and, keyMode 1, point into the same octant) become neighbours in the walk's
-// queue order, so a wave's refill fetches rays that share the upper part of their walk.  Only
-// the order of the walk changes, never a ray's result.
-__device__ __forceinline__ uint32_t sortKey(const DScene& s, float4 o4, float4 d4, int mode) {
-    const int bits = mode == 0 ? 4 : 3;
-    const float cells = static_cast<float>(1 << bits);
-    const float o[3] = {o4.x, o4.y, o4.z};
-    uint32_t q[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float ext = s.triRoot.bmax[a] - s.triRoot.bmin[a];
-        const float f = ext > 0.0F ? (o[a] - s.triRoot.bmin[a]) / ext * cells : 0.0F;
-        q[a] = f >= 1.0F ? static_cast<uint32_t>(fminf(f, cells - 1.0F)) : 0u;  // NaN, < 1: cell 0
-    }
-    uint32_t m = 0;
-    for (int b = 0; b < bits; ++b)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) m |= ((q[a] >> b) & 1u) << (3 * b + a);
-    if (mode == 1) m |= static_cast<uint32_t>((d4.x < 0.0F ? 1 : 0) | (d4.y < 0.0F ? 2 : 0) | (d4.z < 0.0F ? 4 : 0)) << 9;
-    return m;
-}
-
-__device__ __forceinline__ int sortCount(const Level& lv, const int* counters, int level, bool shadow) {
-    return shadow ? min(counters[cntShadows(level)], lv.shadowCap) : min(counters[cntRays(level)], lv.cap);
-}
-
-// pass 1: keys, the block's histogram in LDS, and the block's offset inside each bin
-__global__ __launch_bounds__(kSortThreads) void k_sort_keys(DScene s, Level lv, const int* counters, int level,
-                                                            int shadow, int mode, SortBufs b) {
-    __shared__ int h[kSortBins];
-    for (int i = static_cast<int>(threadIdx.x); i < kSortBins; i += kSortThreads) h[i] = 0;
-    __syncthreads();
-    const int count = sortCount(lv, counters, level, shadow != 0);
-    const float4* O = shadow != 0 ? lv.sO : lv.rO;
-    const float4* D = shadow != 0 ? lv.sD : lv.rD;
-    const int lo = static_cast<int>(static_cast<long long>(count) * blockIdx.x / gridDim.x);
-    const int hi = static_cast<int>(static_cast<long long>(count) * (blockIdx.x + 1) / gridDim.x);
-    for (int i = lo + static_cast<int>(threadIdx.x); i < hi; i += kSortThreads) {
-        const uint32_t k = sortKey(s, O[i], D[i], mode);
-        b.keys[i] = static_cast<uint16_t>(k);
-        atomicAdd(&h[k], 1);
-    }
-    __syncthreads();
-    int* off = b.blockOff + static_cast<size_t>(blockIdx.x) * kSortBins;
-    for (int k = static_cast<int>(threadIdx.x); k < kSortBins; k += kSortThreads) {
-        const int c = h[k];
-        off[k] = c > 0 ? atomicAdd(b.hist + k, c) : 0;
-    }
-}
-
-// pass 2 (one block): bin starts; clears the histogram for the next sort
-__global__ __launch_bounds__(kSortThreads) void k_sort_scan(SortBufs b) {
-    constexpr int kPer = kSortBins / kSortThreads;
-    __shared__ int waveSum[kSortThreads / 64];
-    const int t = static_cast<int>(threadIdx.x);
-    int v[kPer], sum = 0;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        v[j] = b.hist[t * kPer + j];
-        b.hist[t * kPer + j] = 0;
-        sum += v[j];
-    }
-    int total;
-    const int excl = waveExclusiveScan(sum, &total);
-    if (laneId() == 0) waveSum[t >> 6] = total;
-    __syncthreads();
-    int base = 0;
-    for (int w = 0; w < (t >> 6); ++w) base += waveSum[w];
-    int run = base + excl;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        b.start[t * kPer + j] = run;
-        run += v[j];
-    }
-}
-
-// pass 3: every ray's position; perm[position] = ray (order inside a bin is arbitrary)
-__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Level lv, const int* counters, int level, int shadow,
-                                                               SortBufs b) {
-    __shared__ int cur[kSortBins];
-    const int* off = b.blockOff + static_cast<size_t>(blockIdx.x) * kSortBins;
-    for (int k = static_cast<int>(threadIdx.x); k < kSortBins; k += kSortThreads) cur[k] = b.start[k] + off[k];
-    __syncthreads();
-    const int count = sortCount(lv, counters, level, shadow != 0);
-    const int lo = static_cast<int>(static_cast<long long>(count) * blockIdx.x / gridDim.x);
-    const int hi = static_cast<int>(static_cast<long long>(count) * (blockIdx.x + 1) / gridDim.x);
-    for (int i = lo + static_cast<int>(threadIdx.x); i < hi; i += kSortThreads) {
-        const int pos = atomicAdd(&cur[b.keys[i]], 1);
-        b.perm[pos] = i;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
 // launch wrappers
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st) {
     const int blocks = (a.nPaths + 255) / 256;
@@ -1150,7 +956,7 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st, bool deadNext) {
     const int dead = deadNext ? 1 : 0;
-    const bool full = s.textured != 0 || a.binMode != 0 || a.stats != nullptr || s.leanShade == 0;
+    const bool full = s.textured != 0 || a.stats != nullptr || s.leanShade == 0;
     switch (shader) {
         case kShaderWhitted:
             if (full)
@@ -1174,14 +980,6 @@ void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, 
             hipLaunchKernelGGL(k_shade_simple<kShaderNoShadows>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, a);
             break;
     }
-}
-
-void launchSort(const DScene& s, const Level& lv, int* counters, int level, bool shadow, int keyMode,
-                const SortBufs& b, hipStream_t st) {
-    const int sh = shadow ? 1 : 0;
-    hipLaunchKernelGGL(k_sort_keys, dim3(kSortBlocks), dim3(kSortThreads), 0, st, s, lv, counters, level, sh, keyMode, b);
-    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kSortThreads), 0, st, b);
-    hipLaunchKernelGGL(k_sort_scatter, dim3(kSortBlocks), dim3(kSortThreads), 0, st, lv, counters, level, sh, b);
 }
 
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,

@@ -44,7 +44,9 @@ constexpr int kStatMaxNodesRay = 8 + 2 * kMaxLevels;  // counting builds: most n
 constexpr int kStatSkipped = kStatMaxNodesRay + 1;   // rays of a last level whose walk was skipped
 constexpr int kStatShaded = kStatSkipped + 1;        // counting pass: vertices k_shade shaded (hit, not emissive, not capped)
 constexpr int kStatShadeLaunches = kStatShaded + 1;  // k_shade launches of the frame
-constexpr int kNumStats = kStatShadeLaunches + 1;
+constexpr int kStatLeaves = kStatShadeLaunches + 1;  // counting pass: leaf records fetched, closest hit
+constexpr int kStatLeavesShadow = kStatLeaves + 1;   // ... and any hit
+constexpr int kNumStats = kStatLeavesShadow + 1;
 // counting builds: per walk launch (closest / any-hit x level) and wave {start, end (100 MHz
 // ticks), rays fetched, child records fetched}, after the statistics (mrt_wave_log)
 constexpr int kWaveLogWaves = 8192;
@@ -67,10 +69,6 @@ struct Level {
     // material index, -1 none), and the last such write in the vertex's subtree (Shader.cpp:112-120)
     float4* kd;
     float4* last;
-    // ray sorting (tuning key 12, never changes results): queue position q of the closest-hit /
-    // shadow walk takes ray rPerm[q] / sPerm[q] (null: ray q)
-    const int* rPerm;
-    const int* sPerm;
     int cap;
     int shadowCap;
 };
@@ -103,13 +101,7 @@ struct ShadeArgs {
     int samplesLight;  // Config::samplesLight
     float maxPoint[3]; // DepthMap::maxPoint_ (C_wrapper.cpp:79-131 maxDist)
     unsigned long long* stats;  // counting pass only (else null): kStatShaded
-    // emission order of child and shadow rays inside a k_shade block (tuning key 4, never changes
-    // results): 0 compaction only (parent order), 1 binned - children by direction octant and
-    // lobe (diffuse / specular+transmission), shadow rays by light - with ballot multi-scans
-    int binMode;
-    int shadowBits;  // bits of the largest shadow-ray count of a vertex (samplesLight)
 };
-constexpr int kEmitBins = 16;
 
 struct AccumArgs {
     PixelMap map;
@@ -121,23 +113,6 @@ struct AccumArgs {
     int pad;
 };
 
-// Ray sorting (tuning key 12): a counting sort of a level's closest-hit or shadow queue by a
-// spatial key into a permutation the walk reads its rays through (rPerm / sPerm).  Buffers of
-// one stream: keys and perm (queue capacity), hist / start (kSortBins), blockOff (kSortBlocks x
-// kSortBins).  keyMode 0: Morton code of the origin (4 bits per axis); 1: direction octant +
-// origin Morton (3 bits per axis).
-constexpr int kSortBins = 4096;
-constexpr int kSortBlocks = 256;
-constexpr int kSortThreads = 1024;
-struct SortBufs {
-    uint16_t* keys;
-    int* perm;
-    int* hist;   // zero between sorts (the scan clears it)
-    int* start;
-    int* blockOff;
-};
-void launchSort(const DScene& s, const Level& lv, int* counters, int level, bool shadow, int keyMode,
-                const SortBufs& b, hipStream_t st);
 
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,

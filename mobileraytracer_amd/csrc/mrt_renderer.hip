@@ -121,7 +121,6 @@ struct mrt_renderer {
         std::vector<hipEvent_t> syncPool;    // ordering events between the streams
         std::vector<hipEvent_t> evPool;      // profiling: 5 timing events per level and chunk
         size_t evCount = 0;
-        mrt::SortBufs sortR{}, sortS{};      // ray sorting (tuning key 12): closest-hit / shadow stream
     } pipe;
     int chunkSlots = 0;
     int gdepth = 0;
@@ -135,33 +134,10 @@ struct mrt_renderer {
     hipStream_t stream = nullptr;
     int overlap = 1;                     // tuning key 3: shadow rays on their own stream
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
-    int binMode = 0;                     // tuning key 4: binned emission of child / shadow rays (ShadeArgs::binMode)
     int shadowGridPct = 0;               // tuning key 6: shadow walk grid, percent of its occupancy grid (0 auto)
     int refill = 0;                      // tuning key 9: walk refill threshold (0 auto: by paths per lane)
-    int sortMode = 0;                    // tuning key 12: sort queues before their walk (1 shadow, 2 closest hit of levels >= 2)
-    int sortKeyShadow = 0;               // tuning key 13: sort key of shadow queues (launchSort keyMode)
-    int sortKeyRay = 1;                  // tuning key 14: sort key of closest-hit queues
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
-    // tuning key 15: a pass's launches (raygen, every level's walk / shading / shadow walk on both
-    // streams, resolves, accumulate, tally) replayed from a captured HIP graph: one submission per
-    // frame instead of ~25 launches, cross-stream event waits and the host's launch latency.
-    // Measured slower on MI355X (C4 13.87 vs 13.58 ms, N = 8 shard 2.80 vs 2.58 ms; identical
-    // images): the replayed graph loses part of the two streams' overlap.  Off by default.
-    struct GraphKey {
-        int32_t* bitmap;
-        int32_t* packed;
-        int sampleBase, spp;
-        uint64_t gen;
-        bool operator==(const GraphKey& o) const {
-            return bitmap == o.bitmap && packed == o.packed && sampleBase == o.sampleBase && spp == o.spp && gen == o.gen;
-        }
-    };
-    int useGraph = 0;
-    uint64_t graphGen = 1;              // bumped by whatever changes the captured launches
-    GraphKey graphKey{}, graphSeen{};   // the captured pass; the last pass run directly
-    hipGraphExec_t graphExec = nullptr;
-    hipEvent_t graphIn = nullptr, graphOut = nullptr;
     unsigned long long* hostStats = nullptr;  // pinned: the per-pass statistics read back by DMA
 
     // host copies for the GL preview of the Android front end (mrt_preview_arrays; kept only for
@@ -178,10 +154,7 @@ struct mrt_renderer {
     mrt_frame_stats last{};
 
     ~mrt_renderer() {
-        if (graphExec != nullptr) (void)hipGraphExecDestroy(graphExec);
         if (hostStats != nullptr) (void)hipHostFree(hostStats);
-        if (graphIn != nullptr) (void)hipEventDestroy(graphIn);
-        if (graphOut != nullptr) (void)hipEventDestroy(graphOut);
         for (hipEvent_t e : pipe.evPool) (void)hipEventDestroy(e);
         for (hipEvent_t e : pipe.syncPool) (void)hipEventDestroy(e);
         if (pipe.shadowStream != nullptr) (void)hipStreamDestroy(pipe.shadowStream);
@@ -479,7 +452,6 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
 void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     using namespace mrt;
     r->queueMem.release();
-    ++r->graphGen;
     const int spp = std::max(1, r->cfg.samplesPixel);
     const int spl = std::max(1, r->cfg.samplesLight);
     r->chunkSlots = chunkSlots;
@@ -515,30 +487,10 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
         lv.kd = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
         lv.last = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
     }
-    pp.sortR = SortBufs{};  // allocated on first use (ensureSortBufs)
-    pp.sortS = SortBufs{};
     pp.counters = r->queueMem.alloc<int>(kNumCounters);
     pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats + kWaveLogEntries);
     pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
     pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
-}
-
-// Sort buffers of both streams, sized for the largest queue of the current allocation.
-void ensureSortBufs(mrt_renderer* r, hipStream_t st) {
-    using namespace mrt;
-    mrt_renderer::Pipe& pp = r->pipe;
-    if (pp.sortR.keys != nullptr) return;
-    size_t n = 1;
-    for (int l = 1; l <= r->nLevels && l < kMaxLevels; ++l)
-        n = std::max({n, static_cast<size_t>(pp.levels[l].cap), static_cast<size_t>(pp.levels[l].shadowCap)});
-    for (SortBufs* b : {&pp.sortR, &pp.sortS}) {
-        b->keys = r->queueMem.alloc<uint16_t>(n);
-        b->perm = r->queueMem.alloc<int>(n);
-        b->hist = r->queueMem.alloc<int>(kSortBins);
-        b->start = r->queueMem.alloc<int>(kSortBins);
-        b->blockOff = r->queueMem.alloc<int>(static_cast<size_t>(kSortBlocks) * kSortBins);
-        MRT_HIP(hipMemsetAsync(b->hist, 0, sizeof(int) * kSortBins, st));
-    }
 }
 
 // Chunk size: every slot of the shard in one pass, within the path budget.
@@ -575,10 +527,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     const bool counting = (r->profileFlags & 2) != 0;
     mrt_renderer::Pipe& pp = r->pipe;
     const int spl = std::max(1, r->cfg.samplesLight);
-    int splBits = 0;
-    while ((spl >> splBits) != 0) ++splBits;
-    ShadeArgs sa{r->maxDepth, spl, {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z}, counting ? pp.stats : nullptr,
-                 r->binMode, splBits};
+    ShadeArgs sa{r->maxDepth, spl, {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z}, counting ? pp.stats : nullptr};
     const int nLevels = r->nLevels;
     const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
     MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * (kNumStats + (counting ? kWaveLogEntries : 0)), st));
@@ -602,9 +551,6 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     // every material is finite (Ks * 0 and Kd * 0 added to sums that start at +0), and the
     // parents write no payload for them (only their count)
     const bool skipLastShade = skipLast && nLevels >= 2 && r->ds.matsFinite != 0;
-    // ray sorting applies to the while-while BVH walk (the only one that reads the permutation)
-    const int sortMode = r->ds.accel == kAccBVH && r->ds.variant == 1 ? r->sortMode : 0;
-    if (sortMode != 0) ensureSortBufs(r, st);  // the shadow stream waits on st before its first launch
     for (int slot0 = 0; slot0 < r->nSlots && !r->stopFlag.load(); slot0 += r->chunkSlots) {
         const int nChunk = std::min(r->chunkSlots, r->nSlots - slot0);
         MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
@@ -651,14 +597,9 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         }
         for (int l = 1; l <= nLevels; ++l) {
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-            if (!(skipLast && l == nLevels)) {
-                Level lt = pp.levels[l];
-                if ((sortMode & 2) != 0 && l >= 2) {
-                    launchSort(r->ds, lt, pp.counters, l, false, r->sortKeyRay, pp.sortR, st);
-                    lt.rPerm = pp.sortR.perm;
-                }
-                launchTrace(r->ds, lt, pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting, r->traceThreads, st);
-            }
+            if (!(skipLast && l == nLevels))
+                launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting,
+                            r->traceThreads, st);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             if (!(skipLastShade && l == nLevels)) {
@@ -676,15 +617,10 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
             // the last level (depth > RayDepthMax) shades nothing: no shadow rays
             if (l < nLevels) {
-                Level ls = pp.levels[l];
-                if ((sortMode & 1) != 0) {
-                    launchSort(r->ds, ls, pp.counters, l, true, r->sortKeyShadow, pp.sortS, sb);
-                    ls.sPerm = pp.sortS.perm;
-                }
                 // the last shadow walk runs alone: a large shard gives it the full grid (C4 N = 1:
                 // 13.34 -> 13.29 ms); a small one keeps the narrow grid (N = 8: 2.53 vs 2.55 ms)
                 const bool lastAlone = l + 1 == nLevels && r->shadowGridPct == 0 && pathsPerLane >= 8.0;
-                launchShadow(r->ds, ls, pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
+                launchShadow(r->ds, pp.levels[l], pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
                              r->traceThreads, sb, lastAlone ? 100 : shadowPct);
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
@@ -710,69 +646,13 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     }
 }
 
-// renderPass, replayed from a captured graph where the pass is one chunk with nothing timed or
-// counted (tuning key 15).  The first pass of a configuration runs directly (it fills the
-// occupancy and event caches), the second is captured on the renderer's own stream (the
-// caller's may be the null stream, which cannot be captured) and every later one replays it,
-// joined to the caller's stream by two events.  Same launches, same arguments: same bits.
-void renderPassGraphed(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp) {
-    const bool eligible = r->useGraph != 0 && r->profileFlags == 0 && r->nSlots <= r->chunkSlots &&
-                          r->sortMode == 0 && !r->stopFlag.load();
-    if (!eligible) {
-        renderPass(r, dBitmap, dPacked, st, sampleBase, spp);
-        return;
-    }
-    const mrt_renderer::GraphKey key{dBitmap, dPacked, sampleBase, spp, r->graphGen};
-    hipStream_t gs = r->stream;
-    if (!(r->graphExec != nullptr && key == r->graphKey)) {
-        if (!(key == r->graphSeen)) {
-            r->graphSeen = key;
-            renderPass(r, dBitmap, dPacked, st, sampleBase, spp);
-            return;
-        }
-        if (r->graphIn == nullptr) {
-            MRT_HIP(hipEventCreateWithFlags(&r->graphIn, hipEventDisableTiming));
-            MRT_HIP(hipEventCreateWithFlags(&r->graphOut, hipEventDisableTiming));
-        }
-        if (gs != st) {  // the captured pass starts after the caller's earlier work
-            MRT_HIP(hipEventRecord(r->graphIn, st));
-            MRT_HIP(hipStreamWaitEvent(gs, r->graphIn, 0));
-        }
-        hipGraph_t g = nullptr;
-        MRT_HIP(hipStreamBeginCapture(gs, hipStreamCaptureModeRelaxed));
-        try {
-            renderPass(r, dBitmap, dPacked, gs, sampleBase, spp);
-        } catch (...) {
-            (void)hipStreamEndCapture(gs, &g);
-            if (g != nullptr) (void)hipGraphDestroy(g);
-            throw;
-        }
-        MRT_HIP(hipStreamEndCapture(gs, &g));
-        if (r->graphExec != nullptr) MRT_HIP(hipGraphExecDestroy(r->graphExec));
-        r->graphExec = nullptr;
-        const hipError_t e = hipGraphInstantiate(&r->graphExec, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        MRT_HIP(e);
-        r->graphKey = key;
-    }
-    if (gs != st) {
-        MRT_HIP(hipEventRecord(r->graphIn, st));
-        MRT_HIP(hipStreamWaitEvent(gs, r->graphIn, 0));
-    }
-    MRT_HIP(hipGraphLaunch(r->graphExec, gs));
-    if (gs != st) {
-        MRT_HIP(hipEventRecord(r->graphOut, gs));
-        MRT_HIP(hipStreamWaitEvent(st, r->graphOut, 0));
-    }
-}
-
 // One pass (samples [sampleBase, sampleBase + spp)) with its statistics added to *fs.
 // Returns false when the wavefront queues overflowed (the pass's output is then invalid).
 bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int sampleBase, int spp,
              mrt_frame_stats* fs) {
     using namespace mrt;
     const auto t0 = std::chrono::steady_clock::now();
-    renderPassGraphed(r, dBitmap, dPacked, st, sampleBase, spp);
+    renderPass(r, dBitmap, dPacked, st, sampleBase, spp);
     if (r->hostStats == nullptr) MRT_HIP(hipHostMalloc(&r->hostStats, sizeof(unsigned long long) * kNumStats));
     MRT_HIP(hipMemcpyAsync(r->hostStats, r->pipe.stats, sizeof(unsigned long long) * kNumStats, hipMemcpyDeviceToHost, st));
     MRT_HIP(hipStreamSynchronize(st));
@@ -788,6 +668,8 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->triTests += hs[kStatTris];
     fs->shadowNodeRecords += hs[kStatNodesShadow];
     fs->shadowTriTests += hs[kStatTrisShadow];
+    fs->leafRecords += hs[kStatLeaves];
+    fs->shadowLeafRecords += hs[kStatLeavesShadow];
     fs->maxNodeRecordsPerRay = std::max<uint64_t>(fs->maxNodeRecordsPerRay, hs[kStatMaxNodesRay]);
     fs->shadedVertices += hs[kStatShaded];
     fs->shadeLaunches += r->shadeLaunches;
@@ -1147,7 +1029,6 @@ int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
 
 int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
     r->profileFlags = flags;
-    ++r->graphGen;
     return 0;
 }
 
@@ -1166,11 +1047,6 @@ int64_t mrt_wave_log(mrt_renderer* r, uint64_t* out) {
 }
 
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
-    ++r->graphGen;  // every knob can change the captured launches
-    if (key == 15 && (value == 0 || value == 1)) {
-        r->useGraph = value;
-        return 0;
-    }
     if (key == 1 && value >= 0 && value < mrt::kTraceVariants) {
         r->ds.variant = value;
         return 0;
@@ -1191,10 +1067,6 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.anyOrder = value;
         return 0;
     }
-    if (key == 4 && (value == 0 || value == 1)) {
-        r->binMode = value;
-        return 0;
-    }
     if (key == 11 && value >= -1 && value <= 64) {
         r->shadeGridPerCU = value;
         return 0;
@@ -1209,18 +1081,6 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
     }
     if (key == 8 && (value == 0 || value == 1)) {
         r->ds.tailDonate = value;
-        return 0;
-    }
-    if (key == 12 && value >= 0 && value <= 3) {
-        r->sortMode = value;
-        return 0;
-    }
-    if (key == 13 && (value == 0 || value == 1)) {
-        r->sortKeyShadow = value;
-        return 0;
-    }
-    if (key == 14 && (value == 0 || value == 1)) {
-        r->sortKeyRay = value;
         return 0;
     }
     if (key == 6 && value >= 0 && value <= 100) {
@@ -1384,17 +1244,12 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 2: *value = r->ds.cull; return 0;
         case 3: *value = r->overlap; return 0;
         case 7: *value = r->skipLast; return 0;
-        case 4: *value = r->binMode; return 0;
         case 5: *value = r->ds.anyOrder; return 0;
         case 6: *value = r->shadowGridPct; return 0;
         case 8: *value = r->ds.tailDonate; return 0;
         case 9: *value = r->refill; return 0;
         case 10: *value = r->ds.leanShade; return 0;
         case 11: *value = r->shadeGridPerCU; return 0;
-        case 12: *value = r->sortMode; return 0;
-        case 13: *value = r->sortKeyShadow; return 0;
-        case 14: *value = r->sortKeyRay; return 0;
-        case 15: *value = r->useGraph; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

@@ -361,12 +361,11 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
 
 // kAny = false: closest hit -> out[i] = (t, u, v, primitive code);
 // kAny = true:  shadow any-hit -> out[i].w = occluded flag.
-// fetch: kWalkShards cursors, kFetchStride ints apart.  perm (or null): queue position -> ray.
+// fetch: kWalkShards cursors, kFetchStride ints apart.
 template <bool kAny, bool kCount, int kCull>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                TStack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest,
-                                                const int* __restrict__ perm) {
+                                                TStack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest) {
     constexpr int kHelper = -2;  // rayIdx of a lane walking a subtree given by another lane
     const bool donate = s.tailDonate != 0;
     const int top = min(kWalkTop, s.triTop);
@@ -518,7 +517,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 }
             }
             if (need) {
-                rayIdx = got >= 0 && perm != nullptr ? perm[got] : got;  // sorted queues: through the permutation
+                rayIdx = got;
                 if (kCount) {
                     cnt->rayStart = cnt->nodes;
                     if (got >= 0) ++cnt->rays;
@@ -663,6 +662,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 // its exact box, and the cull against that box's entry, decide (BVH.hpp:357-363)
                 const uint32_t lo = static_cast<uint32_t>(first) * 48u;
                 const float4 b0 = bload4(leafBuf, lo);
+                if (kCount) ++cnt->leaves;
                 if (kCull == kCullExact) {
                     const float4 b1 = bload4(leafBuf, lo + 16u);
                     const float4 b2 = bload4(leafBuf, lo + 32u);

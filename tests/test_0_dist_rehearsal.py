@@ -1,0 +1,62 @@
+"""Multi-rank rehearsal of bench.py's distributed path.
+
+bench.py under torch.distributed.run with 2 ranks on the one GPU of a test box: the gloo
+backend (MRT_BENCH_BACKEND=gloo: the gather goes through host memory; the measured multi-GPU path
+is RCCL with one GPU per rank), each rank renders its screen-tile shard into a packed buffer,
+rank 0 gathers and unpacks.  Rank 0's assembled bitmap must equal the single-GPU bench's and the
+oracle's.  The file name sorts first so that this test starts its child processes before the
+pytest process itself initialises the GPU (no process may exec another after that).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+W, H, SPP = 320, 192, 4
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench(tmp, name, nproc):
+    out = os.path.join(tmp, name + ".npy")
+    args = ["bench.py", "--gpus", str(nproc), "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+            "--width", str(W), "--height", str(H), "--spp", str(SPP), "--dump-bitmap", out]
+    env = dict(os.environ, MRT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    return np.load(out), line
+
+
+def test_two_rank_bench_assembles_the_single_gpu_frame(tmp_path, oracle_mod):
+    import json
+    import torch
+    assert not torch.cuda.is_initialized(), "must run before this process touches the GPU"
+    two, line2 = _bench(str(tmp_path), "two", 2)
+    one, _ = _bench(str(tmp_path), "one", 1)
+    j = json.loads(line2)
+    assert j["n_gpus"] == 2 and "gloo gather" in j["config"]["parallelism"]
+    assert np.array_equal(two, one), int((two != one).sum())
+    from mobileraytracer_amd import scenes
+    obj, mtl, cam = scenes.conference()
+    o = oracle_mod.Oracle(W, H, 2, -1, SPP, 1, 5, obj=obj, mtl=mtl, cam=cam)
+    ref = np.zeros(W * H, np.int32)
+    o.render(ref, threads=min(16, os.cpu_count() or 1))
+    o.close()
+    assert np.array_equal(two, ref), int((two != ref).sum())

@@ -329,12 +329,10 @@ def test_shadow_stream_overlap_is_invariant():
             assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
 
 
-def test_binned_emission_and_shadow_order_are_invariant():
-    """Binned emission (tuning key 4: child rays grouped by direction octant and lobe, shadow rays
-    by light, inside each k_shade block) only reorders the queues, and the shadow walk's child
-    order (key 5: near or far first) only changes which occluder is found first: every pixel, ray
-    count and shadow-ray count is the same in all combinations, for Whitted (3-child vertices),
-    PathTracer, more than one light sample and textures."""
+def test_shadow_order_is_invariant():
+    """The shadow walk's child order (key 5: near or far first) only changes which occluder is
+    found first: every pixel, ray count and shadow-ray count is the same, for Whitted (3-child
+    vertices), PathTracer, more than one light sample and textures."""
     import mobileraytracer_amd as m
     cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
              make_cfg(128, 128, shader=1, scene="water", max_depth=4),
@@ -344,10 +342,9 @@ def test_binned_emission_and_shadow_order_are_invariant():
     for cfg in cases:
         outs = []
         with m.Renderer(cfg) as r:
-            for b, a in ((0, 1), (1, 1), (0, 0)):
-                r.set_tuning(4, b)
+            for a in (1, 0):
                 r.set_tuning(5, a)
-                assert r.get_tuning(4) == b and r.get_tuning(5) == a
+                assert r.get_tuning(5) == a
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
                 r.render_frame(bm)
                 st = r.frame_stats()
@@ -357,34 +354,14 @@ def test_binned_emission_and_shadow_order_are_invariant():
             assert outs[0][1:] == other[1:], cfg
 
 
-def test_ray_sorting_is_invariant():
-    """Sorting a queue by a spatial key before its walk (tuning key 12: 1 shadow queues, 2
-    closest-hit queues of levels >= 2; keys 13 / 14: origin Morton, or octant + Morton) changes
-    only the order in which the walk takes the rays: same bitmap and ray counts, over Whitted
-    (3-child vertices), PathTracer, several light samples, textures and chunked passes."""
+def test_removed_tuning_keys_are_rejected():
+    """Binned emission (key 4), queue sorting (12-14) and graph replay (15) measured slower and
+    were removed from the product: their keys are unknown."""
     import mobileraytracer_amd as m
-    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
-             make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5, maxPathsPerPass=4096),
-             make_cfg(128, 128, shader=1, scene="water", max_depth=4),
-             make_cfg(96, 96, shader=2, scene="water", spp=2, max_depth=4, spl=3),
-             make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3),
-             make_cfg(64, 64, shader=2, spp=3, max_depth=6))
-    for cfg in cases:
-        outs = []
-        with m.Renderer(cfg) as r:
-            for mode, ks, kr, ov in ((0, 0, 1, 1), (3, 0, 1, 1), (3, 1, 0, 1), (1, 1, 1, 0), (2, 0, 0, 0)):
-                r.set_tuning(12, mode)
-                r.set_tuning(13, ks)
-                r.set_tuning(14, kr)
-                r.set_tuning(3, ov)
-                assert (r.get_tuning(12), r.get_tuning(13), r.get_tuning(14)) == (mode, ks, kr)
-                bm = np.zeros(cfg.width * cfg.height, np.int32)
-                r.render_frame(bm)
-                st = r.frame_stats()
-                outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"])))
-        for other in outs[1:]:
-            assert np.array_equal(outs[0][0], other[0]), cfg
-            assert outs[0][1:] == other[1:], cfg
+    with m.Renderer(make_cfg(32, 32)) as r:
+        for key in (4, 12, 13, 14, 15):
+            with pytest.raises(Exception):
+                r.set_tuning(key, 1)
 
 
 def test_tail_donation_matches_oracle_and_is_invariant(oracle_mod):
@@ -530,13 +507,25 @@ def test_shard_assembly_over_many_ranks():
     assert np.array_equal(img, single) and srays == rays
 
 
-def test_c5_4k_8spp_shards():
+def test_c5_4k_8spp_shards_and_tiles(oracle_mod):
+    """C5 (3840x2160, 8 spp, PathTracer): the 2- and 8-shard assemblies equal the single-GPU frame,
+    and six whole reference tiles (240x135 px x 8 samples each, spread over the frame) equal the
+    oracle bit for bit."""
     kw = dict(width=3840, height=2160, shader=2, scene="conference", spp=8, max_depth=5)
-    single, rays, st = gpu_render(make_cfg(**kw))
+    cfg = make_cfg(**kw)
+    single, rays, st = gpu_render(cfg)
     assert st["primaryRays"] == 3840 * 2160 * 8
     assert (single != SENTINEL).all()  # 3840x2160 tiles exactly (bx=240, by=135)
-    img, _, srays = _render_shards(kw, 2)
-    assert np.array_equal(img, single) and srays == rays
+    for world in (2, 8):
+        img, _, srays = _render_shards(kw, world)
+        assert np.array_equal(img, single) and srays == rays, world
+    o = oracle_for(oracle_mod, cfg)
+    ref = np.full(3840 * 2160, SENTINEL, np.int32)
+    o.render_tiles([0, 37, 86, 133, 170, 255], ref, threads=min(16, os.cpu_count() or 1))
+    o.close()
+    mask = ref != SENTINEL
+    assert mask.sum() == 6 * 240 * 135
+    assert np.array_equal(single[mask], ref[mask]), int((single[mask] != ref[mask]).sum())
 
 
 # ---- Renderer API semantics -----------------------------------------------------------------------
@@ -626,41 +615,3 @@ def test_invalid_config_raises():
         m.Renderer(bad)
 
 
-def test_graph_replay_is_invariant():
-    """Tuning key 15 replays a pass from a captured HIP graph (first pass of a configuration
-    direct, second captured, later ones replayed).  Every one of those frames equals the
-    direct frame bit for bit, with the same ray counts; a knob change between frames is
-    recaptured (cull off and on give the same image, each through its own capture); the
-    device entry point on a caller's stream replays, joined to that stream by events."""
-    import torch
-    import mobileraytracer_amd as m
-    cfg = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5)
-    n = cfg.width * cfg.height
-    with m.Renderer(cfg) as r:
-        assert r.get_tuning(15) == 0
-        ref = np.zeros(n, np.int32)
-        r.render_frame(ref)
-        st0 = r.frame_stats()
-        ref_stats = (st0["rays"], st0["shadowRays"], st0["walkedRays"])
-        r.set_tuning(15, 1)
-        assert r.get_tuning(15) == 1
-        for _ in range(4):
-            bm = np.zeros(n, np.int32)
-            r.render_frame(bm)
-            st = r.frame_stats()
-            assert np.array_equal(bm, ref)
-            assert (st["rays"], st["shadowRays"], st["walkedRays"]) == ref_stats
-        for cull in (0, 1, 0):
-            r.set_tuning(2, cull)
-            for _ in range(3):
-                bm = np.zeros(n, np.int32)
-                r.render_frame(bm)
-                assert np.array_equal(bm, ref)
-        dev = torch.zeros(n, dtype=torch.int32, device="cuda")
-        side = torch.cuda.Stream()
-        for _ in range(4):
-            with torch.cuda.stream(side):
-                dev.zero_()
-                r.render_frame_device(dev.data_ptr(), 0, side.cuda_stream)
-            side.synchronize()
-            assert np.array_equal(dev.cpu().numpy(), ref)

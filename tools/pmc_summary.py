@@ -12,7 +12,10 @@ TA / TD busy) are averaged per kernel as they are.
 import csv, glob, json, os, re, sys
 from collections import defaultdict
 
-PRODUCT = {"k_trace": r"k_trace<false, 1, 1>", "k_shadow": r"k_shadow<false, 1, 1>", "k_shade": r"k_shade<2, false>"}
+# the default (exact, cull mode 3) walk instantiations and the lean PathTracer shading kernel
+PRODUCT = {"k_trace": r"k_trace<false, 1, 3>", "k_shadow": r"k_shadow<false, 1, 3>", "k_shade": r"k_shade<2, false>"}
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_source_stamp  # noqa: E402
 
 
 def rows(d):
@@ -27,6 +30,7 @@ def main():
     for row in rows(src):
         per[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {"bytes_beyond_l2_per_launch": {}, "counters": {}, "kernels": {},
+           "kernel_source_sha256": kernel_source_stamp(),
            "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, averaged over the dispatches of "
                    "the profiled command; includes Infinity-Cache hits"}
     for short, pat in PRODUCT.items():
