@@ -157,6 +157,18 @@ int mrt_get_frame_stats(const mrt_renderer *r, mrt_frame_stats *stats);
  * wave: start, end in 100 MHz ticks, rays fetched, child records fetched; zero where no wave
  * ran).  Returns the entry count (1,048,576) or -1; out NULL only counts. */
 int64_t mrt_wave_log(mrt_renderer *r, uint64_t *out);
+/* The in-process plugin surface of app/MobileRT/Renderer.hpp:41-63 (include/mobilert_renderer.hpp
+ * builds on these).  mrt_set_camera replaces the renderer's camera: kind 0 Perspective(position,
+ * lookAt, up, hFov, vFov in degrees; Perspective.cpp:8-14, Camera.cpp:14-19), 1 Orthographic(position,
+ * lookAt, up, sizeH, sizeV; Orthographic.cpp:7-13).  mrt_set_pixel_sampler: the Renderer's
+ * samplerPixel_, kind 0 Constant(value) (Constant.cpp:9-11), 1 StaticHaltonSeq (the deterministic
+ * table draws), -1 (default) as C_wrapper.cpp:144-148: StaticHaltonSeq iff samplesPixel > 1.
+ * mrt_set_max_point: DepthMap's maxPoint (DepthMap.cpp; C_wrapper.cpp:79-131 passes maxDist).
+ * Each applies from the next frame; 0 on success. */
+int mrt_set_camera(mrt_renderer *r, int32_t kind, const float *position, const float *lookAt, const float *up,
+                   float a, float b);
+int mrt_set_pixel_sampler(mrt_renderer *r, int32_t kind, float value);
+int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
 /* tuning knobs for A/B measurement (results are identical for every value):
  * key 1 = trace walk: 0 per-wave 64-ray batches with the plain DFS of BVH.hpp:327-384,
  *         1 persistent while-while walk (default),

@@ -19,7 +19,7 @@ EXPORTED_SYMBOLS = (
     "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits", "mrt_set_tuning",
     "mrt_get_tuning", "mrt_triangle_bvh", "mrt_walk_tree", "mrt_decode_texture", "mrt_kat_slab", "mrt_kat_triangle",
     "mrt_trace_rays", "mrt_sample_tables", "mrt_regular_grid", "mrt_grid_box_test", "mrt_create_from_memory",
-    "mrt_preview_arrays", "mrt_wave_log",
+    "mrt_preview_arrays", "mrt_wave_log", "mrt_set_camera", "mrt_set_pixel_sampler", "mrt_set_max_point",
     "mrt_android_read_file", "mrt_android_initialize", "mrt_android_render_into_bitmap",
     "mrt_android_render_into_bitmap_cb", "mrt_android_wait_render", "mrt_android_start_render",
     "mrt_android_stop_render", "mrt_android_finish_render", "mrt_android_state", "mrt_android_fps",
@@ -122,6 +122,9 @@ def load_library(path=LIB_PATH):
                                                   ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64, vp, ctypes.c_int32,
                                                   P(vp)]),
         "mrt_preview_arrays": (ctypes.c_int64, [vp, vp, vp, vp]),
+        "mrt_set_camera": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp, ctypes.c_float, ctypes.c_float]),
+        "mrt_set_pixel_sampler": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_float]),
+        "mrt_set_max_point": (ctypes.c_int, [vp, vp]),
         "mrt_android_read_file": (None, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
         "mrt_android_initialize": (ctypes.c_int32, [P(MrtAndroidConfig)]),
         "mrt_android_render_into_bitmap": (None, [vp, ctypes.c_int32]),

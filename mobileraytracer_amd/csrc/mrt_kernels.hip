@@ -118,8 +118,8 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
     const float pixH = 0.5F / static_cast<float>(a.height);
     const float u = static_cast<float>(x) * invW;
     const float v = static_cast<float>(y) * invH;
-    float r1 = 0.5F, r2 = 0.5F;  // Constant(0.5) when spp <= 1 (C_wrapper.cpp:144-148)
-    if (a.sppTotal > 1) {  // the two draws of the pixel sampler, one 8-byte read
+    float r1 = a.constJitter, r2 = a.constJitter;  // Constant(value) (Constant.cpp:9-11)
+    if (a.tableJitter != 0) {  // StaticHaltonSeq: the two draws of the pixel sampler, one 8-byte read
         const float2 j = a.jitter[sampleBlock(key, 0u)];
         r1 = j.x;
         r2 = j.y;

@@ -91,9 +91,12 @@ struct RaygenArgs {
     int slotBase;    // first pixel slot of this chunk
     int nPaths;      // slots in chunk * spp
     int spp;         // samples processed in this pass
-    int sppTotal;    // samplesPixel of the renderer (decides the pixel sampler)
+    int sppTotal;    // samplesPixel of the renderer
     int sampleBase;  // global index of the first sample of this pass
-    int pad;
+    // the pixel sampler (Renderer's samplerPixel_): 1 StaticHaltonSeq (table draws), 0 Constant
+    // (every draw constJitter); C_wrapper.cpp:144-148 picks StaticHaltonSeq iff samplesPixel > 1
+    int tableJitter;
+    float constJitter;
 };
 
 struct ShadeArgs {

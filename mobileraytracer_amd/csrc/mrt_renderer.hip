@@ -91,6 +91,10 @@ struct mrt_renderer {
     int shader = mrt::kShaderWhitted;  // kShader* after the reference's switch (C_wrapper.cpp:153-193)
     int nLevels = 1;                   // wavefront levels: maxDepth + 1, or 1 for single-level shaders
     mrt::v3 maxPoint{1.0F, 1.0F, 1.0F};  // DepthMap
+    // the pixel sampler: -1 as C_wrapper.cpp:144-148 (StaticHaltonSeq iff samplesPixel > 1),
+    // 0 Constant(pixelConst), 1 StaticHaltonSeq (mrt_set_pixel_sampler)
+    int pixelSampler = -1;
+    float pixelConst = 0.5F;
     int rankIndex = 0, rankCount = 1;
     int device = 0;
 
@@ -449,6 +453,11 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     MRT_HIP(hipStreamSynchronize(st));
 }
 
+void setPixelSampler(const mrt_renderer* r, mrt::RaygenArgs* ra) {
+    ra->tableJitter = r->pixelSampler < 0 ? (r->cfg.samplesPixel > 1 ? 1 : 0) : r->pixelSampler;
+    ra->constJitter = r->pixelSampler == 0 ? r->pixelConst : 0.5F;
+}
+
 void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     using namespace mrt;
     r->queueMem.release();
@@ -565,6 +574,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.nPaths = nChunk * spp;
         ra.spp = spp;
         ra.sppTotal = r->cfg.samplesPixel;
+        setPixelSampler(r, &ra);
         ra.sampleBase = sampleBase;
         launchRaygen(ra, pp.levels[1], pp.counters, st);
         // With few paths per resident walk lane (a small shard: C4 at N >= 4) the levels are short
@@ -1027,6 +1037,36 @@ int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
     return 0;
 }
 
+int mrt_set_camera(mrt_renderer* r, int32_t kind, const float* position, const float* lookAt, const float* up,
+                   float a, float b) {
+    return guarded([&] {
+        const mrt::v3 p{position[0], position[1], position[2]}, l{lookAt[0], lookAt[1], lookAt[2]},
+            u{up[0], up[1], up[2]};
+        if (kind == 0) {
+            r->cam = mrt::makePerspective(p, l, u, a, b);
+        } else if (kind == 1) {
+            r->cam = mrt::makeOrthographic(p, l, u, a, b);
+        } else {
+            throw std::runtime_error("camera kind: 0 perspective, 1 orthographic");
+        }
+    });
+}
+
+int mrt_set_pixel_sampler(mrt_renderer* r, int32_t kind, float value) {
+    if (kind < -1 || kind > 1) {
+        gLastError = "pixel sampler: -1 by samplesPixel, 0 Constant, 1 StaticHaltonSeq";
+        return -1;
+    }
+    r->pixelSampler = kind;
+    r->pixelConst = value;
+    return 0;
+}
+
+int mrt_set_max_point(mrt_renderer* r, const float* maxPoint) {
+    r->maxPoint = mrt::v3{maxPoint[0], maxPoint[1], maxPoint[2]};
+    return 0;
+}
+
 int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
     r->profileFlags = flags;
     return 0;
@@ -1298,6 +1338,7 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
                 ra.nPaths = n;
                 ra.spp = 1;
                 ra.sppTotal = r->cfg.samplesPixel;
+                setPixelSampler(r, &ra);
                 ra.sampleBase = 0;
                 launchRaygen(ra, pp.levels[1], pp.counters, st);
                 launchTrace(r->ds, pp.levels[1], pp.counters, 1, pp.gstack, r->gdepth, pp.stats, false, r->traceThreads, st);
