@@ -18,6 +18,7 @@
 // Cornell image bit-exact.
 #include "mrt_kernels.hpp"
 #include "mrt_trace_ww.hpp"
+#include "mrt_trace_packet.hpp"
 
 #include <algorithm>
 #include <utility>
@@ -222,6 +223,25 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, i
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris, kStatLeaves);
         atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
+        waveLog(cnt, stats, 0, level, t0);
+    }
+}
+
+// Level-1 (camera) rays in cull modes 0 and 3: the wave-coherent walk (mrt_trace_packet.hpp).
+template <bool kCount, int kCull>
+__global__ __launch_bounds__(kWalkThreads, 8) void k_trace_packet(DScene s, Level lv, int* counters, int level,
+                                                                   int2* gstack, int gdepth, unsigned long long* stats) {
+    __shared__ int2 ldsStack[kWalkStack * kWalkThreads];  // per-lane fallback walks only
+    __shared__ int waveStacks[kWalkThreads / 64][kPacketStack];
+    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
+              kWalkStack, kWalkThreads};
+    const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const int count = min(counters[cntRays(level)], lv.cap);
+    int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
+    TravCount cnt{0u, 0u};
+    tracePacket<kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, waveStacks[threadIdx.x / 64]);
+    if (kCount) {
+        reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris, kStatLeaves);
         waveLog(cnt, stats, 0, level, t0);
     }
 }
@@ -941,6 +961,21 @@ void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int
         return;
     }
     const int gridPct = 100;
+    if (level == 1 && s.packet != 0 && s.variant == 1 && (s.cull == kCullNone || s.cull == kCullExact)) {
+        const int g = std::max(1, persistentGrid(k_trace_packet<false, kCullExact>, 10, maxThreads));
+        if (s.cull == kCullExact) {
+            if (countStats)
+                hipLaunchKernelGGL((k_trace_packet<true, kCullExact>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+            else
+                hipLaunchKernelGGL((k_trace_packet<false, kCullExact>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+        } else {
+            if (countStats)
+                hipLaunchKernelGGL((k_trace_packet<true, kCullNone>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+            else
+                hipLaunchKernelGGL((k_trace_packet<false, kCullNone>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+        }
+        return;
+    }
     MRT_LAUNCH_WALK(k_trace, 0);
 }
 
@@ -1032,7 +1067,9 @@ int traceResidentThreadsPerCU() {
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullFast>),
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullCertified>),
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullNone>),
-                             reinterpret_cast<const void*>(k_shadow<false, 1, kCullExact>)};
+                             reinterpret_cast<const void*>(k_shadow<false, 1, kCullExact>),
+                             reinterpret_cast<const void*>(k_trace_packet<false, kCullExact>),
+                             reinterpret_cast<const void*>(k_trace_packet<false, kCullNone>)};
     for (const void* k : kernels) {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWalkThreads, 0) == hipSuccess)

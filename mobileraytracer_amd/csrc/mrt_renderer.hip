@@ -425,6 +425,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.tailDonate = 1;
     d.refill = 32;  // kWalkRefill
     d.leanShade = 1;
+    d.packet = r->stackNeed <= kPacketStack ? 1 : 0;  // the packet walk's uniform stack must hold the tree's need
     d.matsFinite = 1;
     for (const HMaterial& m : sc.materials) {
         for (const v3 c : {m.Kd, m.Ks, m.Kt})
@@ -1123,6 +1124,14 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.tailDonate = value;
         return 0;
     }
+    if (key == 16 && (value == 0 || value == 1)) {
+        if (value == 1 && r->stackNeed > mrt::kPacketStack) {
+            gLastError = "packet walk: the walk tree needs a deeper stack";
+            return -1;
+        }
+        r->ds.packet = value;
+        return 0;
+    }
     if (key == 6 && value >= 0 && value <= 100) {
         r->shadowGridPct = value;
         return 0;
@@ -1290,6 +1299,7 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 9: *value = r->refill; return 0;
         case 10: *value = r->ds.leanShade; return 0;
         case 11: *value = r->shadeGridPerCU; return 0;
+        case 16: *value = r->ds.packet; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

@@ -1,0 +1,201 @@
+// mrt_trace_packet.hpp - wave-coherent ("packet") closest-hit walk for coherent rays on wave64.
+//
+// The camera rays of a wave are 16 neighbouring pixels x 4 samples (k_raygen's queue order), so
+// their walks over the quantized 4-wide tree nearly coincide.  Here the 64 rays of a wave share
+// ONE traversal: a wave-uniform stack of node references in LDS, each node fetched once per wave
+// through the scalar cache (uniform addresses in the constant address space become s_load), and
+// a child entered when ANY walking lane's ray passes its quantized box (a ballot).  Every lane
+// still decides its own leaves exactly as the per-lane walk does (traceWhileWhile): its own test
+// of the reference leaf box, the certified leaf cull of the exact mode, and its own triangle
+// tests (triangle records again scalar loads).  The packet visits a superset of each lane's
+// nodes and its lanes test exactly the leaves they would test alone; betterThan is a total order,
+// so each lane's closest hit is the per-lane walk's, bit for bit (tested: full frames and random
+// rays in tests/).  No lane diverges inside the loop, so VALU lanes stay busy on coherent rays.
+// Cull modes 0 (none) and 3 (exact) only: neither culls an inner node.
+#pragma once
+
+#include "mrt_trace_ww.hpp"
+
+namespace mrt {
+
+// Scalar (SGPR) loads: dwords read through the constant address space at a wave-uniform address
+typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+__device__ __forceinline__ int4 sload4i(ConstU32* p) {
+    return make_int4(static_cast<int>(p[0]), static_cast<int>(p[1]), static_cast<int>(p[2]), static_cast<int>(p[3]));
+}
+__device__ __forceinline__ float4 sload4f(ConstU32* p) {
+    return make_float4(__uint_as_float(p[0]), __uint_as_float(p[1]), __uint_as_float(p[2]), __uint_as_float(p[3]));
+}
+
+// A node reference made wave-uniform (it is, by construction; this tells the compiler).
+__device__ __forceinline__ int uniformInt(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <bool kCount, int kCull>
+__device__ __forceinline__ void tracePacket(const DScene& s, const float4* __restrict__ rOs,
+                                            const float4* __restrict__ rDs, float4* out, int count, int* fetch,
+                                            TStack& st, TravCount* cnt, int* waveStack) {
+    static_assert(kCull == kCullNone || kCull == kCullExact, "packet walk: cull modes 0 and 3");
+    ConstU32* const qn = (ConstU32*)(s.triQNodes);  // NOLINT: address-space casts
+    ConstU32* const tg = (ConstU32*)(s.triGeom);    // NOLINT
+    ConstU32* const lb = (ConstU32*)(s.leafBoxes);  // NOLINT
+    const int lane = static_cast<int>(threadIdx.x & 63u);
+    while (true) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(fetch, 64);
+        base = uniformInt(__shfl(base, 0, 64));
+        if (base >= count) break;
+        const int i = base + lane;
+        const bool valid = i < count;
+        v3 o{0, 0, 0}, d{1, 1, 1};
+        uint32_t src = 0;
+        if (valid) {
+            const float4 o4 = rOs[i], d4 = rDs[i];
+            o = xyz(o4);
+            d = xyz(d4);
+            src = fbits(d4.w);
+        }
+        const v3 inv{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
+        // lanes outside the quantized grid's bound (a zero direction component, ...) take the
+        // per-lane reference walk after the packet (rare; divergent)
+        const bool packed = valid && quantOK(s, o, inv);
+        Best b{kRayLengthMax, 0.0F, 0.0F, kNoPrim};
+        if (packed) {
+            traverse<kPlane, false>(s, s.planeNodes, s.planeRoot, o, d, inv, src, &b, st, cnt);
+            traverse<kSphere, false>(s, s.sphereNodes, s.sphereRoot, o, d, inv, src, &b, st, cnt);
+        }
+        float bt = b.t;
+        uint32_t bcode = b.code;
+        const v3 qa{s.qgrid.step[0] * inv.x, s.qgrid.step[1] * inv.y, s.qgrid.step[2] * inv.z};
+        const v3 qb{(s.qgrid.origin[0] - o.x) * inv.x, (s.qgrid.origin[1] - o.y) * inv.y,
+                    (s.qgrid.origin[2] - o.z) * inv.z};
+        const GRoot& r = s.triRoot;
+        float te;
+        const bool walking =
+            packed && r.count > 0 && slab(r.bmin[0], r.bmin[1], r.bmin[2], r.bmax[0], r.bmax[1], r.bmax[2], o, inv, &te);
+        const uint64_t walkers = __ballot(walking);
+        int ref = walkers != 0 ? r.ref : kRefDone;  // uniform
+        int sp = 0;                                 // uniform
+        // the lane whose entries order the children: the first walking one
+        const int lead = walkers != 0 ? __ffsll(static_cast<unsigned long long>(walkers)) - 1 : 0;
+        while (ref != kRefDone) {
+            if (ref >= 0) {  // ---- inner node: four children, entered on any lane's hit ----
+                int4 raw[kWalkWidth];
+#pragma unroll
+                for (int j = 0; j < kWalkWidth; ++j) raw[j] = sload4i(qn + 4 * (ref * kWalkWidth + j));
+                const auto word = [&](int k) -> uint32_t {
+                    const int4 v = raw[k >> 2];
+                    const int c = k & 3;
+                    return static_cast<uint32_t>(c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w);
+                };
+                uint32_t key[kWalkWidth];
+                int rf[kWalkWidth];
+                int n = 0;
+#pragma unroll
+                for (int c = 0; c < kWalkWidth; ++c) {
+                    const uint32_t w0 = word(3 * c), w1 = word(3 * c + 1), w2 = word(3 * c + 2);
+                    rf[c] = static_cast<int>(word(3 * kWalkWidth + c));
+                    float t;
+                    const bool h = walking && rf[c] != kEmptyChild &&
+                                   qslab(qlo(w0), qhi(w0), qlo(w1), qhi(w1), qlo(w2), qhi(w2), qa, qb, &t);
+                    if (kCount && walking && rf[c] != kEmptyChild) cnt->nodes += 1u;
+                    const bool any = __ballot(h) != 0;
+                    // order: the first walking lane's entry (entries are >= 0: their bits sort as
+                    // unsigned integers); children it misses go last
+                    const uint32_t k = static_cast<uint32_t>(
+                        __builtin_amdgcn_readlane(static_cast<int>(h ? __float_as_uint(t) : 0x7F800000u), lead));
+                    key[c] = any ? k : 0xFFFFFFFFu;
+                    n += any ? 1 : 0;
+                }
+                if (n == 0) {
+                    ref = sp > 0 ? uniformInt(waveStack[--sp]) : kRefDone;
+                    continue;
+                }
+                // ascending sort of the (key, reference) pairs (uniform values: scalar code)
+                const auto cex = [&](int a, int c) {
+                    if (key[c] < key[a]) {
+                        const uint32_t tk = key[a];
+                        key[a] = key[c];
+                        key[c] = tk;
+                        const int tr = rf[a];
+                        rf[a] = rf[c];
+                        rf[c] = tr;
+                    }
+                };
+                cex(0, 1);
+                cex(2, 3);
+                cex(0, 2);
+                cex(1, 3);
+                cex(1, 2);
+#pragma unroll
+                for (int c = kWalkWidth - 1; c >= 1; --c)
+                    if (c < n) {
+                        if (lane == 0) waveStack[sp] = rf[c];
+                        ++sp;
+                    }
+                ref = rf[0];
+                continue;
+            }
+            // ---- a leaf: each walking lane tests the reference box, then its triangles ----
+            const int first = leafFirst(ref);
+            const int nprim = leafCount(ref);
+            const float4 b0 = sload4f(lb + 12 * first), b1 = sload4f(lb + 12 * first + 4), b2 = sload4f(lb + 12 * first + 8);
+            bool test = false;
+            if (walking) {
+                if (kCount) ++cnt->leaves;
+                float tl, ex, ey, ez;
+                test = slabFiniteAxes(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv, &tl, &ex, &ey, &ez);
+                // the exact mode's certified leaf cull (mrt_trace_ww.hpp leafKey)
+                if (kCull == kCullExact && test && tl > bt && leafKey(b1, b2, tl, ex, ey, ez, d, inv) > bt) test = false;
+            }
+            if (__ballot(test) != 0) {
+                for (int k = 0; k < nprim; ++k) {
+                    const int j = first + k;
+                    const float4 ta = sload4f(tg + 12 * j), tb = sload4f(tg + 12 * j + 4), tc = sload4f(tg + 12 * j + 8);
+                    const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
+                    if (test && code != src) {
+                        if (kCount) ++cnt->tris;
+                        float t, u, v;
+                        if (triTest(ta, tb, tc, o, d, &t, &u, &v) && !(t < kEpsilon) && betterThan(t, code, bt, bcode)) {
+                            bt = t;
+                            bcode = code;
+                        }
+                    }
+                }
+            }
+            ref = sp > 0 ? uniformInt(waveStack[--sp]) : kRefDone;
+        }
+        if (valid) {
+            if (!packed) {
+                const Best f = closestHit(s, o, d, src, st, cnt);
+                out[i] = make_float4(f.t, f.u, f.v, bitsf(f.code));
+            } else {
+                for (int j = 0; j < s.nLights; ++j) {  // Shader.cpp:166-171
+                    const float4* l = s.lights + 4 * j;
+                    const float4 a4 = l[0];
+                    if (__float_as_int(a4.w) != 1) continue;
+                    float t, u, v;
+                    if (!triTest(a4, l[1], l[2], o, d, &t, &u, &v)) continue;
+                    if (t < kEpsilon) continue;
+                    const uint32_t code = encodePrim(kLight, static_cast<uint32_t>(j));
+                    if (betterThan(t, code, bt, bcode)) {
+                        bt = t;
+                        bcode = code;
+                    }
+                }
+                float u = b.u, v = b.v, t;  // planes / spheres keep their (0, 0)
+                const uint32_t kind = primKind(bcode);
+                if (kind == kTriangle || kind == kLight) {  // the winner's u, v: same inputs, same bits
+                    const float4* g = kind == kTriangle ? s.triGeom + 3 * primIndex(bcode) : s.lights + 4 * primIndex(bcode);
+                    (void)triTest(g[0], g[1], g[2], o, d, &t, &u, &v);
+                } else {
+                    u = 0.0F;
+                    v = 0.0F;
+                }
+                out[i] = make_float4(bt, u, v, bitsf(bcode));
+            }
+            if (kCount) ++cnt->rays;
+        }
+    }
+}
+
+}  // namespace mrt

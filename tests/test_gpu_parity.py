@@ -354,6 +354,41 @@ def test_shadow_order_is_invariant():
             assert outs[0][1:] == other[1:], cfg
 
 
+def test_packet_walk_matches_oracle_and_is_invariant(oracle_mod):
+    """The wave-coherent packet walk of the camera rays (tuning key 16, on by default: one
+    traversal per wave of 64 rays, mrt_trace_packet.hpp) returns the per-lane walk's hits: same
+    bitmap, ray counts and primary hits in the exact (3) and no-cull (0) modes, on triangle,
+    plane and sphere scenes; the primary hits equal the oracle's."""
+    import mobileraytracer_amd as m
+    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+             make_cfg(128, 128, shader=1, scene="water", max_depth=4),
+             make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3),
+             make_cfg(64, 64, shader=2, spp=3, max_depth=6), make_cfg(96, 64, shader=1, sceneIndex=2),
+             make_cfg(96, 64, shader=1, sceneIndex=3))
+    for cfg in cases:
+        outs = []
+        with m.Renderer(cfg) as r:
+            assert r.get_tuning(16) == 1
+            for packet, cull in ((1, 3), (0, 3), (1, 0), (0, 0)):
+                r.set_tuning(16, packet)
+                r.set_tuning(2, cull)
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"]), r.primary_hits()))
+        for other in outs[1:]:
+            assert np.array_equal(outs[0][0], other[0]), cfg
+            assert outs[0][1:4] == other[1:4], cfg
+            assert all(np.array_equal(a, b) for a, b in zip(outs[0][4], other[4])), cfg
+    for cfg in (make_cfg(128, 96, shader=1, scene="conference"), make_cfg(128, 128, scene="teapot"),
+                make_cfg(96, 64, sceneIndex=3)):
+        ok, oi, ot = oracle_for(oracle_mod, cfg).primary_hits()
+        with m.Renderer(cfg) as r:
+            k, i, t = r.primary_hits()
+        assert np.array_equal(k, ok) and np.array_equal(i, oi)
+        assert np.array_equal(t.view(np.int32), ot.view(np.int32))
+
+
 def test_removed_tuning_keys_are_rejected():
     """Binned emission (key 4), queue sorting (12-14) and graph replay (15) measured slower and
     were removed from the product: their keys are unknown."""
