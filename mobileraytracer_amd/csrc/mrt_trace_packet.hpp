@@ -27,6 +27,35 @@ __device__ __forceinline__ float4 sload4f(ConstU32* p) {
     return make_float4(__uint_as_float(p[0]), __uint_as_float(p[1]), __uint_as_float(p[2]), __uint_as_float(p[3]));
 }
 
+// Keeps scalar-loaded values in SGPRs at this point: every load issued before the first pin is
+// waited for once, there (an empty asm that reads them).
+__device__ __forceinline__ void pinSgprs(float4 v) { asm volatile("" ::"s"(v.x), "s"(v.y), "s"(v.z), "s"(v.w)); }
+__device__ __forceinline__ void pinSgprs(int4 v) { asm volatile("" ::"s"(v.x), "s"(v.y), "s"(v.z), "s"(v.w)); }
+
+// One triangle of the leaf being tested by the packet: A, AB, AC (triGeom's xyz), wave-uniform.
+struct PacketTri {
+    float4 a, ab, ac;
+    __device__ __forceinline__ void pin() const {
+        asm volatile("" ::"s"(a.x), "s"(a.y), "s"(a.z), "s"(ab.x), "s"(ab.y), "s"(ab.z));
+        asm volatile("" ::"s"(ac.x), "s"(ac.y), "s"(ac.z));
+    }
+    // this lane's test (the per-lane walk's: triTest, the t >= epsilon rule, betterThan)
+    template <bool kCount>
+    __device__ __forceinline__ void test(uint32_t code, bool lane, uint32_t src, v3 o, v3 d, float* bt, uint32_t* bcode,
+                                         TravCount* cnt) const {
+        if (!lane || code == src) return;
+        if (kCount) ++cnt->tris;
+        float t, u, v;
+        if (triTest(a, ab, ac, o, d, &t, &u, &v) && !(t < kEpsilon) && betterThan(t, code, *bt, *bcode)) {
+            *bt = t;
+            *bcode = code;
+        }
+    }
+};
+__device__ __forceinline__ PacketTri loadPacketTri(ConstU32* tg, int j) {
+    return PacketTri{sload4f(tg + 12 * j), sload4f(tg + 12 * j + 4), sload4f(tg + 12 * j + 8)};
+}
+
 // A node reference made wave-uniform (it is, by construction; this tells the compiler).
 __device__ __forceinline__ int uniformInt(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -82,6 +111,8 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
                 int4 raw[kWalkWidth];
 #pragma unroll
                 for (int j = 0; j < kWalkWidth; ++j) raw[j] = sload4i(qn + 4 * (ref * kWalkWidth + j));
+#pragma unroll
+                for (int j = 0; j < kWalkWidth; ++j) pinSgprs(raw[j]);  // one round trip per node
                 const auto word = [&](int k) -> uint32_t {
                     const int4 v = raw[k >> 2];
                     const int c = k & 3;
@@ -136,9 +167,19 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
                 continue;
             }
             // ---- a leaf: each walking lane tests the reference box, then its triangles ----
+            // The leaf record and the leaf's first two triangles are fetched in one scalar round
+            // trip (pinned before any use, so the compiler cannot sink a load behind a branch and
+            // pay a second trip), the remaining triangles two per trip.
             const int first = leafFirst(ref);
             const int nprim = leafCount(ref);
+            const int lastTri = r.count - 1;
             const float4 b0 = sload4f(lb + 12 * first), b1 = sload4f(lb + 12 * first + 4), b2 = sload4f(lb + 12 * first + 8);
+            PacketTri tri0 = loadPacketTri(tg, first), tri1 = loadPacketTri(tg, min(first + 1, lastTri));
+            pinSgprs(b0);
+            pinSgprs(b1);
+            pinSgprs(b2);
+            tri0.pin();
+            tri1.pin();
             bool test = false;
             if (walking) {
                 if (kCount) ++cnt->leaves;
@@ -148,18 +189,17 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
                 if (kCull == kCullExact && test && tl > bt && leafKey(b1, b2, tl, ex, ey, ez, d, inv) > bt) test = false;
             }
             if (__ballot(test) != 0) {
-                for (int k = 0; k < nprim; ++k) {
-                    const int j = first + k;
-                    const float4 ta = sload4f(tg + 12 * j), tb = sload4f(tg + 12 * j + 4), tc = sload4f(tg + 12 * j + 8);
-                    const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
-                    if (test && code != src) {
-                        if (kCount) ++cnt->tris;
-                        float t, u, v;
-                        if (triTest(ta, tb, tc, o, d, &t, &u, &v) && !(t < kEpsilon) && betterThan(t, code, bt, bcode)) {
-                            bt = t;
-                            bcode = code;
-                        }
+                for (int k = 0; k < nprim; k += 2) {
+                    if (k > 0) {
+                        tri0 = loadPacketTri(tg, first + k);
+                        tri1 = loadPacketTri(tg, min(first + k + 1, lastTri));
+                        tri0.pin();
+                        tri1.pin();
                     }
+                    tri0.test<kCount>(encodePrim(kTriangle, static_cast<uint32_t>(first + k)), test, src, o, d, &bt, &bcode, cnt);
+                    if (k + 1 < nprim)
+                        tri1.test<kCount>(encodePrim(kTriangle, static_cast<uint32_t>(first + k + 1)), test, src, o, d, &bt,
+                                          &bcode, cnt);
                 }
             }
             ref = sp > 0 ? uniformInt(waveStack[--sp]) : kRefDone;

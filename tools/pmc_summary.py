@@ -12,8 +12,11 @@ TA / TD busy) are averaged per kernel as they are.
 import csv, glob, json, os, re, sys
 from collections import defaultdict
 
-# the default (exact, cull mode 3) walk instantiations and the lean PathTracer shading kernel
-PRODUCT = {"k_trace": r"k_trace<false, 1, 3>", "k_shadow": r"k_shadow<false, 1, 3>", "k_shade": r"k_shade<2, false>"}
+# the default (exact, cull mode 3) walk instantiations and the lean PathTracer shading kernel;
+# "k_trace" is every closest-hit launch of a frame: the camera rays' packet walk and the per-lane
+# walk of the other levels, averaged over their dispatches as bench.py averages its launches
+PRODUCT = {"k_trace": (r"k_trace<false, 1, 3>", r"k_trace_packet<false, 3>"), "k_shadow": (r"k_shadow<false, 1, 3>",),
+           "k_shade": (r"k_shade<2, false>",)}
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import kernel_source_stamp  # noqa: E402
 
@@ -33,14 +36,17 @@ def main():
            "kernel_source_sha256": kernel_source_stamp(),
            "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, averaged over the dispatches of "
                    "the profiled command; includes Infinity-Cache hits"}
-    for short, pat in PRODUCT.items():
-        names = [k for k in per if pat in k]
+    for short, pats in PRODUCT.items():
+        names = [k for k in per if any(p in k for p in pats)]
         if not names:
             continue
-        c = per[names[0]]
+        c = defaultdict(list)  # counter -> values of every dispatch of these kernels
+        for n in names:
+            for k, v in per[n].items():
+                c[k].extend(v)
         avg = {k: sum(v) / len(v) for k, v in c.items() if v}
         out["counters"][short] = avg
-        out["kernels"][short] = names[0]
+        out["kernels"][short] = names
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             out["bytes_beyond_l2_per_launch"][short] = (2.0 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
         if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
