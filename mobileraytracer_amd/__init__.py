@@ -119,8 +119,23 @@ class Renderer:
         stream, 5 = shadow-walk child order (0 near first, 1 far first),
         6 = shadow-walk grid percent (0 auto), 7 = no walk for the depth-capped last level, 8 = tail
         donation (idle lanes of a level's tail walk subtrees of their wave's rays), 9 = refill
-        threshold of the walk waves, 10 = lean k_shade instantiation, 11 = k_shade workgroups per CU."""
+        threshold of the walk waves, 10 = lean k_shade instantiation, 11 = k_shade workgroups per CU,
+        16 = the camera rays' packet walk (cull modes 0 and 3)."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
+
+    def set_camera(self, kind: int, position, look_at, up, a: float, b: float) -> None:
+        """mrt_set_camera: kind 0 Perspective(position, lookAt, up, hFov, vFov in degrees), 1
+        Orthographic(position, lookAt, up, sizeH, sizeV) (Perspective.cpp / Orthographic.cpp)."""
+        vec = lambda v: (ctypes.c_float * 3)(*[float(x) for x in v])  # noqa: E731
+        _native.check(self._lib.mrt_set_camera(self._h, kind, vec(position), vec(look_at), vec(up), a, b))
+
+    def set_pixel_sampler(self, kind: int, value: float = 0.5) -> None:
+        """mrt_set_pixel_sampler: 0 Constant(value), 1 StaticHaltonSeq (the Renderer's pixel sampler)."""
+        _native.check(self._lib.mrt_set_pixel_sampler(self._h, kind, value))
+
+    def set_max_point(self, max_point) -> None:
+        """mrt_set_max_point: DepthMap's maxPoint."""
+        _native.check(self._lib.mrt_set_max_point(self._h, (ctypes.c_float * 3)(*[float(x) for x in max_point])))
 
     def get_tuning(self, key: int) -> int:
         v = ctypes.c_int32(0)

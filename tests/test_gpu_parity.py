@@ -389,6 +389,40 @@ def test_packet_walk_matches_oracle_and_is_invariant(oracle_mod):
         assert np.array_equal(t.view(np.int32), ot.view(np.int32))
 
 
+def test_python_plugin_setters():
+    """Renderer.set_camera / set_pixel_sampler (mrt_set_camera, mrt_set_pixel_sampler, the C++
+    facade's plugins): re-setting the built-in camera (Scenes.cpp: spheres' orthographic,
+    cornell's perspective) or the default pixel sampler leaves the image bit-identical; another
+    camera or sampler changes it."""
+    import mobileraytracer_amd as m
+    W, H = 64, 48
+    ratio = W / H
+    for idx, cam in ((1, (1, (0, 1, -10), (0, 1, 7), (0, 1, 0), 10 * ratio, 10)),
+                     (0, (0, (0, 0, -3.4), (0, 0, 1), (0, 1, 0), 45 * ratio, 45))):
+        cfg = make_cfg(W, H, shader=1, sceneIndex=idx)
+        with m.Renderer(cfg) as r:
+            base = np.zeros(W * H, np.int32)
+            r.render_frame(base)
+            r.set_camera(*cam)
+            same = np.zeros(W * H, np.int32)
+            r.render_frame(same)
+            assert np.array_equal(base, same), idx
+            kind, pos, look, up, a, b = cam
+            r.set_camera(kind, (pos[0] + 0.3, pos[1], pos[2]), look, up, a, b)
+            moved = np.zeros(W * H, np.int32)
+            r.render_frame(moved)
+            assert not np.array_equal(base, moved), idx
+            r.set_pixel_sampler(1)  # StaticHaltonSeq jitter instead of Constant(0.5) at 1 spp
+            r.set_camera(*cam)
+            halton = np.zeros(W * H, np.int32)
+            r.render_frame(halton)
+            assert not np.array_equal(base, halton), idx
+            r.set_pixel_sampler(0, 0.5)
+            back = np.zeros(W * H, np.int32)
+            r.render_frame(back)
+            assert np.array_equal(base, back), idx
+
+
 def test_removed_tuning_keys_are_rejected():
     """Binned emission (key 4), queue sorting (12-14) and graph replay (15) measured slower and
     were removed from the product: their keys are unknown."""
