@@ -24,6 +24,9 @@ struct DScene {
     const float4* triShade;    // 3 per triangle: nA (w = material index bits), nB, nC
     const GNode* triNodes;     // the reference tree (triRootRef)
     const QNode4* triQNodes;   // the walk tree (triRoot), 4-wide and quantized (QNode4)
+    // the same nodes for the packet walk's scalar loads (mrt_trace_packet.hpp), 128 B each: the 24
+    // grid indices as floats (child c: min xyz, max xyz at [6c, 6c + 6)), then the 4 references
+    const float* triQNodesF;
     // per leaf, indexed by its first triangle t (48 B): [3t] = min xyz, max x; [3t+1].xy = max yz
     // (walk-tree leaves are tested exactly before their triangles); [3t+1].zw, [3t+2] = the leaf's
     // certified-cull record (mrt_scene.cpp leafCullRecord; the exact cull mode)

@@ -268,6 +268,23 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.qEnabled = toQuantizedBVH4(wn, sc.triangles.size(), &d.triRoot, kTopNodesMax, &d.triTop, &d.qgrid, &qn) ? 1 : 0;
     if (d.qEnabled == 0 || qn.empty()) qn.resize(1);  // (a leaf or empty root: no inner node)
     d.triQNodes = r->sceneMem.upload(qn, st);
+    {
+        // the packet walk's copy: float(q) is exact (q < 2^16), so its planes fma(q, qa, qb) are
+        // the per-lane walk's bit for bit, without a conversion per bound (its loads are scalar:
+        // twice the bytes cost nothing there)
+        static_assert(kWalkWidth == 4, "packet nodes: 4 children");
+        std::vector<float> qf(32 * qn.size(), 0.0F);
+        for (size_t k = 0; k < qn.size(); ++k) {
+            const QNode4& q = qn[k];
+            for (int c = 0; c < kWalkWidth; ++c) {
+                const uint32_t w0 = q.q[3 * c], w1 = q.q[3 * c + 1], w2 = q.q[3 * c + 2];
+                const uint32_t v[6] = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16, w2 & 0xFFFFu, w2 >> 16};
+                for (int j = 0; j < 6; ++j) qf[32 * k + 6 * static_cast<size_t>(c) + static_cast<size_t>(j)] = static_cast<float>(v[j]);
+                std::memcpy(&qf[32 * k + 24 + static_cast<size_t>(c)], &q.ref[c], sizeof(int32_t));
+            }
+        }
+        d.triQNodesF = r->sceneMem.upload(qf, st);
+    }
     // a visit pushes up to kWalkWidth - 1 entries: the walk's stack holds that many per level
     {
         int depth4 = 0;

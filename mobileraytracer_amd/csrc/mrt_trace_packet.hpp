@@ -59,14 +59,16 @@ __device__ __forceinline__ PacketTri loadPacketTri(ConstU32* tg, int j) {
 // A node reference made wave-uniform (it is, by construction; this tells the compiler).
 __device__ __forceinline__ int uniformInt(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Closest hit of camera rays: rOs / rDs -> out = (t, u, v, primitive code).  (The any-hit form
+// for the level-1 shadow rays was built, exact and slower: DESIGN.md section 3.1.)
 template <bool kCount, int kCull>
 __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __restrict__ rOs,
                                             const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                             TStack& st, TravCount* cnt, int* waveStack) {
     static_assert(kCull == kCullNone || kCull == kCullExact, "packet walk: cull modes 0 and 3");
-    ConstU32* const qn = (ConstU32*)(s.triQNodes);  // NOLINT: address-space casts
-    ConstU32* const tg = (ConstU32*)(s.triGeom);    // NOLINT
-    ConstU32* const lb = (ConstU32*)(s.leafBoxes);  // NOLINT
+    ConstU32* const qnf = (ConstU32*)(s.triQNodesF);  // NOLINT: address-space casts
+    ConstU32* const tg = (ConstU32*)(s.triGeom);      // NOLINT
+    ConstU32* const lb = (ConstU32*)(s.leafBoxes);    // NOLINT
     const int lane = static_cast<int>(threadIdx.x & 63u);
     while (true) {
         int base = 0;
@@ -108,34 +110,43 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
         const int lead = walkers != 0 ? __ffsll(static_cast<unsigned long long>(walkers)) - 1 : 0;
         while (ref != kRefDone) {
             if (ref >= 0) {  // ---- inner node: four children, entered on any lane's hit ----
-                int4 raw[kWalkWidth];
+                // the node's float grid indices (DScene::triQNodesF): one scalar round trip
+                float4 nf[8];
 #pragma unroll
-                for (int j = 0; j < kWalkWidth; ++j) raw[j] = sload4i(qn + 4 * (ref * kWalkWidth + j));
+                for (int j = 0; j < 8; ++j) nf[j] = sload4f(qnf + 32 * ref + 4 * j);
 #pragma unroll
-                for (int j = 0; j < kWalkWidth; ++j) pinSgprs(raw[j]);  // one round trip per node
-                const auto word = [&](int k) -> uint32_t {
-                    const int4 v = raw[k >> 2];
+                for (int j = 0; j < 8; ++j) pinSgprs(nf[j]);
+                const auto fw = [&](int k) -> float {  // word k (a compile-time constant after unrolling)
+                    const float4 v = nf[k >> 2];
                     const int c = k & 3;
-                    return static_cast<uint32_t>(c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w);
+                    return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
                 };
                 uint32_t key[kWalkWidth];
                 int rf[kWalkWidth];
                 int n = 0;
 #pragma unroll
                 for (int c = 0; c < kWalkWidth; ++c) {
-                    const uint32_t w0 = word(3 * c), w1 = word(3 * c + 1), w2 = word(3 * c + 2);
-                    rf[c] = static_cast<int>(word(3 * kWalkWidth + c));
+                    rf[c] = __float_as_int(fw(24 + c));
+                    const bool used = rf[c] != kEmptyChild;  // uniform
+                    // the per-lane walk's planes bit for bit (float(q) is exact); every lane
+                    // computes, the walking ones count
                     float t;
-                    const bool h = walking && rf[c] != kEmptyChild &&
-                                   qslab(qlo(w0), qhi(w0), qlo(w1), qhi(w1), qlo(w2), qhi(w2), qa, qb, &t);
-                    if (kCount && walking && rf[c] != kEmptyChild) cnt->nodes += 1u;
-                    const bool any = __ballot(h) != 0;
-                    // order: the first walking lane's entry (entries are >= 0: their bits sort as
-                    // unsigned integers); children it misses go last
+                    const bool h = qslab(fw(6 * c), fw(6 * c + 1), fw(6 * c + 2), fw(6 * c + 3), fw(6 * c + 4),
+                                         fw(6 * c + 5), qa, qb, &t);
+                    if (kCount && walking && used) cnt->nodes += 1u;
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(h) & walkers;  // (no short circuit:
+                    const bool any = (m != 0u) & used;                              // straight-line code)
+                    // order: the lead lane's entry (entries are >= 0: their bits sort as unsigned
+                    // integers); children it misses go last
                     const uint32_t k = static_cast<uint32_t>(
                         __builtin_amdgcn_readlane(static_cast<int>(h ? __float_as_uint(t) : 0x7F800000u), lead));
                     key[c] = any ? k : 0xFFFFFFFFu;
-                    n += any ? 1 : 0;
+                }
+                // children entered (counted on the uniform keys: scalar code)
+#pragma unroll
+                for (int c = 0; c < kWalkWidth; ++c) {  // (integer form: no lane-mask booleans)
+                    const uint32_t x = ~key[c];
+                    n += static_cast<int>((x | (0u - x)) >> 31);
                 }
                 if (n == 0) {
                     ref = sp > 0 ? uniformInt(waveStack[--sp]) : kRefDone;

@@ -16,6 +16,9 @@ def main():
     r = m.Renderer(cfg)
     if "VARIANT" in os.environ:
         r.set_tuning(1, int(os.environ["VARIANT"]))
+    for kv in filter(None, os.environ.get("TUNE", "").split(",")):  # e.g. TUNE=16=2,5=0
+        k, v = kv.split("=")
+        r.set_tuning(int(k), int(v))
     d = torch.zeros(max(w * h, r.scene_info()["pixelSlotsMax"]), dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
     r.set_profiling(timing=True)
