@@ -615,7 +615,9 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // refill threshold: larger batches where a lane sees few paths (a small shard: the tail
         // dominates; C4 shard at N = 8: 24 / 32 / 40 -> 2.68 / 2.64 / 2.61 ms), smaller where it
         // sees many (N = 1: 13.77 / 13.86 / 13.88 ms)
-        r->ds.refill = r->refill > 0 ? r->refill : pathsPerLane < 4.0 ? 40 : 24;
+        // (re-tuned in round 3 with the walk's phase exits: N = 8 40 / 48 / 56 -> 3.17 / 3.07 /
+        // 3.14 ms; N = 1 24 / 32 / 36 -> 16.60 / 16.52 / 16.54 ms)
+        r->ds.refill = r->refill > 0 ? r->refill : pathsPerLane < 4.0 ? 48 : 32;
         size_t sync = 0;
         hipEvent_t shadowDone[kMaxLevels] = {};
         if (sb != st) {
