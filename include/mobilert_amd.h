@@ -195,7 +195,8 @@ int mrt_primary_hits(mrt_renderer *r, int32_t *kind, int32_t *index, float *t);
 int64_t mrt_triangle_bvh(const mrt_config *cfg, float *boxes, int32_t *offsets, int32_t *counts, int32_t *order);
 /* Host only: the quantized wide walk tree the BVH walk traverses:
  * returns the node count or -1; with non-NULL outputs fills nodes (count x 4W uint32: 3W box
- * words, W child references; W = the walk width, root[2]), grid[6] (origin xyz, step xyz) and
+ * words, child c's axis a at 3c + a as min | max << 16; W child references; W = the walk width,
+ * root[2]), grid[6] (origin xyz, step xyz) and
  * root[3] (reference, triangles, W). */
 int64_t mrt_walk_tree(const mrt_config *cfg, uint32_t *nodes, float *grid, int32_t *root);
 /* Host only: the RegularGrid accelerator's build (RegularGrid.hpp:112-289, gridSize 32) for one

@@ -149,6 +149,8 @@ def load_library(path=LIB_PATH):
         "mrt_trace_rays": (ctypes.c_int, [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("MOBILERT_LIB") and not hasattr(lib, name):
+            continue  # an older A/B build without a newer test entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

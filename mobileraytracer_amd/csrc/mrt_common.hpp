@@ -170,8 +170,8 @@ static_assert(sizeof(GNode) == 64, "GNode must be 64 bytes");
 
 // Walk-tree node ("quantized walk tree"): up to four children, each
 // child's box as 16-bit coordinates on one scene-wide grid (real value origin + q * step per axis)
-// rounded OUTWARD by one extra grid step (q[3c .. 3c+2] = child c's minx | miny << 16,
-// minz | maxx << 16, maxy | maxz << 16), and their references (kEmptyChild: no child): 64 bytes,
+// rounded OUTWARD by one extra grid step (q[3c + a] = child c's min | max << 16 on axis a), and
+// their references (kEmptyChild: no child): 64 bytes,
 // four 16-byte loads per visit, about half the dependent visits of a BVH2.
 constexpr int32_t kEmptyChild = 0x7FFFFFFE;
 #ifndef MRT_WALK_WIDTH

@@ -145,9 +145,11 @@ __device__ __forceinline__ bool finiteInv(v3 inv) {
     return __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
 }
 
-// Short traversal stack: the top `depth` (power of two) entries live in LDS (conflict-free
-// layout [slot][thread]), deeper entries spill to a per-thread global area.
+// Short traversal stack of the cull modes: each entry is a child's reference and its entry t
+// (8 B; culled entries are skipped at the pop).  The top `depth` (power of two) entries live in
+// LDS (conflict-free layout [slot][thread]), deeper entries spill to a per-thread global area.
 struct TStack {
+    static constexpr bool kKeys = true;
     int2* lds;    // &ldsBase[threadIdx.x]; slot s at lds[s * stride]
     int2* gbase;  // overflow areas (kernel-uniform base) ...
     int gofs;     // ... and this thread's offset into them (32-bit: one VGPR)
@@ -168,6 +170,45 @@ struct TStack {
         return v;
     }
 };
+
+// The stack of the modes that never cull an inner node (0 and 3, the default): references only
+// (4 B), so the same LDS holds twice the entries (16 per thread, [slot][thread]); deeper entries
+// spill to the per-thread global area as TStack's do.
+template <int kThreads>
+struct RefStack {
+    static constexpr bool kKeys = false;
+    static constexpr int kDepth = 2 * kLdsStackMin;
+    int* lds;    // &ldsBase[threadIdx.x]
+    int* gbase;  // overflow areas ...
+    int gofs;    // ... and this thread's offset into them
+    int sp;
+    __device__ __forceinline__ void push(int ref, float) {
+        const int slot = sp & (kDepth - 1);
+        if (sp >= kDepth) gbase[gofs + sp - kDepth] = lds[slot * kThreads];
+        lds[slot * kThreads] = ref;
+        ++sp;
+    }
+    __device__ __forceinline__ int2 pop() {  // (reference, 0)
+        --sp;
+        const int slot = sp & (kDepth - 1);
+        const int v = lds[slot * kThreads];
+        if (sp >= kDepth) lds[slot * kThreads] = gbase[gofs + sp - kDepth];
+        return make_int2(v, 0);
+    }
+};
+
+// A walk kernel's stack over its LDS array (kLdsStackMin int2 per thread) and its global spill
+// area (gdepth int2 per thread, gdepth >= the tree's stack need - kLdsStackMin).
+template <int kThreads>
+__device__ __forceinline__ TStack makeKeyStack(int2* ldsBase, int2* gstack, int gdepth) {
+    return TStack{ldsBase + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kThreads + threadIdx.x) * gdepth, 0,
+                  kLdsStackMin, kThreads};
+}
+template <int kThreads>
+__device__ __forceinline__ RefStack<kThreads> makeRefStack(int2* ldsBase, int2* gstack, int gdepth) {
+    return RefStack<kThreads>{reinterpret_cast<int*>(ldsBase) + threadIdx.x, reinterpret_cast<int*>(gstack),
+                              static_cast<int>(blockIdx.x * kThreads + threadIdx.x) * gdepth * 2, 0};
+}
 
 struct Best {
     float t, u, v;
@@ -378,9 +419,9 @@ __device__ __forceinline__ bool gridWalk(const DScene& s, const GGrid& g, v3 o, 
     return false;
 }
 
-template <int kKind, bool kAny>
+template <int kKind, bool kAny, class Stack>
 __device__ __forceinline__ bool traverse(const DScene& s, const GNode* nodes, const GRoot& root, v3 o, v3 d, v3 inv,
-                                         uint32_t src, Best* b, TStack& st, TravCount* cnt) {
+                                         uint32_t src, Best* b, Stack& st, TravCount* cnt) {
     if (root.count == 0) return false;  // BVH.hpp:328-330
     float te;
     if (!slab(root.bmin[0], root.bmin[1], root.bmin[2], root.bmax[0], root.bmax[1], root.bmax[2], o, inv, &te))
@@ -426,7 +467,8 @@ __device__ __forceinline__ bool traverse(const DScene& s, const GNode* nodes, co
 }
 
 // Shader::rayTrace intersection part (Shader.cpp:86-111): planes, spheres, triangles, lights.
-__device__ __forceinline__ Best closestHit(const DScene& s, v3 o, v3 d, uint32_t src, TStack& st, TravCount* cnt) {
+template <class Stack>
+__device__ __forceinline__ Best closestHit(const DScene& s, v3 o, v3 d, uint32_t src, Stack& st, TravCount* cnt) {
     const v3 inv = v3{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
     Best b{kRayLengthMax, 0.0F, 0.0F, kNoPrim};
     traverse<kPlane, false>(s, s.planeNodes, s.planeRoot, o, d, inv, src, &b, st, cnt);
@@ -451,7 +493,8 @@ __device__ __forceinline__ Best closestHit(const DScene& s, v3 o, v3 d, uint32_t
 }
 
 // Shader::shadowTrace (Shader.cpp:132-158): any hit closer than `dist`, lights excluded.
-__device__ __forceinline__ bool anyHit(const DScene& s, v3 o, v3 d, uint32_t src, float dist, TStack& st,
+template <class Stack>
+__device__ __forceinline__ bool anyHit(const DScene& s, v3 o, v3 d, uint32_t src, float dist, Stack& st,
                                        TravCount* cnt) {
     const v3 inv = v3{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
     Best b{dist, 0.0F, 0.0F, kNoPrim};

@@ -191,12 +191,21 @@ __device__ __forceinline__ void waveLog(const TravCount& cnt, unsigned long long
     }
 }
 
+// A walk's traversal stack: the cull modes pop against each entry's key (TStack); the others
+// store references only (RefStack: twice the entries in the same LDS)
+template <int kCull>
+__device__ __forceinline__ auto makeWalkStack(int2* ldsStack, int2* gstack, int gdepth) {
+    if constexpr (kCull == kCullFast || kCull == kCullCertified)
+        return makeKeyStack<kWalkThreads>(ldsStack, gstack, gdepth);
+    else
+        return makeRefStack<kWalkThreads>(ldsStack, gstack, gdepth);
+}
+
 template <bool kCount, int kVariant, int kCull>
 __global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, int* counters, int level,
                                                             int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
-              kWalkStack, kWalkThreads};
+    auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
     const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int count = min(counters[cntRays(level)], lv.cap);
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
@@ -233,8 +242,7 @@ __global__ __launch_bounds__(kWalkThreads, 8) void k_trace_packet(DScene s, Leve
                                                                    int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];  // per-lane fallback walks only
     __shared__ int waveStacks[kWalkThreads / 64][kPacketStack];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
-              kWalkStack, kWalkThreads};
+    auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
     const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int count = min(counters[cntRays(level)], lv.cap);
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
@@ -250,8 +258,7 @@ template <bool kCount, int kVariant, int kCull>
 __global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, int* counters, int level,
                                                              int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
-    TStack st{ldsStack + threadIdx.x, gstack, static_cast<int>(blockIdx.x * kWalkThreads + threadIdx.x) * gdepth, 0,
-              kWalkStack, kWalkThreads};
+    auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
     const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int count = min(counters[cntShadows(level)], lv.shadowCap);
     int* fetch = counters + kCntFetchShards + (kMaxLevels + level) * kMaxFetchShards * kFetchStride;

@@ -278,7 +278,8 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
             const QNode4& q = qn[k];
             for (int c = 0; c < kWalkWidth; ++c) {
                 const uint32_t w0 = q.q[3 * c], w1 = q.q[3 * c + 1], w2 = q.q[3 * c + 2];
-                const uint32_t v[6] = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16, w2 & 0xFFFFu, w2 >> 16};
+                // (min xyz, max xyz) from the per-axis words min | max << 16
+                const uint32_t v[6] = {w0 & 0xFFFFu, w1 & 0xFFFFu, w2 & 0xFFFFu, w0 >> 16, w1 >> 16, w2 >> 16};
                 for (int j = 0; j < 6; ++j) qf[32 * k + 6 * static_cast<size_t>(c) + static_cast<size_t>(j)] = static_cast<float>(v[j]);
                 std::memcpy(&qf[32 * k + 24 + static_cast<size_t>(c)], &q.ref[c], sizeof(int32_t));
             }

@@ -1008,12 +1008,16 @@ struct Quantizer {
         while (q < 65535.0 && org[a] + q * step[a] < static_cast<double>(b) + step[a]) q += 1.0;
         return static_cast<uint32_t>(q);
     }
-    // one box as three words: minx | miny << 16, minz | maxx << 16, maxy | maxz << 16
+    // one box as three words, one per axis: min | max << 16 (the walk rotates a word by 16 bits
+    // when the ray's 1/d is negative on that axis, mrt_trace_ww.hpp qslabNF, so min <= max)
     bool box(const float* mn, const float* mx, uint32_t* w) const {
         for (int a = 0; a < 3; ++a)
             if (!std::isfinite(mn[a]) || !std::isfinite(mx[a])) return false;
-        const uint32_t q[6] = {lo(mn[0], 0), lo(mn[1], 1), lo(mn[2], 2), hi(mx[0], 0), hi(mx[1], 1), hi(mx[2], 2)};
-        for (int k = 0; k < 3; ++k) w[k] = q[2 * k] | (q[2 * k + 1] << 16);
+        for (int a = 0; a < 3; ++a) {
+            const uint32_t l = lo(mn[a], a), h = hi(mx[a], a);
+            if (l > h) return false;
+            w[a] = l | (h << 16);
+        }
         return true;
     }
 };

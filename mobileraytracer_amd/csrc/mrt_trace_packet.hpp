@@ -61,10 +61,10 @@ __device__ __forceinline__ int uniformInt(int v) { return __builtin_amdgcn_readf
 
 // Closest hit of camera rays: rOs / rDs -> out = (t, u, v, primitive code).  (The any-hit form
 // for the level-1 shadow rays was built, exact and slower: DESIGN.md section 3.1.)
-template <bool kCount, int kCull>
+template <bool kCount, int kCull, class Stack>
 __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __restrict__ rOs,
                                             const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                            TStack& st, TravCount* cnt, int* waveStack) {
+                                            Stack& st, TravCount* cnt, int* waveStack) {
     static_assert(kCull == kCullNone || kCull == kCullExact, "packet walk: cull modes 0 and 3");
     ConstU32* const qnf = (ConstU32*)(s.triQNodesF);  // NOLINT: address-space casts
     ConstU32* const tg = (ConstU32*)(s.triGeom);      // NOLINT

@@ -82,7 +82,8 @@ __device__ __forceinline__ int lanesBelowIn(uint64_t m) {
                                                       __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
 }
 
-__device__ __forceinline__ int popCulled(TStack& st, float lim, bool cull) {
+template <class Stack>
+__device__ __forceinline__ int popCulled(Stack& st, float lim, bool cull) {
     while (st.sp > 0) {
         const int2 e = st.pop();
         if (!cull || !(__int_as_float(e.y) > lim)) return e.x;
@@ -158,8 +159,9 @@ __device__ __forceinline__ float leafKey(float4 r1, float4 r2, float te, float e
 }
 
 // Culling against the keys, near-first order (by box entry) and the push of the far child.
+template <class Stack>
 __device__ __forceinline__ int chooseChildren(bool hl, bool hr, float tl, float tr, float kl, float kr, int refL,
-                                              int refR, float lim, bool cull, TStack& st, bool rightFirst) {
+                                              int refR, float lim, bool cull, Stack& st, bool rightFirst) {
     if (cull) {
         hl = hl && !(kl > lim);
         hr = hr && !(kr > lim);
@@ -210,8 +212,8 @@ constexpr int innerCullMode() {
 // Reference-tree nodes (GNode, exact boxes, from global memory).
 // finite: wave-uniform, every active lane's 1/d is finite (slabFinite applies; otherwise the
 // exact slab, and the certified mode does not cull)
-template <int kCull>
-__device__ __forceinline__ int innerStep(BufRes nodes, int ref, v3 o, v3 d, v3 inv, float lim, TStack& st,
+template <int kCull, class Stack>
+__device__ __forceinline__ int innerStep(BufRes nodes, int ref, v3 o, v3 d, v3 inv, float lim, Stack& st,
                                          TravCount* cnt, bool count, bool finite, int order) {
     constexpr bool cull = kCull != kCullNone;
     const uint32_t off = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(GNode));
@@ -263,8 +265,7 @@ __device__ __forceinline__ int innerStep(BufRes nodes, int ref, v3 o, v3 d, v3 i
 
 // The quantized walk tree's planes: t = fma(q, qa, qb) with qa = step / d, qb = (origin - o) / d
 // per axis (rounded as the Quantizer's bound in mrt_scene.cpp assumes); the slab logic of slabFinite.
-__device__ __forceinline__ float qlo(uint32_t w) { return static_cast<float>(w & 0xFFFFu); }
-__device__ __forceinline__ float qhi(uint32_t w) { return static_cast<float>(w >> 16); }
+// This form (the packet walk's) takes the bounds as floats, min xyz then max xyz.
 __device__ __forceinline__ bool qslab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, v3 qa, v3 qb,
                                       float* tEntry) {
     const float t1x = fmaf(mnx, qa.x, qb.x), t2x = fmaf(mxx, qa.x, qb.x);
@@ -272,6 +273,26 @@ __device__ __forceinline__ bool qslab(float mnx, float mny, float mnz, float mxx
     const float t1z = fmaf(mnz, qa.z, qb.z), t2z = fmaf(mxz, qa.z, qb.z);
     const float e = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fmaxf(fminf(t1z, t2z), 0.0F));
     const float tMax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+    *tEntry = e;
+    return tMax >= e;
+}
+// The per-lane walk's form on the node's words.  A child's axis is one word, min | max << 16
+// (QNode4).  For qa > 0 the min plane is the nearer one: fma is monotone in q (correctly rounded),
+// so min(t(min), t(max)) = t(min); for qa < 0 the max plane.  The word is rotated by 16 bits when
+// the axis's 1/d is negative (nearFarShift, one v_alignbit), after which its low half is the near
+// plane and its high half the far one: the same entry and exit without the three min / max pairs
+// (19 VALU per child instead of 22).  quantOK rays have finite, nonzero qa and qb: no NaN.
+__device__ __forceinline__ uint32_t nearFarShift(float qa) { return (__float_as_uint(qa) >> 27) & 16u; }
+__device__ __forceinline__ bool qslabNF(uint32_t wx, uint32_t wy, uint32_t wz, uint32_t sx, uint32_t sy, uint32_t sz,
+                                        v3 qa, v3 qb, float* tEntry) {
+    const uint32_t rx = __builtin_amdgcn_alignbit(wx, wx, sx);
+    const uint32_t ry = __builtin_amdgcn_alignbit(wy, wy, sy);
+    const uint32_t rz = __builtin_amdgcn_alignbit(wz, wz, sz);
+    const float nx = fmaf(static_cast<float>(rx & 0xFFFFu), qa.x, qb.x), fx = fmaf(static_cast<float>(rx >> 16), qa.x, qb.x);
+    const float ny = fmaf(static_cast<float>(ry & 0xFFFFu), qa.y, qb.y), fy = fmaf(static_cast<float>(ry >> 16), qa.y, qb.y);
+    const float nz = fmaf(static_cast<float>(rz & 0xFFFFu), qa.z, qb.z), fz = fmaf(static_cast<float>(rz >> 16), qa.z, qb.z);
+    const float e = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.0F));
+    const float tMax = fminf(fminf(fx, fy), fz);
     *tEntry = e;
     return tMax >= e;
 }
@@ -311,9 +332,9 @@ __device__ __forceinline__ void sortChildren(float* k, int* r) {
 // leaves are tested exactly before their triangles (traceWhileWhile).  The hit children are
 // visited in order of entry (order 0: nearest first; 1: farthest first): the first now, the
 // others pushed.
-template <int kCull>
+template <int kCull, class Stack>
 __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, int top, int ref, v3 qa, v3 qb,
-                                          float lim, TStack& st, TravCount* cnt, bool count, int order) {
+                                          float lim, Stack& st, TravCount* cnt, bool count, int order) {
     constexpr int W = kWalkWidth;
     constexpr bool cull = kCull != kCullNone;
     int4 raw[W];
@@ -332,6 +353,7 @@ __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, i
         return static_cast<uint32_t>(c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w);
     };
     constexpr float kInf = __builtin_inff();
+    const uint32_t sx = nearFarShift(qa.x), sy = nearFarShift(qa.y), sz = nearFarShift(qa.z);
     const float sg = order == 0 ? 1.0F : -1.0F;  // sort keys: the entry (nearest first) or its negation
     float key[W];
     int rf[W];
@@ -343,14 +365,14 @@ __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, i
         const bool used = rf[c] != kEmptyChild;
         if (count) cnt->nodes += used ? 1u : 0u;
         float t;
-        bool h = qslab(qlo(w0), qhi(w0), qlo(w1), qhi(w1), qlo(w2), qhi(w2), qa, qb, &t) && used;
+        bool h = qslabNF(w0, w1, w2, sx, sy, sz, qa, qb, &t) && used;
         if (cull) h = h && !(t > lim);
         n += h ? 1 : 0;
         key[c] = h ? sg * t : kInf;  // misses last
     }
     if (n == 0) return popCulled(st, lim, cull);
     sortChildren<W>(key, rf);
-    // push the others farthest-in-order first (the stack's key is the entry, for popCulled)
+    // push the others farthest-in-order first (a keyed stack's key is the entry, for popCulled)
 #pragma unroll
     for (int k = W - 1; k >= 1; --k)
         if (k < n) st.push(rf[k], sg * key[k]);
@@ -385,10 +407,10 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
 // kAny = false: closest hit -> out[i] = (t, u, v, primitive code);
 // kAny = true:  shadow any-hit -> out[i].w = occluded flag.
 // fetch: kWalkShards cursors, kFetchStride ints apart.
-template <bool kAny, bool kCount, int kCull>
+template <bool kAny, bool kCount, int kCull, class Stack>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                TStack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest) {
+                                                Stack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest) {
     constexpr int kHelper = -2;  // rayIdx of a lane walking a subtree given by another lane
     const bool donate = s.tailDonate != 0;
     const int top = min(kWalkTop, s.triTop);

@@ -60,8 +60,9 @@ def test_walk_tree_holds_reference_leaves_with_margin(case):
             if ref == EMPTY:
                 continue
             exact = child_box(ref)
-            q = np.array([w[3 * c] & 0xFFFF, w[3 * c] >> 16, w[3 * c + 1] & 0xFFFF,
-                          w[3 * c + 1] >> 16, w[3 * c + 2] & 0xFFFF, w[3 * c + 2] >> 16], np.float64)
+            # one word per axis: min | max << 16
+            q = np.array([w[3 * c] & 0xFFFF, w[3 * c + 1] & 0xFFFF, w[3 * c + 2] & 0xFFFF,
+                          w[3 * c] >> 16, w[3 * c + 1] >> 16, w[3 * c + 2] >> 16], np.float64)
             qmin, qmax = org + q[:3] * step, org + q[3:] * step
             assert np.all(qmin <= exact[:3] - step), (i, c)
             assert np.all(qmax >= exact[3:] + step), (i, c)
