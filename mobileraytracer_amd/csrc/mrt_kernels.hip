@@ -419,10 +419,11 @@ __device__ __forceinline__ uint32_t lightChoice(const DScene& s, float pick) {
 // Light sample i of a shading point (Whitted.cpp:41-53, PathTracer.cpp:53-67):
 // returns false when cos <= 0 (no shadow ray is built).
 // pick / r / q: the three table draws of this sample (light choice, area-light point)
+// lights: DScene::lights, or k_shade's LDS copy of it
 __device__ __forceinline__ bool lightSample(const DScene& s, const HitGeom& g, float pick, float r, float q,
-                                           v3* dirOut, float* distOut, v3* contribOut) {
+                                           v3* dirOut, float* distOut, v3* contribOut, const float4* lights) {
     const uint32_t chosen = lightChoice(s, pick);
-    const float4* l = s.lights + 4 * chosen;
+    const float4* l = lights + 4 * chosen;
     const float4 a4 = l[0];
     v3 pos;
     if (__float_as_int(a4.w) == 1) {  // AreaLight::getPosition (AreaLight.cpp:17-26)
@@ -463,10 +464,11 @@ struct ShadeState {
 };
 
 // kw: textureWrite of this hit (w >= 0: the material's Kd is that texel when shade() runs)
+// mats / lights: DScene::mats / lights, or k_shade's LDS copies of them
 template <int kShader>
 __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, float4 d4, float4 h, uint32_t tc,
-                                                   int level, const ShadeArgs& a,
-                                                   float4 kw = make_float4(0.0F, 0.0F, 0.0F, -1.0F)) {
+                                                   int level, const ShadeArgs& a, float4 kw, const float4* mats,
+                                                   const float4* lights) {
     ShadeState v{};
     v.terminal = true;
     v.leaf = make_float4(0.0F, 0.0F, 0.0F, 0.0F);
@@ -491,10 +493,10 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     if (kind == kMiss || level > a.maxDepth) return v;
     v3 Le, Kd{0, 0, 0}, Ks{0, 0, 0}, Kt{0, 0, 0};
     if (kind == kLight) {
-        Le = xyz(s.lights[4 * primIndex(code) + 3]);
+        Le = xyz(lights[4 * primIndex(code) + 3]);
     } else {
         v.mat = hitMaterial(s, code);
-        const float4* m = s.mats + 4 * v.mat;
+        const float4* m = mats + 4 * v.mat;
         const float4 le4 = m[0];
         Le = xyz(le4);
         v.ior = le4.w;
@@ -510,14 +512,14 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
     v.g = hitGeometry(s, xyz(o4), v.d, h);
     v.direct = hasPositive(Kd) && s.nLights > 0;
     if (v.direct) {
-        v.ok0 = lightSample(s, v.g, pick0, lr0, lq0, &v.ld0, &v.dist0, &v.lc0);
+        v.ok0 = lightSample(s, v.g, pick0, lr0, lq0, &v.ld0, &v.dist0, &v.lc0, lights);
         v.nShadow = static_cast<int>(v.ok0);
         for (int k = 1; k < a.samplesLight; ++k) {
             v3 ld, lc;
             float dist;
             if (lightSample(s, v.g, s.tables[sampleIndex(v.key, tc, purposeLightPick(k))].x,
                             s.tables[sampleIndex(v.key, tc, purposeLightR(k))].y,
-                            s.tables[sampleIndex(v.key, tc, purposeLightS(k))].y, &ld, &dist, &lc))
+                            s.tables[sampleIndex(v.key, tc, purposeLightS(k))].y, &ld, &dist, &lc, lights))
                 ++v.nShadow;
         }
     }
@@ -537,7 +539,7 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
 // payloads are not written and their directions not computed.
 __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, int i, const Level& lv, const Level& nx,
                                           int shadowBase, int childBase, int* counters, const ShadeArgs& a,
-                                          bool deadNext) {
+                                          bool deadNext, const float4* lights) {
     if (v.terminal) {
         lv.res[i] = v.leaf;
         lv.vtx[i] = make_int4(-1, 0, 0, 0);
@@ -553,7 +555,7 @@ __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, 
                 if (!v.ok0) continue;
             } else if (!lightSample(s, v.g, s.tables[sampleIndex(v.key, v.tc, purposeLightPick(k))].x,
                                     s.tables[sampleIndex(v.key, v.tc, purposeLightR(k))].y,
-                                    s.tables[sampleIndex(v.key, v.tc, purposeLightS(k))].y, &ld, &dist, &lc)) {
+                                    s.tables[sampleIndex(v.key, v.tc, purposeLightS(k))].y, &ld, &dist, &lc, lights)) {
                 continue;
             }
             const int j = shadowBase + written;
@@ -600,10 +602,22 @@ __device__ __forceinline__ v3 firstChildDir(const ShadeState& v) {
 
 // kFull: the general kernel (textures, counting); the lean instantiation (no
 // texture, compaction only, no statistics) needs fewer registers: 65 VGPRs instead of 103, so
-// 7 waves per SIMD instead of 4
+// 7 waves per SIMD instead of 4, and reads the materials and lights (eight of a vertex's 64-B
+// gathers, from tables of a few KB) from a copy in LDS instead of through the texture path,
+// which the hit, ray and shading-record gathers keep busy.  (kShadeLdsTable: the launch falls
+// back to the general kernel for scenes whose tables do not fit.)
+constexpr int kShadeLdsTable = 256;  // float4: 4 per material, then 4 per light
 template <int kShader, bool kFull>
 __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a,
                                                   int deadNext) {
+    __shared__ float4 tab[kFull ? 1 : kShadeLdsTable];
+    if constexpr (!kFull) {
+        const int nm = 4 * s.nMats, nt = nm + 4 * s.nLights;
+        for (int k = static_cast<int>(threadIdx.x); k < nt; k += kBlock) tab[k] = k < nm ? s.mats[k] : s.lights[k - nm];
+        __syncthreads();
+    }
+    const float4* const mats = kFull ? s.mats : tab;
+    const float4* const lights = kFull ? s.lights : tab + 4 * s.nMats;
     const int count = min(counters[cntRays(level)], lv.cap);
     // {rays of level+1, shadow rays of level}: one 64-bit allocation per block and iteration
     auto* pair = reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1));
@@ -624,14 +638,14 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
                 lv.kd[i] = kw;
                 lv.last[i] = kw;
             }
-            v = shadePrepare<kShader>(s, lv.rO[i], lv.rD[i], h, lv.tree[i], level, a, kw);
+            v = shadePrepare<kShader>(s, lv.rO[i], lv.rD[i], h, lv.tree[i], level, a, kw, mats, lights);
             if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
         }
         int childBase, shadowBase;
         const int nC = active ? v.nChild : 0, nS = active ? v.nShadow : 0;
         blockAllocPair(pair, nC, nS, &childBase, &shadowBase, allocLds, parity);
         parity ^= 1;
-        if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, dead);
+        if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, dead, lights);
         if (kFull && a.stats != nullptr) {  // counting pass: shaded (non-terminal) vertices
             const uint64_t m = __ballot(active && !v.terminal);
             if (laneId() == 0 && m != 0) atomicAdd(a.stats + kStatShaded, static_cast<unsigned long long>(__popcll(m)));
@@ -697,7 +711,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int
                         float dist;
                         if (lightSample(s, g, s.tables[sampleIndex(key, tc, purposeLightPick(k))].x,
                                         s.tables[sampleIndex(key, tc, purposeLightR(k))].y,
-                                        s.tables[sampleIndex(key, tc, purposeLightS(k))].y, &ld, &dist, &lc))
+                                        s.tables[sampleIndex(key, tc, purposeLightS(k))].y, &ld, &dist, &lc, s.lights))
                             rgb = rgb + lc;  // Le * cosNl
                     }
                     rgb = rgb * Kd;
@@ -998,7 +1012,8 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st, bool deadNext) {
     const int dead = deadNext ? 1 : 0;
-    const bool full = s.textured != 0 || a.stats != nullptr || s.leanShade == 0;
+    const bool full = s.textured != 0 || a.stats != nullptr || s.leanShade == 0 ||
+                      4 * (s.nMats + s.nLights) > kShadeLdsTable;
     switch (shader) {
         case kShaderWhitted:
             if (full)
