@@ -9,9 +9,11 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <fstream>
 #include <random>
 #include <sstream>
+#include <string>
 #include <thread>
 #include <unordered_map>
 
@@ -1051,6 +1053,70 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
                      dz = static_cast<double>(b.mx.z) - b.mn.z;
         return dx * dy + dy * dz + dz * dx;
     };
+    // Optimal collapse (MOBILERT_COLLAPSE != "greedy"): the walk visits every wide node whose box
+    // the ray passes (no inner node is culled in the exact mode), each visit testing all its
+    // children, so the expected cost of a wide tree is proportional to the summed surface area of
+    // its wide nodes (the leaves are the same in every collapse).  Dynamic programming over the
+    // BVH2 (Ylitie et al. 2017): forest[i][j] = the least cost of covering node i's subtree with at
+    // most j trees, each tree root a leaf or a wide node; a wide node's children are the best
+    // forest of at most kWalkWidth trees under its two BVH2 children.
+    const char* collapseEnv = std::getenv("MOBILERT_COLLAPSE");
+    const bool optimal = collapseEnv == nullptr || std::string(collapseEnv) != "greedy";
+    constexpr int W1 = kWalkWidth + 1;
+    std::vector<double> forest;  // [i * W1 + j], j = 1..kWalkWidth
+    std::vector<int8_t> split;   // [i * W1 + j]: trees taken from the left child (0: node i itself);
+                                 // [i * W1]: the split of node i as a wide node
+    if (optimal) {
+        forest.assign(nodes.size() * W1, 0.0);  // leaves: 0 (the same in every tree)
+        split.assign(nodes.size() * W1, 0);
+        std::vector<std::pair<int32_t, bool>> post{{0, false}};
+        while (!post.empty()) {
+            const auto [i, done] = post.back();
+            post.pop_back();
+            if (!inner(i)) continue;
+            const size_t ui = static_cast<size_t>(i);
+            const int32_t l = nodes[ui].indexOffset, r = l + 1;
+            if (!done) {
+                post.push_back({i, true});
+                post.push_back({l, false});
+                post.push_back({r, false});
+                continue;
+            }
+            const size_t ul = static_cast<size_t>(l) * W1, ur = static_cast<size_t>(r) * W1;
+            auto best = [&](int j, int* k) {  // at most j trees split between the two children
+                double c = std::numeric_limits<double>::infinity();
+                for (int a = 1; a < j; ++a) {
+                    const double v = forest[ul + static_cast<size_t>(a)] + forest[ur + static_cast<size_t>(j - a)];
+                    if (v < c) {
+                        c = v;
+                        *k = a;
+                    }
+                }
+                return c;
+            };
+            int kw = 1;
+            const double asWide = area(i) + best(kWalkWidth, &kw);  // node i as a wide node
+            split[ui * W1] = static_cast<int8_t>(kw);
+            forest[ui * W1 + 1] = asWide;
+            for (int j = 2; j < W1; ++j) {
+                int k = 1;
+                const double c = best(j, &k);
+                const bool self = asWide <= c;
+                forest[ui * W1 + static_cast<size_t>(j)] = self ? asWide : c;
+                split[ui * W1 + static_cast<size_t>(j)] = static_cast<int8_t>(self ? 0 : k);
+            }
+        }
+    }
+    // the trees of node i's best forest of at most j (BVH2 indices, left to right)
+    std::function<void(int32_t, int, std::vector<int32_t>&)> trees = [&](int32_t i, int j, std::vector<int32_t>& out) {
+        const int k = inner(i) && j > 1 ? split[static_cast<size_t>(i) * W1 + static_cast<size_t>(j)] : 0;
+        if (k == 0) {
+            out.push_back(i);
+            return;
+        }
+        trees(nodes[static_cast<size_t>(i)].indexOffset, k, out);
+        trees(nodes[static_cast<size_t>(i)].indexOffset + 1, j - k, out);
+    };
     // collapse: the 4-wide node of BVH2 node i has up to four BVH2 descendants as children
     std::vector<std::array<int32_t, kWalkWidth>> kids;  // per walk node: BVH2 indices (-1: none)
     std::vector<int32_t> node4Of(nodes.size(), -1);
@@ -1064,7 +1130,13 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
         work.pop_back();
         const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
         std::vector<int32_t> c{l, l + 1};
-        while (c.size() < static_cast<size_t>(kWalkWidth)) {
+        if (optimal) {  // node i's best split into at most kWalkWidth trees
+            const int kw = split[static_cast<size_t>(i) * W1];
+            c.clear();
+            trees(l, kw, c);
+            trees(l + 1, kWalkWidth - kw, c);
+        }
+        while (!optimal && c.size() < static_cast<size_t>(kWalkWidth)) {
             int best = -1;
             double ba = -1.0;
             for (size_t k = 0; k < c.size(); ++k)

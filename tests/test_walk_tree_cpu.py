@@ -72,3 +72,35 @@ def test_walk_tree_holds_reference_leaves_with_margin(case):
     assert sorted(seen) == sorted(leaves.keys())
     # the root's union is the reference root box
     assert np.array_equal(union[int(root[0])].astype(np.float32), boxes[0])
+
+
+def _wide_node_area(nodes, grid, width):
+    """Summed surface area of the walk tree's wide nodes (each the union of its child boxes, from
+    the quantized words): the exact-mode walk's expected visit cost up to a constant."""
+    refs = nodes[:, 3 * width:].view(np.int32)
+    org, step = grid[:3].astype(np.float64), grid[3:].astype(np.float64)
+    w = nodes[:, :3 * width].astype(np.int64).reshape(len(nodes), width, 3)
+    lo = org + (w & 0xFFFF) * step
+    hi = org + (w >> 16) * step
+    used = (refs != EMPTY)[:, :, None]
+    lo = np.where(used, lo, np.inf).min(1)
+    hi = np.where(used, hi, -np.inf).max(1)
+    d = hi - lo
+    return float((d[:, 0] * d[:, 1] + d[:, 1] * d[:, 2] + d[:, 2] * d[:, 0]).sum())
+
+
+@pytest.mark.parametrize("case", [dict(scene="conference"), dict(scene="water"), dict(scene="teapot")])
+def test_optimal_collapse_beats_greedy(case, monkeypatch):
+    """The wide tree's collapse (mrt_scene.cpp toQuantizedBVH4) minimises the summed area of the
+    wide nodes by dynamic programming; the greedy collapse (MOBILERT_COLLAPSE=greedy) is one of
+    the trees it considers, so its sum is never larger (up to the quantization's outward step)."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, **case)
+    nodes, grid, root = m.walk_tree(cfg)
+    monkeypatch.setenv("MOBILERT_COLLAPSE", "greedy")
+    gnodes, ggrid, groot = m.walk_tree(cfg)
+    width = int(root[2])
+    assert int(root[1]) == int(groot[1])
+    a_opt, a_greedy = _wide_node_area(nodes, grid, width), _wide_node_area(gnodes, ggrid, width)
+    assert a_opt <= a_greedy * 1.0001, (a_opt, a_greedy)
+    assert len(nodes) <= len(gnodes)
