@@ -22,6 +22,8 @@ constexpr int kLdsStackMin = 8;     // per-thread stack entries (8 bytes) in LDS
 struct DScene {
     const float4* triGeom;     // 3 per triangle (BVH order): A, AB, AC  (xyz)
     const float4* triShade;    // 3 per triangle: nA (w = material index bits), nB, nC
+    const float4* triHead;     // 1 per triangle: nA, w = bits of ((material + 1) << 1 | flat): flat when
+                               // nA, nB and nC are the same bits (then triShade is not read)
     const GNode* triNodes;     // the reference tree (triRootRef)
     const QNode4* triQNodes;   // the walk tree (triRoot), 4-wide and quantized (QNode4)
     // the same nodes for the packet walk's scalar loads (mrt_trace_packet.hpp), 128 B each: the 24

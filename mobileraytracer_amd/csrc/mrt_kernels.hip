@@ -342,9 +342,15 @@ __device__ __forceinline__ HitGeom hitGeometry(const DScene& s, v3 o, v3 d, floa
     g.P = o + d * h.x;  // Triangle.cpp:99, Plane.cpp:62, Sphere.cpp:71
     g.src = code;
     if (kind == kTriangle) {
-        const float4* sh = s.triShade + 3 * j;
+        const float4 head = s.triHead[j];
+        const v3 nA = xyz(head);
+        v3 nB = nA, nC = nA;  // a flat triangle's normals are nA's bits
+        if ((__float_as_int(head.w) & 1) == 0) {
+            nB = xyz(s.triShade[3 * j + 1]);
+            nC = xyz(s.triShade[3 * j + 2]);
+        }
         const float w = 1.0F - h.y - h.z;  // Triangle.cpp:96-97
-        g.N = normalize(xyz(sh[0]) * w + xyz(sh[1]) * h.y + xyz(sh[2]) * h.z);
+        g.N = normalize(nA * w + nB * h.y + nC * h.z);
     } else if (kind == kPlane) {
         g.N = xyz(s.planes[2 * j]);
     } else {  // sphere
@@ -357,7 +363,7 @@ __device__ __forceinline__ HitGeom hitGeometry(const DScene& s, v3 o, v3 d, floa
 __device__ __forceinline__ int hitMaterial(const DScene& s, uint32_t code) {
     const uint32_t kind = primKind(code);
     const uint32_t j = primIndex(code);
-    if (kind == kTriangle) return __float_as_int(s.triShade[3 * j].w);
+    if (kind == kTriangle) return (__float_as_int(s.triHead[j].w) >> 1) - 1;
     if (kind == kPlane) return __float_as_int(s.planes[2 * j].w);
     return __float_as_int(s.spheres[2 * j + 1].x);
 }

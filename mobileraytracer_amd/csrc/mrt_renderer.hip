@@ -338,6 +338,15 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     }
     d.triShade = r->sceneMem.upload(v, st);
     v.clear();
+    // the 16-B head of each shading record (what k_shade gathers first): nA and
+    // ((material + 1) << 1 | flat), flat when the three normals are the same bits (every
+    // triangle of an OBJ without normals, OBJLoader.cpp:175-181), so nB and nC are not read
+    for (const HTriangle& t : sc.triangles) {
+        const bool flat = std::memcmp(&t.nA, &t.nB, sizeof(t.nA)) == 0 && std::memcmp(&t.nA, &t.nC, sizeof(t.nA)) == 0;
+        v.push_back(f4(t.nA, asFloat(static_cast<int32_t>((static_cast<uint32_t>(t.mat + 1) << 1) | (flat ? 1u : 0u)))));
+    }
+    d.triHead = r->sceneMem.upload(v, st);
+    v.clear();
     // textures: triangle texture coordinates, texture table and texels (textured scenes only)
     d.textured = 0;
     for (const HMaterial& m : sc.materials) d.textured |= (m.texId >= 0 && !sc.textures.empty()) ? 1 : 0;
