@@ -1200,7 +1200,9 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
         for (int c = 0; c < kWalkWidth; ++c) {
             const int32_t b = k4[static_cast<size_t>(c)];
             if (b < 0) {
-                q.q[3 * c] = q.q[3 * c + 1] = q.q[3 * c + 2] = 0u;
+                // an inverted box (min 65535, max 0 on every axis): the per-lane walk's near / far
+                // test (qslabNF) misses it for every quantOK ray, so it needs no slot check
+                q.q[3 * c] = q.q[3 * c + 1] = q.q[3 * c + 2] = 0xFFFFu;
                 q.ref[c] = kEmptyChild;
                 continue;
             }

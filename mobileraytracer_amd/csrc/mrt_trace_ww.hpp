@@ -362,10 +362,11 @@ __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, i
     for (int c = 0; c < W; ++c) {
         const uint32_t w0 = word(3 * c), w1 = word(3 * c + 1), w2 = word(3 * c + 2);
         rf[c] = static_cast<int>(word(3 * W + c));
-        const bool used = rf[c] != kEmptyChild;
-        if (count) cnt->nodes += used ? 1u : 0u;
+        if (count) cnt->nodes += rf[c] != kEmptyChild ? 1u : 0u;
         float t;
-        bool h = qslabNF(w0, w1, w2, sx, sy, sz, qa, qb, &t) && used;
+        // (an unused slot holds an inverted box, which this test misses: near > far on every axis,
+        // since |qb| <= 4 * 65535 |qa| for quantOK rays keeps fma(65535, qa, qb) != qb)
+        bool h = qslabNF(w0, w1, w2, sx, sy, sz, qa, qb, &t);
         if (cull) h = h && !(t > lim);
         n += h ? 1 : 0;
         key[c] = h ? sg * t : kInf;  // misses last
@@ -380,7 +381,8 @@ __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, i
 }
 
 // A ray may walk the quantized tree when the Quantizer's bound (mrt_scene.cpp) holds for it: every 1/d
-// component in [2^-40, 2^90] and the origin within 4 grid extents of the grid origin per axis.
+// component in [2^-40, 2^90], qa = step / d normal (>= 2^-100: an unused slot's inverted box then
+// always misses, innerStepQ) and the origin within 4 grid extents of the grid origin per axis.
 __device__ __forceinline__ bool quantOK(const DScene& s, v3 o, v3 inv) {
     if (s.qEnabled == 0) return false;
     const float ov[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
@@ -388,7 +390,7 @@ __device__ __forceinline__ bool quantOK(const DScene& s, v3 o, v3 inv) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float ai = fabsf(iv[a]);
-        ok = ok && ai >= 0x1p-40F && ai <= 0x1p90F &&
+        ok = ok && ai >= 0x1p-40F && ai <= 0x1p90F && ai * s.qgrid.step[a] >= 0x1p-100F &&
              fabsf(ov[a] - s.qgrid.origin[a]) <= 4.0F * 65535.0F * s.qgrid.step[a];
     }
     return ok;
