@@ -659,6 +659,67 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
     }
 }
 
+// The same allocation for one wave (no barrier: the fused level-1 kernel's waves run their
+// packets independently): one 64-bit atomic per wave and packet.
+__device__ __forceinline__ void waveAllocPair(unsigned long long* pair, int nLo, int nHi, int* baseLo, int* baseHi) {
+    const int lane = laneId();
+    const unsigned long long v =
+        (static_cast<unsigned long long>(static_cast<unsigned>(nHi)) << 32) | static_cast<unsigned>(nLo);
+    unsigned long long x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    const unsigned long long total = __shfl(x, 63, 64);
+    unsigned long long base = 0;
+    if (lane == 0 && total != 0) base = atomicAdd(pair, total);
+    base = __shfl(base, 0, 64);
+    const unsigned long long e = base + (x - v);
+    *baseLo = static_cast<int>(static_cast<unsigned>(e & 0xFFFFFFFFull));
+    *baseHi = static_cast<int>(static_cast<unsigned>(e >> 32));
+}
+
+// Level 1 fused: the packet walk shades each packet's hits as soon as the packet is done
+// (shadePrepare / shadeEmit of k_shade, the lean form), so the camera rays' shading runs inside
+// the latency-bound packet walk instead of as a separate launch after it.  Same vertex records,
+// shadow and child rays as k_shade (queue order differs, as it does between launches).
+template <int kShader>
+struct PacketShade {
+    const DScene* s;
+    Level lv, nx;
+    int* counters;
+    int level;
+    ShadeArgs a;
+    bool dead;
+    __device__ __forceinline__ void operator()(int i, bool valid, float4 o4, float4 d4, float4 h) const {
+        ShadeState v{};
+        if (valid) {
+            v = shadePrepare<kShader>(*s, o4, d4, h, lv.tree[i], level, a, make_float4(0.0F, 0.0F, 0.0F, -1.0F), s->mats,
+                                      s->lights);
+            if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
+        }
+        int childBase, shadowBase;
+        waveAllocPair(reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1)), valid ? v.nChild : 0,
+                      valid ? v.nShadow : 0, &childBase, &shadowBase);
+        if (valid) shadeEmit(*s, v, i, lv, nx, shadowBase, childBase, counters, a, dead, s->lights);
+    }
+};
+
+template <int kShader, int kCull>
+__global__ __launch_bounds__(kWalkThreads, 6) void k_trace_packet_shade(DScene s, Level lv, Level nx, int* counters,
+                                                                         int level, ShadeArgs a, int deadNext,
+                                                                         int2* gstack, int gdepth) {
+    __shared__ int2 ldsStack[kWalkStack * kWalkThreads];  // per-lane fallback walks only
+    __shared__ int waveStacks[kWalkThreads / 64][kPacketStack];
+    auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
+    const int count = min(counters[cntRays(level)], lv.cap);
+    int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
+    TravCount cnt{0u, 0u};
+    const PacketShade<kShader> post{&s, lv, nx, counters, level, a, deadNext != 0};
+    tracePacket<false, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, waveStacks[threadIdx.x / 64], post);
+}
+
 // Single-level shaders: the camera ray's shade() spawns no rays, so the result is final here.
 //   DepthMap (DepthMap.cpp:13-18), DiffuseMaterial (DiffuseMaterial.cpp:12-28),
 //   NoShadows (NoShadows.cpp:13-44: direct light without shadow rays + ambient).
@@ -1013,6 +1074,31 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
         return;
     }
     MRT_LAUNCH_WALK(k_shadow, 5);
+}
+
+bool launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
+                           const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext) {
+    if (s.fuseShade == 0 || level != 1 || s.accel != kAccBVH || s.packet == 0 || s.variant != 1 ||
+        (s.cull != kCullNone && s.cull != kCullExact) || (shader != kShaderWhitted && shader != kShaderPathTracer) ||
+        s.textured != 0 || a.stats != nullptr || s.leanShade == 0)
+        return false;
+    const int dead = deadNext ? 1 : 0;
+#define MRT_LAUNCH_FUSED(SH, C)                                                                                  \
+    do {                                                                                                         \
+        const int g = std::max(1, persistentGrid(k_trace_packet_shade<SH, C>, 12 + (SH == kShaderWhitted ? 0 : 1) + \
+                                                 (C == kCullExact ? 0 : 2), maxThreads));                         \
+        hipLaunchKernelGGL((k_trace_packet_shade<SH, C>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, nx, counters,  \
+                           level, a, dead, gstack, gdepth);                                                     \
+    } while (0)
+    if (shader == kShaderPathTracer) {
+        if (s.cull == kCullExact) MRT_LAUNCH_FUSED(kShaderPathTracer, kCullExact);
+        else MRT_LAUNCH_FUSED(kShaderPathTracer, kCullNone);
+    } else {
+        if (s.cull == kCullExact) MRT_LAUNCH_FUSED(kShaderWhitted, kCullExact);
+        else MRT_LAUNCH_FUSED(kShaderWhitted, kCullNone);
+    }
+#undef MRT_LAUNCH_FUSED
+    return true;
 }
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,

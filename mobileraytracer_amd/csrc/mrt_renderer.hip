@@ -453,6 +453,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.refill = 32;  // kWalkRefill
     d.leanShade = 1;
     d.packet = r->stackNeed <= kPacketStack ? 1 : 0;  // the packet walk's uniform stack must hold the tree's need
+    d.fuseShade = 1;
     d.matsFinite = 1;
     for (const HMaterial& m : sc.materials) {
         for (const v3 c : {m.Kd, m.Ks, m.Kt})
@@ -637,12 +638,18 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         }
         for (int l = 1; l <= nLevels; ++l) {
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-            if (!(skipLast && l == nLevels))
+            // level 1 without per-launch events or counting: the packet walk shades its own hits
+            const bool fused = !timing && !(skipLast && l == nLevels) && !(skipLastShade && l == nLevels) &&
+                               launchTraceShadeFused(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa,
+                                                     pp.gstack, r->gdepth, r->traceThreads, st,
+                                                     skipLastShade && l + 1 == nLevels);
+            if (fused) ++r->shadeLaunches;
+            if (!fused && !(skipLast && l == nLevels))
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting,
                             r->traceThreads, st);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
-            if (!(skipLastShade && l == nLevels)) {
+            if (!fused && !(skipLastShade && l == nLevels)) {
                 launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa,
                             shadePerCU > 0 ? r->cus * shadePerCU : r->workGrid, st,
                             skipLastShade && l + 1 == nLevels);
@@ -1161,6 +1168,10 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.packet = value;
         return 0;
     }
+    if (key == 17 && (value == 0 || value == 1)) {
+        r->ds.fuseShade = value;
+        return 0;
+    }
     if (key == 6 && value >= 0 && value <= 100) {
         r->shadowGridPct = value;
         return 0;
@@ -1329,6 +1340,7 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 10: *value = r->ds.leanShade; return 0;
         case 11: *value = r->shadeGridPerCU; return 0;
         case 16: *value = r->ds.packet; return 0;
+        case 17: *value = r->ds.fuseShade; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

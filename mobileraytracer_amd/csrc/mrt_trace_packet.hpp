@@ -61,10 +61,15 @@ __device__ __forceinline__ int uniformInt(int v) { return __builtin_amdgcn_readf
 
 // Closest hit of camera rays: rOs / rDs -> out = (t, u, v, primitive code).  (The any-hit form
 // for the level-1 shadow rays was built, exact and slower: DESIGN.md section 3.1.)
-template <bool kCount, int kCull, class Stack>
+// post(i, valid, o4, d4, hit): called by every lane of the wave after each packet (the fused
+// level-1 shading of k_trace_packet_shade; a no-op otherwise).
+struct NoPost {
+    __device__ __forceinline__ void operator()(int, bool, float4, float4, float4) const {}
+};
+template <bool kCount, int kCull, class Stack, class Post = NoPost>
 __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __restrict__ rOs,
                                             const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                            Stack& st, TravCount* cnt, int* waveStack) {
+                                            Stack& st, TravCount* cnt, int* waveStack, Post post = Post()) {
     static_assert(kCull == kCullNone || kCull == kCullExact, "packet walk: cull modes 0 and 3");
     ConstU32* const qnf = (ConstU32*)(s.triQNodesF);  // NOLINT: address-space casts
     ConstU32* const tg = (ConstU32*)(s.triGeom);      // NOLINT
@@ -79,8 +84,10 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
         const bool valid = i < count;
         v3 o{0, 0, 0}, d{1, 1, 1};
         uint32_t src = 0;
+        float4 o4 = make_float4(0.0F, 0.0F, 0.0F, 0.0F), d4 = o4;
         if (valid) {
-            const float4 o4 = rOs[i], d4 = rDs[i];
+            o4 = rOs[i];
+            d4 = rDs[i];
             o = xyz(o4);
             d = xyz(d4);
             src = fbits(d4.w);
@@ -215,10 +222,11 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
             }
             ref = sp > 0 ? uniformInt(waveStack[--sp]) : kRefDone;
         }
+        float4 hit = make_float4(0.0F, 0.0F, 0.0F, 0.0F);
         if (valid) {
             if (!packed) {
                 const Best f = closestHit(s, o, d, src, st, cnt);
-                out[i] = make_float4(f.t, f.u, f.v, bitsf(f.code));
+                hit = make_float4(f.t, f.u, f.v, bitsf(f.code));
             } else {
                 for (int j = 0; j < s.nLights; ++j) {  // Shader.cpp:166-171
                     const float4* l = s.lights + 4 * j;
@@ -242,10 +250,12 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
                     u = 0.0F;
                     v = 0.0F;
                 }
-                out[i] = make_float4(bt, u, v, bitsf(bcode));
+                hit = make_float4(bt, u, v, bitsf(bcode));
             }
+            out[i] = hit;
             if (kCount) ++cnt->rays;
         }
+        post(i, valid, o4, d4, hit);
     }
 }
 

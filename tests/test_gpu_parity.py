@@ -389,6 +389,34 @@ def test_packet_walk_matches_oracle_and_is_invariant(oracle_mod):
         assert np.array_equal(t.view(np.int32), ot.view(np.int32))
 
 
+def test_fused_level1_shading_is_invariant():
+    """Level 1's packet walk shading its own hits (tuning key 17, on by default:
+    k_trace_packet_shade, one launch instead of the walk and k_shade) gives the separate
+    launches' bitmap, ray counts and primary hits: Whitted and PathTracer, 2 light samples,
+    both cull modes that walk packets, a textured scene (which keeps the separate launches)."""
+    import mobileraytracer_amd as m
+    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+             make_cfg(128, 128, shader=1, scene="water", max_depth=4),
+             make_cfg(96, 96, shader=2, scene="water", spp=2, max_depth=4, spl=2),
+             make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3),
+             make_cfg(64, 64, shader=2, spp=3, max_depth=6), make_cfg(96, 64, shader=1, sceneIndex=3))
+    for cfg in cases:
+        outs = []
+        with m.Renderer(cfg) as r:
+            assert r.get_tuning(17) == 1
+            for fuse, cull in ((1, 3), (0, 3), (1, 0), (0, 0)):
+                r.set_tuning(17, fuse)
+                r.set_tuning(2, cull)
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"]), r.primary_hits()))
+        for other in outs[1:]:
+            assert np.array_equal(outs[0][0], other[0]), cfg
+            assert outs[0][1:4] == other[1:4], cfg
+            assert all(np.array_equal(a, b) for a, b in zip(outs[0][4], other[4])), cfg
+
+
 def test_python_plugin_setters():
     """Renderer.set_camera / set_pixel_sampler (mrt_set_camera, mrt_set_pixel_sampler, the C++
     facade's plugins): re-setting the built-in camera (Scenes.cpp: spheres' orthographic,
