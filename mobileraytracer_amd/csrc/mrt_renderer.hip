@@ -619,10 +619,10 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                               : pathsPerLane < 4.0  ? 50
                               : pathsPerLane < 8.0  ? 75
                                                     : 70;
-        // k_shade's grid: where a lane sees many paths a deeper grid hides the shading's gathers
-        // beside the concurrent shadow walk (14 / 28 per CU: N = 1 13.55 / 13.48 ms, N = 4 shard
-        // 4.10 / 4.07 ms); the smallest shards keep 14 (N = 8: 2.55 / 2.56 ms)
-        const int shadePerCU = r->shadeGridPerCU >= 0 ? r->shadeGridPerCU : pathsPerLane < 4.0 ? 14 : 28;
+        // k_shade's grid: 14 workgroups per CU.  (Round 2: 28 where a lane sees >= 4 paths, N = 1
+        // 13.55 / 13.48 ms at 14 / 28; round 3, with the materials in LDS and the 16-B shading
+        // record head, 14 everywhere: N = 1 15.47 / 15.53 ms, 20 / 36: 15.52 / 15.54 ms.)
+        const int shadePerCU = r->shadeGridPerCU >= 0 ? r->shadeGridPerCU : 14;
         // refill threshold: larger batches where a lane sees few paths (a small shard: the tail
         // dominates; C4 shard at N = 8: 24 / 32 / 40 -> 2.68 / 2.64 / 2.61 ms), smaller where it
         // sees many (N = 1: 13.77 / 13.86 / 13.88 ms)
