@@ -240,6 +240,12 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     r.set_tuning(3, args.overlap)
+    # MRT_BENCH_TUNING="17=0,...": tuning keys for profiling runs (tools/pmc_run.sh profiles the
+    # timed frames with level 1 unfused, so that its PMC averages cover the same walk launches as
+    # the serialised roofline frames)
+    for kv in filter(None, os.environ.get("MRT_BENCH_TUNING", "").split(",")):
+        k, v = kv.split("=")
+        r.set_tuning(int(k), int(v))
     info = r.scene_info()
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
