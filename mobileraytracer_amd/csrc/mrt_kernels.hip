@@ -102,10 +102,9 @@ __device__ __forceinline__ void slotToXY(const PixelMap& m, int slot, int* x, in
 }
 // rect.z = unit width (columns), rect.w = unit height (rows)
 
-__global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* counters) {
-    const int p = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
-    if (p == 0) counters[cntRays(1)] = a.nPaths;
-    if (p >= a.nPaths) return;
+// Camera ray of path p (Renderer.cpp:108-111, 131-140 with Perspective / Orthographic::generateRay):
+// origin (w = path key bits), direction (w = kNoPrim: no source primitive).
+__device__ __forceinline__ void cameraRay(const RaygenArgs& a, int p, float4* o4, float4* d4) {
     const int slot = a.slotBase + p / a.spp;
     const int s = p % a.spp;
     int x, y;
@@ -145,8 +144,18 @@ __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* cou
         origin = c.position;
         dir = normalize(dest - c.position);
     }
-    lv.rO[p] = make_float4(origin.x, origin.y, origin.z, bitsf(key));
-    lv.rD[p] = make_float4(dir.x, dir.y, dir.z, bitsf(kNoPrim));
+    *o4 = make_float4(origin.x, origin.y, origin.z, bitsf(key));
+    *d4 = make_float4(dir.x, dir.y, dir.z, bitsf(kNoPrim));
+}
+
+__global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* counters) {
+    const int p = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p == 0) counters[cntRays(1)] = a.nPaths;
+    if (p >= a.nPaths) return;
+    float4 o4, d4;
+    cameraRay(a, p, &o4, &d4);
+    lv.rO[p] = o4;
+    lv.rD[p] = d4;
     lv.tree[p] = 1u;
 }
 
@@ -694,9 +703,8 @@ struct PacketShade {
     bool dead;
     __device__ __forceinline__ void operator()(int i, bool valid, float4 o4, float4 d4, float4 h) const {
         ShadeState v{};
-        if (valid) {
-            v = shadePrepare<kShader>(*s, o4, d4, h, lv.tree[i], level, a, make_float4(0.0F, 0.0F, 0.0F, -1.0F), s->mats,
-                                      s->lights);
+        if (valid) {  // (tree code 1: a camera ray)
+            v = shadePrepare<kShader>(*s, o4, d4, h, 1u, level, a, make_float4(0.0F, 0.0F, 0.0F, -1.0F), s->mats, s->lights);
             if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
         }
         int childBase, shadowBase;
@@ -706,18 +714,30 @@ struct PacketShade {
     }
 };
 
+// ... and its camera rays are generated where they are walked (cameraRay, k_raygen's function):
+// level 1's ray records are not written or read
+struct PacketRays {
+    const RaygenArgs* a;
+    __device__ __forceinline__ void operator()(int i, float4* o4, float4* d4) const { cameraRay(*a, i, o4, d4); }
+};
+
+#ifndef MRT_FUSED_WAVES
+#define MRT_FUSED_WAVES 6
+#endif
 template <int kShader, int kCull>
-__global__ __launch_bounds__(kWalkThreads, 6) void k_trace_packet_shade(DScene s, Level lv, Level nx, int* counters,
+__global__ __launch_bounds__(kWalkThreads, MRT_FUSED_WAVES) void k_trace_packet_shade(DScene s, Level lv, Level nx, int* counters,
                                                                          int level, ShadeArgs a, int deadNext,
-                                                                         int2* gstack, int gdepth) {
+                                                                         int2* gstack, int gdepth, RaygenArgs ra) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];  // per-lane fallback walks only
     __shared__ int waveStacks[kWalkThreads / 64][kPacketStack];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
-    const int count = min(counters[cntRays(level)], lv.cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) counters[cntRays(level)] = ra.nPaths;  // (k_raygen's count)
+    const int count = min(ra.nPaths, lv.cap);
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
     const PacketShade<kShader> post{&s, lv, nx, counters, level, a, deadNext != 0};
-    tracePacket<false, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, waveStacks[threadIdx.x / 64], post);
+    tracePacket<false, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, waveStacks[threadIdx.x / 64], post,
+                              PacketRays{&ra});
 }
 
 // Single-level shaders: the camera ray's shade() spawns no rays, so the result is final here.
@@ -1076,19 +1096,22 @@ void launchShadow(const DScene& s, const Level& lv, int* counters, int level, in
     MRT_LAUNCH_WALK(k_shadow, 5);
 }
 
-bool launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
-                           const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext) {
-    if (s.fuseShade == 0 || level != 1 || s.accel != kAccBVH || s.packet == 0 || s.variant != 1 ||
-        (s.cull != kCullNone && s.cull != kCullExact) || (shader != kShaderWhitted && shader != kShaderPathTracer) ||
-        s.textured != 0 || a.stats != nullptr || s.leanShade == 0)
-        return false;
+bool canFuseLevel1(int shader, const DScene& s, const ShadeArgs& a) {
+    return s.fuseShade != 0 && s.accel == kAccBVH && s.packet != 0 && s.variant == 1 &&
+           (s.cull == kCullNone || s.cull == kCullExact) && (shader == kShaderWhitted || shader == kShaderPathTracer) &&
+           s.textured == 0 && a.stats == nullptr && s.leanShade != 0;
+}
+
+void launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
+                           const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext,
+                           const RaygenArgs& ra) {
     const int dead = deadNext ? 1 : 0;
 #define MRT_LAUNCH_FUSED(SH, C)                                                                                  \
     do {                                                                                                         \
         const int g = std::max(1, persistentGrid(k_trace_packet_shade<SH, C>, 12 + (SH == kShaderWhitted ? 0 : 1) + \
                                                  (C == kCullExact ? 0 : 2), maxThreads));                         \
         hipLaunchKernelGGL((k_trace_packet_shade<SH, C>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, nx, counters,  \
-                           level, a, dead, gstack, gdepth);                                                     \
+                           level, a, dead, gstack, gdepth, ra);                                                 \
     } while (0)
     if (shader == kShaderPathTracer) {
         if (s.cull == kCullExact) MRT_LAUNCH_FUSED(kShaderPathTracer, kCullExact);
@@ -1098,7 +1121,6 @@ bool launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const L
         else MRT_LAUNCH_FUSED(kShaderWhitted, kCullNone);
     }
 #undef MRT_LAUNCH_FUSED
-    return true;
 }
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,

@@ -124,10 +124,13 @@ void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st, int gridPct = 100);
 // deadNext: level + 1 is the depth-capped last level (its rays are counted, never written)
-// Level 1's walk and shading in one launch (k_trace_packet_shade) where it applies (DScene::fuseShade,
-// the packet walk, Whitted / PathTracer, the lean shading); returns false (nothing launched) otherwise.
-bool launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
-                           const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext);
+// Level 1's ray generation, walk and shading in one launch (k_trace_packet_shade) where it applies
+// (canFuseLevel1: DScene::fuseShade, the packet walk, Whitted / PathTracer, the lean shading, no
+// counting); it replaces launchRaygen + launchTrace + launchShade of level 1.
+bool canFuseLevel1(int shader, const DScene& s, const ShadeArgs& a);
+void launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
+                           const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext,
+                           const RaygenArgs& ra);
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st, bool deadNext = false);
 // deadChildren: level + 1 is the depth-capped last level, whose results are all zero; its

@@ -605,7 +605,10 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.sppTotal = r->cfg.samplesPixel;
         setPixelSampler(r, &ra);
         ra.sampleBase = sampleBase;
-        launchRaygen(ra, pp.levels[1], pp.counters, st);
+        // level 1 fused (ray generation, packet walk and shading in one launch) where it applies
+        const bool fuseL1 = !timing && nLevels >= 1 && !(skipLast && nLevels == 1) &&
+                            !(skipLastShade && nLevels == 1) && canFuseLevel1(shader, r->ds, sa);
+        if (!fuseL1) launchRaygen(ra, pp.levels[1], pp.counters, st);
         // With few paths per resident walk lane (a small shard: C4 at N >= 4) the levels are short
         // and tail-bound, and a full-width shadow walk starves the next level's shading of CUs;
         // a narrower shadow grid leaves them room (C4 shard at N = 8: 2.92 -> 2.83 ms; at N = 1 the
@@ -638,12 +641,14 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         }
         for (int l = 1; l <= nLevels; ++l) {
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-            // level 1 without per-launch events or counting: the packet walk shades its own hits
-            const bool fused = !timing && !(skipLast && l == nLevels) && !(skipLastShade && l == nLevels) &&
-                               launchTraceShadeFused(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa,
-                                                     pp.gstack, r->gdepth, r->traceThreads, st,
-                                                     skipLastShade && l + 1 == nLevels);
-            if (fused) ++r->shadeLaunches;
+            // level 1 without per-launch events or counting: the packet walk generates its camera rays
+            // and shades its own hits
+            const bool fused = fuseL1 && l == 1;
+            if (fused) {
+                launchTraceShadeFused(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, pp.gstack,
+                                      r->gdepth, r->traceThreads, st, skipLastShade && l + 1 == nLevels, ra);
+                ++r->shadeLaunches;
+            }
             if (!fused && !(skipLast && l == nLevels))
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting,
                             r->traceThreads, st);

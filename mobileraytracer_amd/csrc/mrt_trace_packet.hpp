@@ -14,6 +14,8 @@
 // Cull modes 0 (none) and 3 (exact) only: neither culls an inner node.
 #pragma once
 
+#include <type_traits>
+
 #include "mrt_trace_ww.hpp"
 
 namespace mrt {
@@ -66,10 +68,15 @@ __device__ __forceinline__ int uniformInt(int v) { return __builtin_amdgcn_readf
 struct NoPost {
     __device__ __forceinline__ void operator()(int, bool, float4, float4, float4) const {}
 };
-template <bool kCount, int kCull, class Stack, class Post = NoPost>
+// rays(i, &o4, &d4): ray i (the fused kernel generates camera rays; otherwise rOs / rDs are read)
+struct NoRays {
+    __device__ __forceinline__ void operator()(int, float4*, float4*) const {}
+};
+template <bool kCount, int kCull, class Stack, class Post = NoPost, class Rays = NoRays>
 __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __restrict__ rOs,
                                             const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                            Stack& st, TravCount* cnt, int* waveStack, Post post = Post()) {
+                                            Stack& st, TravCount* cnt, int* waveStack, Post post = Post(),
+                                            Rays rays = Rays()) {
     static_assert(kCull == kCullNone || kCull == kCullExact, "packet walk: cull modes 0 and 3");
     ConstU32* const qnf = (ConstU32*)(s.triQNodesF);  // NOLINT: address-space casts
     ConstU32* const tg = (ConstU32*)(s.triGeom);      // NOLINT
@@ -86,8 +93,12 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
         uint32_t src = 0;
         float4 o4 = make_float4(0.0F, 0.0F, 0.0F, 0.0F), d4 = o4;
         if (valid) {
-            o4 = rOs[i];
-            d4 = rDs[i];
+            if constexpr (std::is_same<Rays, NoRays>::value) {
+                o4 = rOs[i];
+                d4 = rDs[i];
+            } else {
+                rays(i, &o4, &d4);
+            }
             o = xyz(o4);
             d = xyz(d4);
             src = fbits(d4.w);

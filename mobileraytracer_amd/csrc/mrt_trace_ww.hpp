@@ -330,11 +330,11 @@ __device__ __forceinline__ void sortChildren(float* k, int* r) {
 // the rays admitted to this tree a child passes whenever a leaf below passes the reference test,
 // and its entry is at most that leaf's: the visit set is a superset of the reference's, and the
 // leaves are tested exactly before their triangles (traceWhileWhile).  The hit children are
-// visited in order of entry (order 0: nearest first; 1: farthest first): the first now, the
-// others pushed.
-template <int kCull, class Stack>
+// visited in order of entry (kOrder 0: nearest first; 1: farthest first, a compile-time choice
+// made per wave from the uniform DScene::anyOrder): the first now, the others pushed.
+template <int kCull, int kOrder, class Stack>
 __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, int top, int ref, v3 qa, v3 qb,
-                                          float lim, Stack& st, TravCount* cnt, bool count, int order) {
+                                          float lim, Stack& st, TravCount* cnt, bool count) {
     constexpr int W = kWalkWidth;
     constexpr bool cull = kCull != kCullNone;
     int4 raw[W];
@@ -354,7 +354,7 @@ __device__ __forceinline__ int innerStepQ(BufRes qnodes, const QNode4* ldsTop, i
     };
     constexpr float kInf = __builtin_inff();
     const uint32_t sx = nearFarShift(qa.x), sy = nearFarShift(qa.y), sz = nearFarShift(qa.z);
-    const float sg = order == 0 ? 1.0F : -1.0F;  // sort keys: the entry (nearest first) or its negation
+    constexpr float sg = kOrder == 0 ? 1.0F : -1.0F;  // sort keys: the entry (nearest first) or its negation
     float key[W];
     int rf[W];
     int n = 0;
@@ -690,7 +690,8 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             const bool finite = __ballot(!finiteInv(inv)) == 0;
             const int order = kAny ? s.anyOrder : 0;
             ref = refTree ? innerStep<kInner>(nodeBuf, ref, o, d, inv, curLim, st, cnt, kCount, finite, order)
-                          : innerStepQ<kInner>(qBuf, ldsTop, top, ref, qa, qb, curLim, st, cnt, kCount, order);
+                          : order == 0 ? innerStepQ<kInner, 0>(qBuf, ldsTop, top, ref, qa, qb, curLim, st, cnt, kCount)
+                                       : innerStepQ<kInner, 1>(qBuf, ldsTop, top, ref, qa, qb, curLim, st, cnt, kCount);
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
                 ref = popCulled(st, curLim, cull);
