@@ -1,4 +1,7 @@
-"""Prints the kernel timeline of the last frame in a rocprofv3 kernel trace (CSV or rocpd .db)."""
+"""Prints the kernel timeline of the last product frame in a rocprofv3 kernel trace (CSV or rocpd
+.db): frames start at k_raygen or, with level 1 fused, at k_trace_packet_shade; the last frame that
+starts with the fused kernel is a timed frame of bench.py (its profiling frames after the timed
+ones run level 1 unfused), else the last frame."""
 import csv, sqlite3, sys
 
 
@@ -14,7 +17,10 @@ def rows_of(path):
 
 
 rows = sorted(rows_of(sys.argv[1]), key=lambda r: r[1])
-first = [i for i, r in enumerate(rows) if "k_raygen" in r[0]][-1]
+starts = [i for i, r in enumerate(rows) if "k_raygen" in r[0] or "k_trace_packet_shade" in r[0]]
+fused = [i for i in starts if "k_trace_packet_shade" in rows[i][0]]
+first = fused[-1] if fused else starts[-1]
+end = next((i for i in starts if i > first), len(rows))
 t0 = rows[first][1]
-for n, s, e, q in rows[first:]:
+for n, s, e, q in rows[first:end]:
     print(f"{(s - t0) / 1e3:8.1f} {(e - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} q{q} {n[:60]}")
