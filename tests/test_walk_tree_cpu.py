@@ -104,3 +104,31 @@ def test_optimal_collapse_beats_greedy(case, monkeypatch):
     a_opt, a_greedy = _wide_node_area(nodes, grid, width), _wide_node_area(gnodes, ggrid, width)
     assert a_opt <= a_greedy * 1.0001, (a_opt, a_greedy)
     assert len(nodes) <= len(gnodes)
+
+
+@pytest.mark.parametrize("case", [dict(scene="conference"), dict(scene="water"), dict(sceneIndex=3)])
+def test_unused_slots_hold_inverted_boxes(case):
+    """An unused child slot of the walk tree holds min 65535 / max 0 on every axis
+    (mrt_scene.cpp toQuantizedBVH4), which the kernel's near / far slab test (qslabNF) misses
+    without a slot check: near > far on the axis for every ray with |qb| <= 4 * 65535 |qa| and a
+    normal qa (quantOK), checked here on random such rays with the fma's exact value rounded once."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, **case)
+    nodes, grid, root = m.walk_tree(cfg)
+    if int(root[0]) < 0:
+        return
+    width = int(root[2])
+    refs = nodes[:, 3 * width:].view(np.int32)
+    words = nodes[:, :3 * width].reshape(len(nodes), width, 3)
+    empty = refs == EMPTY
+    assert np.all(words[empty] == 0x0000FFFF)
+    assert np.all((words[~empty] & 0xFFFF) <= (words[~empty] >> 16))  # used slots: min <= max
+    rng = np.random.default_rng(5)
+    qa = (rng.choice([-1.0, 1.0], 20000) * 2.0 ** rng.uniform(-100, 60, 20000)).astype(np.float32)
+    qb = (qa.astype(np.float64) * rng.uniform(-4 * 65535, 4 * 65535, 20000)).astype(np.float32)
+    f32 = lambda x: x.astype(np.float32)  # noqa: E731  (products of a 16-bit q and qa are exact in float64)
+    lo = f32(65535.0 * qa.astype(np.float64) + qb.astype(np.float64))  # the min plane's fma
+    hi = f32(0.0 * qa.astype(np.float64) + qb.astype(np.float64))      # the max plane's fma
+    near = np.where(qa > 0, lo, hi)  # the rotated word: near = min plane for qa > 0, else max
+    far = np.where(qa > 0, hi, lo)
+    assert np.all(near > far)
