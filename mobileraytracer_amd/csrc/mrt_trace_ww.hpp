@@ -2,9 +2,9 @@
 //
 // Same reachability, culling and tie rules as traverse<> in mrt_device.hpp (so results are
 // identical, tested), organised for SIMD efficiency on CDNA's 64-lane waves:
-//   * inner nodes are walked until (nearly) every active lane has found a leaf (leaves are
-//     postponed one at a time), then the lanes test their leaves together: inner-node and leaf
-//     code no longer alternate inside one wave iteration;
+//   * inner nodes are walked until EVERY active lane has found a leaf (leaves are postponed
+//     one at a time), then all lanes test their leaves together: inner-node and leaf code no
+//     longer alternate inside one wave iteration;
 //   * lanes whose ray has finished take a new ray (one wave-aggregated atomic per refill, once
 //     kRefill lanes are idle) instead of idling until the slowest ray of a 64-ray batch is done;
 //   * 8 work cursors per level, one per XCD group of workgroups (blockIdx % 8), each over a
@@ -15,10 +15,10 @@
 // Planes / spheres (tiny BVHs, empty for OBJ scenes) are tested at ray fetch with the simple
 // walker, area lights when the triangle walk ends, in the reference's category order.
 //
-// Measured alternatives (removed from the build after A/B on MI355X): 8-wide
-// nodes, compressed 32-B and binary16 nodes, tail assist, trimmed grids, last-occluder shadow
-// test, one launch for all levels, ray sorting, concurrent chunk pipelines, certified culls of
-// inner nodes - all result-invariant and all slower than this walk on the C4 frame.
+// Measured alternatives (removed from the build after A/B on MI355X): 4-wide
+// nodes, compressed 32-B nodes, tail assist, trimmed grids, last-occluder shadow test, one
+// launch for all levels, ray sorting, concurrent chunk pipelines - all result-invariant and all
+// slower than this walk on the C4 frame.
 #pragma once
 
 #include "mrt_device.hpp"
