@@ -111,26 +111,59 @@ def cpu_baseline(args, scene):
             "rays_counted": "built (every Ray constructed, Ray.cpp:25-28)"}
 
 
+def strip_comments(src):
+    """C++ source without its comments and with whitespace runs collapsed: the code a compiler
+    sees (string and character literals kept verbatim), so documentation edits leave the kernel
+    source stamp unchanged."""
+    out, i, n = [], 0, len(src)
+    while i < n:
+        c = src[i]
+        if c in "\"'":
+            j = i + 1
+            while j < n and src[j] != c:
+                j += 2 if src[j] == "\\" else 1
+            out.append(src[i:j + 1])
+            i = j + 1
+        elif src.startswith("//", i):
+            j = src.find("\n", i)
+            i = n if j < 0 else j
+        elif src.startswith("/*", i):
+            j = src.find("*/", i + 2)
+            i = n if j < 0 else j + 2
+            out.append(" ")
+        else:
+            out.append(c)
+            i += 1
+    return " ".join("".join(out).split())
+
+
 def kernel_source_stamp():
-    """sha256 of the HIP sources the walk / shading kernels are built from: a PMC profile is
-    reported only while it was measured on this exact code."""
+    """sha256 of the HIP sources the walk / shading kernels are built from, comments stripped: a
+    PMC profile is reported only while it was measured on this exact code."""
     import hashlib
     h = hashlib.sha256()
     d = os.path.join(HERE, "mobileraytracer_amd", "csrc")
     for name in sorted(os.listdir(d)):
         if name.endswith((".hip", ".hpp")):
-            with open(os.path.join(d, name), "rb") as f:
-                h.update(name.encode() + b"\0" + f.read())
+            with open(os.path.join(d, name), encoding="utf-8") as f:
+                h.update(name.encode() + b"\0" + strip_comments(f.read()).encode())
     return h.hexdigest()
 
 
-PMC_PROFILE = os.path.join("profiles", "r03_pmc_traffic.json")
+PMC_PROFILE = os.path.join("profiles", "r04_pmc_traffic.json")
 
 
-def pmc_traffic():
+def workload_key(args, shard_of):
+    """What a PMC profile must have measured to be reported on this bench line."""
+    return {"width": args.width, "height": args.height, "spp": args.spp, "max_depth": args.max_depth,
+            "shader": args.shader, "shard_of": shard_of}
+
+
+def pmc_traffic(workload):
     """Bytes beyond L2 per launch for each kernel from the committed rocprofv3 PMC summary
     (tools/pmc_run.sh: FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md),
-    used only when its kernel-source stamp equals this build's (else stale: traffic null)."""
+    used only when its kernel-source stamp equals this build's AND it profiled this workload (else
+    traffic null: a profile of other kernels or of another frame size is never reported)."""
     path = os.path.join(HERE, PMC_PROFILE)
     if not os.path.exists(path):
         return {}, {"file": PMC_PROFILE, "status": "absent"}
@@ -140,67 +173,100 @@ def pmc_traffic():
     if j.get("kernel_source_sha256") != stamp:
         return {}, {"file": PMC_PROFILE, "status": "stale (measured on other kernel sources)",
                     "profile_sha256": j.get("kernel_source_sha256"), "build_sha256": stamp}
+    if j.get("workload") != workload:
+        return {}, {"file": PMC_PROFILE, "status": "other workload (profiled: %s)" % (j.get("workload"),)}
     return j.get("bytes_beyond_l2_per_launch", {}), {"file": PMC_PROFILE, "status": "current",
-                                                     "kernel_source_sha256": stamp}
+                                                     "kernel_source_sha256": stamp, "workload": workload}
 
 
 def kernel_roofline(r, step):
-    """Per-kernel algorithmic bytes and serialised launch durations (outside the timed region)."""
+    """Per-kernel algorithmic bytes and serialised launch durations (outside the timed region).
+
+    Kernels as the timed frames run them: level 1 is ONE launch, k_trace_packet_shade (camera rays
+    generated, packet-walked and shaded); k_trace is the per-lane closest-hit walk of levels 2 ..
+    maxDepth (level maxDepth + 1 is not walked); k_shade shades levels 2 .. maxDepth; k_shadow walks
+    the shadow rays of every level.  Bytes per level come from one counting frame (which runs level
+    1 as separate launches: the same walk, counted), durations from two frames with the shadow
+    stream serialised and HIP events around every launch on the stream it runs on."""
     r.set_profiling(counting=True)
     step()
     c = r.frame_stats()
     r.set_tuning(3, 0)  # shadow rays on the render stream: every launch timed alone
     r.set_profiling(timing=True)
-    tr_ms = sh_ms = sd_ms = 0.0
-    tr_n = sh_n = sd_n = 0
-    for _ in range(2):
+    keys = ("traceMs", "shadowMs", "shadeMs", "fusedMs", "traceLaunches", "shadowLaunches", "shadeLaunches",
+            "fusedLaunches")
+    t = dict.fromkeys(keys, 0)
+    frames = 2
+    for _ in range(frames):
         step()
-        t = r.frame_stats()
-        tr_ms += t["traceMs"]; sh_ms += t["shadowMs"]; sd_ms += t["shadeMs"]
-        tr_n += t["traceLaunches"]; sh_n += t["shadowLaunches"]; sd_n += t["shadeLaunches"]
+        f = r.frame_stats()
+        for k in keys:
+            t[k] += f[k]
     r.set_profiling()
     r.set_tuning(3, 1)
-    walked, shadows, shaded = c["walkedRays"], c["shadowRays"], c["shadedVertices"]
+    md = r.config.maxDepth
+    rays = c["levelRays"]          # index l - 1: rays of depth l
+    shadows = c["levelShadowRays"]
+    nodes, tris, leaves = c["levelNodeRecords"], c["levelTriTests"], c["levelLeafRecords"]
+    shaded = c["levelShadedVertices"]
+    fused = t["fusedLaunches"] > 0
+    walk_levels = range(1 if fused else 0, md)  # k_trace: depths 2 (1 unfused) .. maxDepth
     # k_trace: per ray 32 (ray read: origin, direction) + 16 (hit write) + 32 per node record + 36 per
-    # triangle test; k_shadow: 32 (ray read) + 4 (flag write) + the same gathers (SURVEY.md 8(d))
-    trace_b = 48.0 * walked + 32.0 * c["nodeRecords"] + 36.0 * c["triTests"]
-    shadow_b = 36.0 * shadows + 32.0 * c["shadowNodeRecords"] + 36.0 * c["shadowTriTests"]
-    # the bytes the kernels' load instructions actually request: 16 per child record of the
-    # quantized 4-wide tree (a 64-B node holds four), 48 per walk-tree leaf record (exact box +
-    # certified-cull record), 36 per triangle test (three 12-B loads: A, AB, AC)
-    trace_f = 48.0 * walked + 16.0 * c["nodeRecords"] + 48.0 * c["leafRecords"] + 36.0 * c["triTests"]
-    shadow_f = 36.0 * shadows + 16.0 * c["shadowNodeRecords"] + 48.0 * c["shadowLeafRecords"] + 36.0 * c["shadowTriTests"]
-    # k_shade (DESIGN.md section 3): per vertex 52 read (origin, direction, hit, tree code) + 16
-    # written (vertex or result record); per shaded hit 48 (normals, material id) + 64 (material)
-    # + 64 (light) + 32 (the vertex's six draws, one compact block); per shadow ray 48 written;
-    # per child ray 36 written
-    levels = c["levelRays"]
-    shaded_rays = sum(levels[:r.config.maxDepth])  # levels 1..maxDepth (the last is not shaded)
-    children = sum(levels[1:r.config.maxDepth + 1])
-    shade_b = 68.0 * shaded_rays + 208.0 * shaded + 48.0 * shadows + 36.0 * children
-    fr = max(1, 2)
+    # triangle test (SURVEY.md 8(d)); `fetched`: the bytes the load instructions request - 16 per child
+    # record of the quantized 4-wide tree, 48 per walk-tree leaf record (exact box + certified-cull
+    # record), 36 per triangle test (three 12-B loads: A, AB, AC)
+    trace_b = sum(48.0 * rays[l] + 32.0 * nodes[l] + 36.0 * tris[l] for l in walk_levels)
+    trace_f = sum(48.0 * rays[l] + 16.0 * nodes[l] + 48.0 * leaves[l] + 36.0 * tris[l] for l in walk_levels)
+    # k_shadow: 32 (ray read) + 4 (flag write) + the same gathers
+    n_sh = c["shadowRays"]
+    shadow_b = 36.0 * n_sh + 32.0 * c["shadowNodeRecords"] + 36.0 * c["shadowTriTests"]
+    shadow_f = 36.0 * n_sh + 16.0 * c["shadowNodeRecords"] + 48.0 * c["shadowLeafRecords"] + 36.0 * c["shadowTriTests"]
 
-    def entry(name, frame_bytes, ms, launches, fetched_bytes=None):
-        launches_pf = launches / fr
+    # shading of depth l (DESIGN.md section 3): per ray 52 read (origin, direction, hit, tree code) + 16
+    # written (vertex or result record); per shaded hit 48 (normals, material id) + 64 (material) + 64
+    # (light) + 32 (the vertex's six draws, one compact block); per shadow ray 48 written; per child ray
+    # 36 written (not for the depth-capped level's children, whose payloads are never written)
+    def shade_bytes(l, read_rays=True):
+        child = 36.0 * rays[l + 1] if l + 1 < md else 0.0
+        return (68.0 if read_rays else 16.0) * rays[l] + 208.0 * shaded[l] + 48.0 * shadows[l] + child
+
+    shade_levels = range(1 if fused else 0, md)
+    shade_b = sum(shade_bytes(l) for l in shade_levels)
+    # the fused level-1 launch: the packet walk's gathers (no ray record read: the rays are generated
+    # in the kernel; no hit record written: it is shaded in the same wave) + level 1's shading
+    fused_b = 32.0 * nodes[0] + 36.0 * tris[0] + shade_bytes(0, read_rays=False)
+    fused_f = 16.0 * nodes[0] + 48.0 * leaves[0] + 36.0 * tris[0] + shade_bytes(0, read_rays=False)
+
+    def entry(frame_bytes, ms, launches, fetched_bytes=None, levels=None):
+        launches_pf = launches / frames
         per_launch = frame_bytes / max(1.0, launches_pf)
         avg_ms = ms / max(1, launches)
         ach = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         e = {"algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches_per_frame": launches_pf,
              "achieved": ach, "peak": PEAK_VMEM_GBS, "unit": "GB/s", "frac": ach / PEAK_VMEM_GBS}
+        if levels is not None:
+            e["depths"] = levels
         if fetched_bytes is not None:
             f = fetched_bytes / max(1.0, launches_pf)
             fa = f / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
             e.update({"fetched_bytes_per_launch": f, "achieved_fetched": fa, "frac_fetched": fa / PEAK_VMEM_GBS})
         return e
 
-    per_ray = {"nodes": c["nodeRecords"] / max(1, walked), "tris": c["triTests"] / max(1, walked),
-               "leaves": c["leafRecords"] / max(1, walked),
-               "shadow_nodes": c["shadowNodeRecords"] / max(1, shadows),
-               "shadow_tris": c["shadowTriTests"] / max(1, shadows),
-               "shadow_leaves": c["shadowLeafRecords"] / max(1, shadows), "shaded_vertices": shaded}
-    return {"k_trace": entry("k_trace", trace_b, tr_ms, tr_n, trace_f),
-            "k_shadow": entry("k_shadow", shadow_b, sh_ms, sh_n, shadow_f),
-            "k_shade": entry("k_shade", shade_b, sd_ms, sd_n)}, per_ray
+    walked = sum(rays[l] for l in walk_levels)
+    per_ray = {"nodes": sum(nodes[l] for l in walk_levels) / max(1, walked),
+               "tris": sum(tris[l] for l in walk_levels) / max(1, walked),
+               "leaves": sum(leaves[l] for l in walk_levels) / max(1, walked),
+               "camera_nodes": nodes[0] / max(1, rays[0]), "camera_tris": tris[0] / max(1, rays[0]),
+               "shadow_nodes": c["shadowNodeRecords"] / max(1, n_sh),
+               "shadow_tris": c["shadowTriTests"] / max(1, n_sh),
+               "shadow_leaves": c["shadowLeafRecords"] / max(1, n_sh), "shaded_vertices": c["shadedVertices"]}
+    lv = lambda rng: [l + 1 for l in rng]  # noqa: E731
+    out = {"k_trace": entry(trace_b, t["traceMs"], t["traceLaunches"], trace_f, lv(walk_levels)),
+           "k_shadow": entry(shadow_b, t["shadowMs"], t["shadowLaunches"], shadow_f),
+           "k_shade": entry(shade_b, t["shadeMs"], t["shadeLaunches"] - t["fusedLaunches"], None, lv(shade_levels))}
+    if fused:
+        out["k_trace_packet_shade"] = entry(fused_b, t["fusedMs"], t["fusedLaunches"], fused_f, [1])
+    return out, per_ray
 
 
 def main():
@@ -309,11 +375,26 @@ def main():
         dist.barrier()
     d2h_ms = (time.perf_counter() - t2) / k2 * 1e3
 
+    # median of 5 frames, each timed alone (synchronised on both sides)
+    singles = []
+    for _ in range(5):
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        singles.append((time.perf_counter() - t3) * 1e3)
+    median5_ms = sorted(singles)[2]
+
     if dist_on:
         red = "cpu" if backend == "gloo" else "cuda"
         t = torch.tensor([elapsed], dtype=torch.float64, device=red)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        t = torch.tensor([median5_ms], dtype=torch.float64, device=red)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        median5_ms = float(t.item())
         n = torch.tensor([rays, walked], dtype=torch.float64, device=red)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         rays, walked = [int(x) for x in n.tolist()]
@@ -323,7 +404,8 @@ def main():
         return
 
     frames = max(1, args.steps)
-    traffic, traffic_src = pmc_traffic() if world == 1 else ({}, {"status": "not collected for N > 1"})
+    traffic, traffic_src = pmc_traffic(workload_key(args, shard_of)) if world == 1 else (
+        {}, {"status": "not collected for N > 1"})
     for name, e in kernels.items():
         tb = traffic.get(name)
         e["traffic"] = tb
@@ -341,6 +423,8 @@ def main():
         # timed window includes it); `value` excludes it
         "ms_per_step_with_d2h": d2h_ms,
         "value_with_d2h": (walked / frames) / (d2h_ms * 1e-3) / 1e6 if d2h_ms else None,
+        # BASELINE.md section 2's statistic: the median of 5 single frames (max over ranks)
+        "ms_per_step_median5": median5_ms,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -369,7 +453,7 @@ def main():
             # cache-resident scene (PMC: texture-data unit busy ~92 %, bytes beyond L2 ~11 % of the
             # algorithmic bytes; profiles/), not by HBM
             "bound": "vmem-gather",
-            "kernel": "k_trace (closest hit)",
+            "kernel": "k_trace (closest hit, per-lane walk of depths %s)" % dom.get("depths"),
             "achieved": dom["achieved"],
             "peak": PEAK_VMEM_GBS,
             "unit": "GB/s",

@@ -82,6 +82,9 @@ typedef struct mrt_scene_info {
     int64_t pixelSlots;      /* pixels rendered by this shard per sample */
     int64_t pixelSlotsMax;   /* max over shards (size of a gather slot) */
     int64_t deviceBytes;     /* device memory held by the renderer */
+    int64_t shadowStreamPriority; /* HIP priority of the renderer's shadow-walk stream: another
+                                     priority than the render stream's (0), so the two never share a
+                                     hardware queue whatever streams the process created before */
 } mrt_scene_info;
 
 typedef struct mrt_frame_stats {
@@ -111,6 +114,14 @@ typedef struct mrt_frame_stats {
     uint64_t leafRecords;          /* counting pass only: walk-tree leaf records (exact leaf boxes)
                                       fetched by closest-hit rays */
     uint64_t shadowLeafRecords;    /* ... and by shadow rays */
+    uint64_t levelNodeRecords[16]; /* counting pass only: nodeRecords of the closest-hit rays of depth 1..16 */
+    uint64_t levelTriTests[16];    /* ... triTests */
+    uint64_t levelLeafRecords[16]; /* ... leafRecords */
+    double fusedMs;                /* profiling: summed duration of the fused level-1 launches
+                                      (k_trace_packet_shade: camera rays generated, walked and shaded;
+                                      not in traceMs / shadeMs) */
+    int64_t fusedLaunches;         /* fused level-1 launches of the frame (counted in shadeLaunches too) */
+    uint64_t levelShadedVertices[16]; /* counting pass only: shadedVertices of depth 1..16 */
 } mrt_frame_stats;
 
 /* A named byte buffer (a map_Kd texture file handed over by the Android front end). */
@@ -180,7 +191,13 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  * key 8 = tail donation: idle lanes of a level's tail walk subtrees of their wave's rays (0, 1 default),
  * key 9 = idle lanes before a walk wave fetches new rays (1-64, default 32),
  * key 10 = k_shade's lean instantiation where it applies (1, default) or always the general one (0),
- * key 11 = k_shade workgroups per CU (-1 default: 14 below 4 paths per walk lane, else 28; 0: 8).
+ * key 11 = k_shade workgroups per CU (-1 default: 14; 0: 8; 1-64: that many),
+ * key 16 = camera rays by the wave-coherent packet walk in cull modes 0 and 3 (1, default) or the
+ *          per-lane walk (0); refused (-1) when the walk tree needs a deeper traversal stack than
+ *          the packet walk's LDS stack (kPacketStack),
+ * key 17 = level 1 fused: camera rays generated, packet-walked and shaded in one launch (1, default,
+ *          where it applies: BVH, packet walk, Whitted / PathTracer, untextured, lean shading, no
+ *          counting) or the separate raygen / walk / shade launches (0).
  * (Keys 4, 12-15 - binned emission, queue sorting, graph replay - measured slower and were removed.) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);

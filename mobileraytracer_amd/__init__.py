@@ -120,7 +120,10 @@ class Renderer:
         6 = shadow-walk grid percent (0 auto), 7 = no walk for the depth-capped last level, 8 = tail
         donation (idle lanes of a level's tail walk subtrees of their wave's rays), 9 = refill
         threshold of the walk waves, 10 = lean k_shade instantiation, 11 = k_shade workgroups per CU,
-        16 = the camera rays' packet walk (cull modes 0 and 3)."""
+        16 = the camera rays' packet walk (cull modes 0 and 3; refused when the walk tree needs a
+        deeper stack than the packet walk's), 17 = level 1 fused (camera rays generated,
+        packet-walked and shaded in one launch).  Results are identical for every value, except
+        key 2 = 1 (documented inexact)."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 
     def set_camera(self, kind: int, position, look_at, up, a: float, b: float) -> None:
@@ -158,6 +161,8 @@ class Renderer:
         out["levelShadowRays"] = list(s.levelShadowRays)
         out["levelTraceMs"] = list(s.levelTraceMs)
         out["levelShadowMs"] = list(s.levelShadowMs)
+        for k in ("levelNodeRecords", "levelTriTests", "levelLeafRecords", "levelShadedVertices"):
+            out[k] = list(getattr(s, k))
         return out
 
     def primary_hits(self):

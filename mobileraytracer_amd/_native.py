@@ -55,7 +55,7 @@ class MrtBlob(ctypes.Structure):
 class MrtSceneInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "triangles", "lights", "planes", "spheres", "materials", "triangleNodes", "triangleBvhDepth",
-        "pixelSlots", "pixelSlotsMax", "deviceBytes")]
+        "pixelSlots", "pixelSlotsMax", "deviceBytes", "shadowStreamPriority")]
 
 
 class MrtFrameStats(ctypes.Structure):
@@ -71,6 +71,10 @@ class MrtFrameStats(ctypes.Structure):
         ("maxNodeRecordsPerRay", ctypes.c_uint64),
         ("walkedRays", ctypes.c_uint64), ("shadedVertices", ctypes.c_uint64), ("shadeLaunches", ctypes.c_int64),
         ("leafRecords", ctypes.c_uint64), ("shadowLeafRecords", ctypes.c_uint64),
+        ("levelNodeRecords", ctypes.c_uint64 * 16), ("levelTriTests", ctypes.c_uint64 * 16),
+        ("levelLeafRecords", ctypes.c_uint64 * 16),
+        ("fusedMs", ctypes.c_double), ("fusedLaunches", ctypes.c_int64),
+        ("levelShadedVertices", ctypes.c_uint64 * 16),
     ]
 
 

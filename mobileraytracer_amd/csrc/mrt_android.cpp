@@ -166,7 +166,7 @@ void mrt_android_render_into_bitmap_cb(int32_t* pixels, int32_t nThreads, mrt_an
         r = gRenderer;
         ++gActive;  // before the thread starts: an initialize / reset right after this call waits for it
     }
-    std::thread([r, pixels, done, user] {  // detached render thread (:883-889)
+    auto body = [r, pixels, done, user] {  // detached render thread (:883-889)
         int32_t rep = 1;
         while (gState == MRT_STATE_BUSY && rep > 0) {
             if (r != nullptr) (void)mrt_render_frame(r.get(), pixels);
@@ -185,7 +185,22 @@ void mrt_android_render_into_bitmap_cb(int32_t* pixels, int32_t nThreads, mrt_an
         }
         gIdle.notify_all();
         gState = MRT_STATE_IDLE;
-    }).detach();
+    };
+    try {
+        std::thread(body).detach();
+    } catch (const std::exception&) {  // std::system_error: no thread was started
+        // undo what the thread would have undone, so later initialize / reset / wait calls do not
+        // block on it, and hand the pixels back (the JNI caller unlocks its bitmap in done)
+        {
+            std::lock_guard<std::mutex> lock(gMutex);
+            --gActive;
+        }
+        gIdle.notify_all();
+        if (done != nullptr) done(user);
+        gFinished = true;
+        gRendered.notify_all();
+        gState = MRT_STATE_IDLE;
+    }
 }
 
 void mrt_android_render_into_bitmap(int32_t* pixels, int32_t nThreads) {

@@ -240,6 +240,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, i
     }
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris, kStatLeaves);
+        reduceCounts<kCount>(cnt, stats, kStatLevelNodes + level - 1, kStatLevelTris + level - 1, kStatLevelLeaves + level - 1);
         atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
         waveLog(cnt, stats, 0, level, t0);
     }
@@ -259,6 +260,7 @@ __global__ __launch_bounds__(kWalkThreads, 8) void k_trace_packet(DScene s, Leve
     tracePacket<kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, waveStacks[threadIdx.x / 64]);
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris, kStatLeaves);
+        reduceCounts<kCount>(cnt, stats, kStatLevelNodes + level - 1, kStatLevelTris + level - 1, kStatLevelLeaves + level - 1);
         waveLog(cnt, stats, 0, level, t0);
     }
 }
@@ -663,7 +665,10 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
         if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, dead, lights);
         if (kFull && a.stats != nullptr) {  // counting pass: shaded (non-terminal) vertices
             const uint64_t m = __ballot(active && !v.terminal);
-            if (laneId() == 0 && m != 0) atomicAdd(a.stats + kStatShaded, static_cast<unsigned long long>(__popcll(m)));
+            if (laneId() == 0 && m != 0) {
+                atomicAdd(a.stats + kStatShaded, static_cast<unsigned long long>(__popcll(m)));
+                atomicAdd(a.stats + kStatLevelShaded + level - 1, static_cast<unsigned long long>(__popcll(m)));
+            }
         }
     }
 }

@@ -47,7 +47,12 @@ constexpr int kStatShaded = kStatSkipped + 1;        // counting pass: vertices 
 constexpr int kStatShadeLaunches = kStatShaded + 1;  // k_shade launches of the frame
 constexpr int kStatLeaves = kStatShadeLaunches + 1;  // counting pass: leaf records fetched, closest hit
 constexpr int kStatLeavesShadow = kStatLeaves + 1;   // ... and any hit
-constexpr int kNumStats = kStatLeavesShadow + 1;
+// counting pass, closest hit, per level (+ level - 1): child records, triangle tests, leaf records
+constexpr int kStatLevelNodes = kStatLeavesShadow + 1;
+constexpr int kStatLevelTris = kStatLevelNodes + kMaxLevels;
+constexpr int kStatLevelLeaves = kStatLevelTris + kMaxLevels;
+constexpr int kStatLevelShaded = kStatLevelLeaves + kMaxLevels;  // counting pass: kStatShaded per level
+constexpr int kNumStats = kStatLevelShaded + kMaxLevels;
 // counting builds: per walk launch (closest / any-hit x level) and wave {start, end (100 MHz
 // ticks), rays fetched, child records fetched}, after the statistics (mrt_wave_log)
 constexpr int kWaveLogWaves = 8192;

@@ -97,6 +97,7 @@ struct mrt_renderer {
     float pixelConst = 0.5F;
     int rankIndex = 0, rankCount = 1;
     int device = 0;
+    int shadowPriority = 0;  // the shadow stream's priority (createShadowStream)
 
     // scene
     mrt::GCamera cam{};
@@ -142,6 +143,7 @@ struct mrt_renderer {
     int refill = 0;                      // tuning key 9: walk refill threshold (0 auto: by paths per lane)
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
+    bool fusedL1 = false;                // the last pass ran level 1 as k_trace_packet_shade
     unsigned long long* hostStats = nullptr;  // pinned: the per-pass statistics read back by DMA
 
     // host copies for the GL preview of the Android front end (mrt_preview_arrays; kept only for
@@ -498,7 +500,6 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     const int nLevels = r->nLevels;
     r->gdepth = std::max(1, r->stackNeed - kLdsStackMin);
     mrt_renderer::Pipe& pp = r->pipe;
-    if (pp.shadowStream == nullptr) MRT_HIP(hipStreamCreateWithFlags(&pp.shadowStream, hipStreamNonBlocking));
     // Ray / hit / payload buffers of levels L and L+2 are never live together (level L's rays are
     // dead once k_shade(L) has read them; its vertex and result records stay until the resolve),
     // but one set per level keeps the shadow stream's overlap free of reuse hazards.
@@ -529,6 +530,27 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats + kWaveLogEntries);
     pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
     pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
+}
+
+// The shadow walks' stream.  HIP maps a process's streams onto a few hardware queues (a pool per
+// priority level, GPU_MAX_HW_QUEUES each); two streams on one queue run their kernels one after the
+// other, so a shadow walk on the render stream's queue no longer overlaps the next level (one
+// rank's C4 shard at N = 8: 2.81 -> 3.54 ms when RCCL's streams were created first, DESIGN.md
+// section 6).  A stream of another priority than the caller's (normal-priority) render stream
+// comes from another pool: the least priority where the device has one below normal, else the
+// greatest.  MOBILERT_SHADOW_PRIORITY=normal|least|greatest overrides this (A/B measurements).
+void createShadowStream(mrt_renderer* r) {
+    int least = 0, greatest = 0;
+    MRT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    int prio = least != 0 ? least : greatest;
+    if (const char* e = std::getenv("MOBILERT_SHADOW_PRIORITY")) {
+        const std::string v(e);
+        if (v == "normal") prio = 0;
+        else if (v == "least") prio = least;
+        else if (v == "greatest") prio = greatest;
+    }
+    r->shadowPriority = prio;
+    MRT_HIP(hipStreamCreateWithPriority(&r->pipe.shadowStream, hipStreamNonBlocking, prio));
 }
 
 // Chunk size: every slot of the shard in one pass, within the path budget.
@@ -606,8 +628,10 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         setPixelSampler(r, &ra);
         ra.sampleBase = sampleBase;
         // level 1 fused (ray generation, packet walk and shading in one launch) where it applies
-        const bool fuseL1 = !timing && nLevels >= 1 && !(skipLast && nLevels == 1) &&
-                            !(skipLastShade && nLevels == 1) && canFuseLevel1(shader, r->ds, sa);
+        // (with per-launch events too: the serialised roofline frames time the kernel the timed frames run)
+        const bool fuseL1 = nLevels >= 1 && !(skipLast && nLevels == 1) && !(skipLastShade && nLevels == 1) &&
+                            canFuseLevel1(shader, r->ds, sa);
+        r->fusedL1 = fuseL1;
         if (!fuseL1) launchRaygen(ra, pp.levels[1], pp.counters, st);
         // With few paths per resident walk lane (a small shard: C4 at N >= 4) the levels are short
         // and tail-bound, and a full-width shadow walk starves the next level's shading of CUs;
@@ -722,6 +746,12 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->shadowTriTests += hs[kStatTrisShadow];
     fs->leafRecords += hs[kStatLeaves];
     fs->shadowLeafRecords += hs[kStatLeavesShadow];
+    for (int l = 0; l < kMaxLevels && l < 16; ++l) {
+        fs->levelNodeRecords[l] += hs[kStatLevelNodes + l];
+        fs->levelTriTests[l] += hs[kStatLevelTris + l];
+        fs->levelLeafRecords[l] += hs[kStatLevelLeaves + l];
+        fs->levelShadedVertices[l] += hs[kStatLevelShaded + l];
+    }
     fs->maxNodeRecordsPerRay = std::max<uint64_t>(fs->maxNodeRecordsPerRay, hs[kStatMaxNodesRay]);
     fs->shadedVertices += hs[kStatShaded];
     fs->shadeLaunches += r->shadeLaunches;
@@ -737,14 +767,19 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
             MRT_HIP(hipEventElapsedTime(&ta, pp.evPool[e], pp.evPool[e + 1]));
             MRT_HIP(hipEventElapsedTime(&tc, pp.evPool[e + 1], pp.evPool[e + 2]));
             MRT_HIP(hipEventElapsedTime(&tb, pp.evPool[e + 3], pp.evPool[e + 4]));
-            fs->traceMs += ta;
-            fs->shadeMs += tc;
-            fs->shadowMs += tb;
             const size_t lvl = (e / 5) % static_cast<size_t>(r->nLevels);
+            if (lvl == 0 && r->fusedL1) {  // one launch: ray generation, walk and shading of level 1
+                fs->fusedMs += ta;
+                fs->fusedLaunches += 1;
+            } else {
+                fs->traceMs += ta;
+                fs->shadeMs += tc;
+            }
+            fs->shadowMs += tb;
             fs->levelTraceMs[lvl] += ta;
             fs->levelShadowMs[lvl] += tb;
             const bool last = lvl + 1 == static_cast<size_t>(r->nLevels);
-            if (!(r->walkSkipped && last)) fs->traceLaunches += 1;
+            if (!(r->walkSkipped && last) && !(lvl == 0 && r->fusedL1)) fs->traceLaunches += 1;
             if (!last) fs->shadowLaunches += 1;  // the last level builds no shadow rays
         }
     }
@@ -802,6 +837,10 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs.triTests += prev.triTests;
                     fs.shadowNodeRecords += prev.shadowNodeRecords;
                     fs.shadowTriTests += prev.shadowTriTests;
+                    fs.leafRecords += prev.leafRecords;
+                    fs.shadowLeafRecords += prev.shadowLeafRecords;
+                    fs.fusedMs += prev.fusedMs;
+                    fs.fusedLaunches += prev.fusedLaunches;
                     fs.maxNodeRecordsPerRay = std::max(fs.maxNodeRecordsPerRay, prev.maxNodeRecordsPerRay);
                     fs.shadedVertices += prev.shadedVertices;
                     fs.shadeLaunches += prev.shadeLaunches;
@@ -816,6 +855,12 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                         fs.levelShadowRays[l] += prev.levelShadowRays[l];
                         fs.levelTraceMs[l] += prev.levelTraceMs[l];
                         fs.levelShadowMs[l] += prev.levelShadowMs[l];
+                        if (l < 16) {
+                            fs.levelNodeRecords[l] += prev.levelNodeRecords[l];
+                            fs.levelTriTests[l] += prev.levelTriTests[l];
+                            fs.levelLeafRecords[l] += prev.levelLeafRecords[l];
+                            fs.levelShadedVertices[l] += prev.levelShadedVertices[l];
+                        }
                     }
                 } else {
                     if (acc != nullptr)
@@ -866,6 +911,7 @@ mrt_renderer* createRenderer(const mrt_config* cfg, const MemScene* mem = nullpt
     if (cfg->device >= 0) MRT_HIP(hipSetDevice(cfg->device));
     MRT_HIP(hipGetDevice(&r->device));
     MRT_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+    createShadowStream(r.get());
     hipDeviceProp_t prop;
     MRT_HIP(hipGetDeviceProperties(&prop, r->device));
     r->traceThreads = prop.multiProcessorCount * traceResidentThreadsPerCU();
@@ -1076,12 +1122,19 @@ int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
     info->pixelSlots = r->nSlots;
     info->pixelSlotsMax = r->maxSlots;
     info->deviceBytes = static_cast<int64_t>(r->sceneMem.total + r->queueMem.total + r->frameMem.total);
+    info->shadowStreamPriority = r->shadowPriority;
     return 0;
 }
 
 int mrt_set_camera(mrt_renderer* r, int32_t kind, const float* position, const float* lookAt, const float* up,
                    float a, float b) {
     return guarded([&] {
+        if (r == nullptr || position == nullptr || lookAt == nullptr || up == nullptr)
+            throw std::runtime_error("mrt_set_camera: null argument");
+        if (!std::isfinite(a) || !std::isfinite(b)) throw std::runtime_error("mrt_set_camera: non-finite field of view / size");
+        for (int k = 0; k < 3; ++k)
+            if (!std::isfinite(position[k]) || !std::isfinite(lookAt[k]) || !std::isfinite(up[k]))
+                throw std::runtime_error("mrt_set_camera: non-finite position / lookAt / up");
         const mrt::v3 p{position[0], position[1], position[2]}, l{lookAt[0], lookAt[1], lookAt[2]},
             u{up[0], up[1], up[2]};
         if (kind == 0) {
@@ -1095,6 +1148,10 @@ int mrt_set_camera(mrt_renderer* r, int32_t kind, const float* position, const f
 }
 
 int mrt_set_pixel_sampler(mrt_renderer* r, int32_t kind, float value) {
+    if (r == nullptr) {
+        gLastError = "mrt_set_pixel_sampler: null renderer";
+        return -1;
+    }
     if (kind < -1 || kind > 1) {
         gLastError = "pixel sampler: -1 by samplesPixel, 0 Constant, 1 StaticHaltonSeq";
         return -1;
@@ -1105,8 +1162,10 @@ int mrt_set_pixel_sampler(mrt_renderer* r, int32_t kind, float value) {
 }
 
 int mrt_set_max_point(mrt_renderer* r, const float* maxPoint) {
-    r->maxPoint = mrt::v3{maxPoint[0], maxPoint[1], maxPoint[2]};
-    return 0;
+    return guarded([&] {
+        if (r == nullptr || maxPoint == nullptr) throw std::runtime_error("mrt_set_max_point: null argument");
+        r->maxPoint = mrt::v3{maxPoint[0], maxPoint[1], maxPoint[2]};
+    });
 }
 
 int mrt_set_profiling(mrt_renderer* r, int32_t flags) {

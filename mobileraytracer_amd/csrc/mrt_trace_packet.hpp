@@ -263,7 +263,8 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
                 }
                 hit = make_float4(bt, u, v, bitsf(bcode));
             }
-            out[i] = hit;
+            // (the fused level-1 kernel shades the hit right here: nothing reads it from memory)
+            if constexpr (std::is_same<Post, NoPost>::value) out[i] = hit;
             if (kCount) ++cnt->rays;
         }
         post(i, valid, o4, d4, hit);

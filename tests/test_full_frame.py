@@ -279,3 +279,59 @@ def test_quantized_walk_tree_boundary_rays(oracle_mod):
     assert np.array_equal(ok, ref_hits[0][sel]) and np.array_equal(oi, ref_hits[1][sel])
     assert np.array_equal(ot.view(np.int32), ref_hits[2][sel].view(np.int32))
     assert np.array_equal(occ, ref_occ[sel])
+
+
+def test_packet_walk_grazing_bundles(oracle_mod):
+    """The camera rays' packet walk (tuning key 16) enters a child when ANY walking lane passes its
+    quantized box and orders children by the first walking lane's entry, then each lane tests the
+    exact reference leaf box, the certified leaf key and its own triangles.  Its hits equal the
+    per-lane walk's provided every quantized ancestor box holds the exact box of every leaf below it
+    as the slab test computes it (the Quantizer's margin).  Coherent 64-ray
+    bundles (one packet each: mrt_trace_rays fills waves with 64 consecutive rays) aimed tangent
+    to leaf-box corners, edges and faces, with a spread of 1e-7 .. 1e-3 rad, stress exactly that:
+    packet on / off and cull modes 0 / 3 give the reference walk's hits, and a sample the oracle's."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, shader=1, scene="conference")
+    boxes, off, cnt, _ = m.triangle_bvh(cfg)
+    lo, hi = boxes[0, :3].astype(np.float64), boxes[0, 3:].astype(np.float64)
+    leaf = boxes[cnt > 0].astype(np.float64)
+    rng = np.random.default_rng(21)
+    nb = 4096  # bundles
+    b = leaf[rng.integers(0, len(leaf), nb)]
+    corner = np.where(rng.random((nb, 3)) < 0.5, b[:, :3], b[:, 3:])
+    tgt = b[:, :3] + rng.random((nb, 3)) * (b[:, 3:] - b[:, :3])
+    kind = rng.integers(0, 3, nb)  # 0 corner, 1 edge, 2 face
+    ax = rng.integers(0, 3, (nb, 2))
+    for i in range(nb):
+        if kind[i] == 0:
+            tgt[i] = corner[i]
+        else:
+            tgt[i, ax[i, 0]] = corner[i, ax[i, 0]]
+            if kind[i] == 1:
+                tgt[i, ax[i, 1]] = corner[i, ax[i, 1]]
+    o = lo + rng.random((nb, 3)) * (hi - lo)
+    d0 = tgt - o
+    d0 /= np.linalg.norm(d0, axis=1, keepdims=True)
+    spread = 10.0 ** rng.uniform(-7, -3, nb)
+    jit = rng.normal(size=(nb, 64, 3)) * spread[:, None, None]
+    jit[:, 0] = 0.0  # the bundle's first ray exactly at the target
+    d = d0[:, None, :] + jit
+    d = (d / np.linalg.norm(d, axis=2, keepdims=True)).reshape(-1, 3).astype(np.float32)
+    o = np.repeat(o, 64, axis=0).astype(np.float32)
+    res = {}
+    with m.Renderer(cfg) as r:
+        for walk, cull, packet in ((0, 0, 0), (1, 3, 1), (1, 3, 0), (1, 0, 1), (1, 0, 0)):
+            r.set_tuning(1, walk)
+            r.set_tuning(2, cull)
+            r.set_tuning(16, packet)
+            res[(walk, cull, packet)] = r.trace_rays(o, d)
+    ref = res[(0, 0, 0)]
+    assert (ref[0] == 3).mean() > 0.5
+    for key, hits in res.items():
+        assert all(np.array_equal(x, y) for x, y in zip(hits, ref)), key
+    o_ = oracle_for(oracle_mod, cfg)
+    sel = np.arange(0, len(o), 37)
+    ok, oi, ot = o_.trace_rays(o[sel], d[sel])
+    o_.close()
+    assert np.array_equal(ok, ref[0][sel]) and np.array_equal(oi, ref[1][sel])
+    assert np.array_equal(ot.view(np.int32), ref[2][sel].view(np.int32))

@@ -89,6 +89,19 @@ def test_library_loads_without_gpu(native_lib_path):
     assert lib.mrt_last_error() is not None
 
 
+def test_setters_reject_null_arguments(native_lib_path):
+    """mrt_set_camera / mrt_set_max_point / mrt_set_pixel_sampler return -1 with mrt_last_error set
+    on a NULL renderer or vector (no GPU needed: the checks come before any device work)."""
+    from mobileraytracer_amd import _native
+    lib = _native.load_library(native_lib_path)
+    v = (ctypes.c_float * 3)(0.0, 0.0, 1.0)
+    assert lib.mrt_set_camera(None, 0, v, v, v, 45.0, 45.0) == -1
+    assert b"null" in lib.mrt_last_error()
+    assert lib.mrt_set_max_point(None, v) == -1
+    assert lib.mrt_set_max_point(None, None) == -1
+    assert lib.mrt_set_pixel_sampler(None, 0, 0.5) == -1
+
+
 def test_ctypes_layouts_match_header(tmp_path):
     """The ctypes mirror of mrt_config / mrt_scene_info / mrt_frame_stats matches the C header."""
     from mobileraytracer_amd import _native

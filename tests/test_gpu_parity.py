@@ -595,6 +595,26 @@ def test_shard_assembly_is_identical_to_single_gpu():
         assert np.array_equal(sharding.unpack(gathered, 1920, 1080, world, ref), single)
 
 
+def test_shadow_overlap_survives_rccl_streams():
+    """The renderer keeps its shadow walks on a stream of another priority than the render stream,
+    so the two never share a hardware queue, whatever streams the process created before it: one
+    rank's C4 shard at N = 8 renders as fast with an RCCL process group (and its streams) created
+    BEFORE the renderer as without one (round 3 measured 3.54 against 2.81 ms when they shared a
+    queue).  Two fresh processes (tools/stream_probe.py), HIP's default hardware-queue count."""
+    import json, subprocess, sys
+    env = dict(os.environ)
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    probe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "stream_probe.py")
+    out = {}
+    for first in (False, True):
+        cmd = [sys.executable, probe, "--frames", "30"] + (["--pg-first"] if first else [])
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+        assert res.returncode == 0, res.stderr[-2000:]
+        out[first] = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out[True]["shadow_stream_priority"] != 0
+    assert out[True]["ms_per_frame"] < 1.08 * out[False]["ms_per_frame"], out
+
+
 def test_shard_assembly_over_many_ranks():
     """More shards than one unpack launch takes (kUnpackRanks = 16): 17 ranks of a small frame
     assemble to the single-GPU image."""
@@ -605,23 +625,28 @@ def test_shard_assembly_over_many_ranks():
 
 
 def test_c5_4k_8spp_shards_and_tiles(oracle_mod):
-    """C5 (3840x2160, 8 spp, PathTracer): the 2- and 8-shard assemblies equal the single-GPU frame,
-    and six whole reference tiles (240x135 px x 8 samples each, spread over the frame) equal the
-    oracle bit for bit."""
+    """C5 (3840x2160, 8 spp, PathTracer): the 2-, 4- and 8-shard assemblies equal the single-GPU
+    frame ("image identical across 1/2/4/8 GPUs"), and 32 whole reference tiles
+    (240x135 px x 8 samples each, Renderer.cpp:125-135), stratified so that every tile row and
+    every tile column of the 16 x 16 grid holds two of them, equal the oracle bit for bit."""
     kw = dict(width=3840, height=2160, shader=2, scene="conference", spp=8, max_depth=5)
     cfg = make_cfg(**kw)
     single, rays, st = gpu_render(cfg)
     assert st["primaryRays"] == 3840 * 2160 * 8
     assert (single != SENTINEL).all()  # 3840x2160 tiles exactly (bx=240, by=135)
-    for world in (2, 8):
+    for world in (2, 4, 8):
         img, _, srays = _render_shards(kw, world)
         assert np.array_equal(img, single) and srays == rays, world
+    # tile k covers column k % 16, row k / 16; rows r and columns (r * 5) % 16, (r * 5 + 8) % 16
+    tiles = sorted({16 * r + (5 * r + 8 * h) % 16 for r in range(16) for h in range(2)})
+    assert len(tiles) == 32
+    assert {t % 16 for t in tiles} == set(range(16)) and {t // 16 for t in tiles} == set(range(16))
     o = oracle_for(oracle_mod, cfg)
     ref = np.full(3840 * 2160, SENTINEL, np.int32)
-    o.render_tiles([0, 37, 86, 133, 170, 255], ref, threads=min(16, os.cpu_count() or 1))
+    o.render_tiles(tiles, ref, threads=min(16, os.cpu_count() or 1))
     o.close()
     mask = ref != SENTINEL
-    assert mask.sum() == 6 * 240 * 135
+    assert mask.sum() == 32 * 240 * 135
     assert np.array_equal(single[mask], ref[mask]), int((single[mask] != ref[mask]).sum())
 
 

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc CSVs of tools/pmc_run.sh into bytes beyond L2 per launch per kernel.
 
-usage: python tools/pmc_summary.py <pmc_run output dir> <out.json>
+usage: python tools/pmc_summary.py <pmc_run output dir> <out.json> [bench arguments of the profiled command]
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section)
 FETCH_SIZE on gfx950 reads exactly half of the bytes of a wide (16 B/lane) stream, so the read
@@ -12,13 +12,24 @@ TA / TD busy) are averaged per kernel as they are.
 import csv, glob, json, os, re, sys
 from collections import defaultdict
 
-# the default (exact, cull mode 3) walk instantiations and the lean PathTracer shading kernel;
-# "k_trace" is every closest-hit launch of a frame: the camera rays' packet walk and the per-lane
-# walk of the other levels, averaged over their dispatches as bench.py averages its launches
-PRODUCT = {"k_trace": (r"k_trace<false, 1, 3>", r"k_trace_packet<false, 3>"), "k_shadow": (r"k_shadow<false, 1, 3>",),
-           "k_shade": (r"k_shade<2, false>",)}
+# the kernels of the timed frames in the default (exact, cull mode 3) configuration, as bench.py's
+# roofline names them: level 1 fused (k_trace_packet_shade), the per-lane closest-hit walk of the
+# deeper levels, the shadow walk and the lean PathTracer shading kernel
+PRODUCT = {"k_trace": (r"k_trace<false, 1, 3>",), "k_trace_packet_shade": (r"k_trace_packet_shade<2, 3>",),
+           "k_shadow": (r"k_shadow<false, 1, 3>",), "k_shade": (r"k_shade<2, false>",)}
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import kernel_source_stamp  # noqa: E402
+from bench import kernel_source_stamp, workload_key  # noqa: E402
+
+
+def profiled_workload(extra):
+    """bench.py's workload key for the bench arguments of the profiled command."""
+    import argparse
+    p = argparse.ArgumentParser()
+    for k, v in (("--width", 1920), ("--height", 1080), ("--spp", 4), ("--max-depth", 5), ("--shader", 2),
+                 ("--shard-of", 0)):
+        p.add_argument(k, type=int, default=v)
+    a, _ = p.parse_known_args(extra)
+    return workload_key(a, a.shard_of if a.shard_of > 1 else 0)
 
 
 def rows(d):
@@ -33,7 +44,7 @@ def main():
     for row in rows(src):
         per[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {"bytes_beyond_l2_per_launch": {}, "counters": {}, "kernels": {},
-           "kernel_source_sha256": kernel_source_stamp(),
+           "kernel_source_sha256": kernel_source_stamp(), "workload": profiled_workload(sys.argv[3:]),
            "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, averaged over the dispatches of "
                    "the profiled command; includes Infinity-Cache hits"}
     for short, pats in PRODUCT.items():
