@@ -30,14 +30,6 @@ import os
 import sys
 import time
 
-# Hardware queues per process (read by the HIP runtime at its initialisation, so before torch is
-# imported).  HIP's default of 4 is shared by every stream of the process: with RCCL's and
-# torch's streams created, the renderer's render and shadow streams can land on one queue and the
-# shadow walk then no longer overlaps the next level (one rank's C4 shard at N = 8: 2.81 ms
-# without a process group, 3.54 ms with one at 4 queues, 2.87 ms at 8).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
-
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
@@ -65,6 +57,8 @@ def parse():
     # C5: --width 3840 --height 2160 --spp 8 --shard-of 8), and the final bitmap saved as .npy
     p.add_argument("--shard-of", type=int, default=0)
     p.add_argument("--dump-bitmap", default="")
+    # the scene: the Conference stand-in (default) or the flat-geometry stand-in (rehearsal lines)
+    p.add_argument("--scene", choices=("conference", "flat"), default="conference")
     return p.parse_args()
 
 
@@ -156,7 +150,7 @@ PMC_PROFILE = os.path.join("profiles", "r04_pmc_traffic.json")
 def workload_key(args, shard_of):
     """What a PMC profile must have measured to be reported on this bench line."""
     return {"width": args.width, "height": args.height, "spp": args.spp, "max_depth": args.max_depth,
-            "shader": args.shader, "shard_of": shard_of}
+            "shader": args.shader, "shard_of": shard_of, "scene": getattr(args, "scene", "conference")}
 
 
 def pmc_traffic(workload):
@@ -291,14 +285,14 @@ def main():
         torch.cuda.set_device(local)
     else:
         torch.cuda.set_device(0)
-    scene = scenes.conference()
+    scene = scenes.conference() if args.scene == "conference" else scenes.conference_flat()
     shard_of = args.shard_of if (args.shard_of > 1 and not dist_on) else 0
     cfg = m.Config(width=args.width, height=args.height, shader=args.shader, sceneIndex=-1,
                    samplesPixel=args.spp, samplesLight=1, maxDepth=args.max_depth, objFilePath=scene[0],
                    mtlFilePath=scene[1], camFilePath=scene[2], rankIndex=rank,
                    rankCount=shard_of if shard_of else world, device=torch.cuda.current_device())
-    # the renderer (and its two HIP streams) before the process group, so that RCCL's streams
-    # take the later hardware queues
+    # (the renderer checks at creation that its render and shadow streams run concurrently, whatever
+    # streams RCCL or torch created: DESIGN.md section 6)
     r = m.Renderer(cfg)
     if dist_on:
         if backend == "gloo":
@@ -431,8 +425,11 @@ def main():
         "dtype": "f32",
         "data": "synthetic" if scenes.is_standin(scene[0]) else "conference.obj",
         "config": {
-            "workload": f"conference_{args.width}x{args.height}_{args.spp}spp_pathtracer_depth{args.max_depth}",
-            "scene": ("conference stand-in: 331179 triangles + 2 area lights, reference conference.mtl/.cam "
+            "workload": ("conference" if args.scene == "conference" else "conference_flat") +
+                        f"_{args.width}x{args.height}_{args.spp}spp_pathtracer_depth{args.max_depth}",
+            "scene": (("conference stand-in" if args.scene == "conference" else
+                       "flat-geometry conference stand-in (large flat triangles, slivers, coplanar panels)") +
+                      ": 331179 triangles + 2 area lights, reference conference.mtl/.cam "
                       "(conference.obj is absent from the reference snapshot)") if scenes.is_standin(scene[0])
             else scene[0],
             "resolution": [args.width, args.height],

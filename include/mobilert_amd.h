@@ -82,9 +82,11 @@ typedef struct mrt_scene_info {
     int64_t pixelSlots;      /* pixels rendered by this shard per sample */
     int64_t pixelSlotsMax;   /* max over shards (size of a gather slot) */
     int64_t deviceBytes;     /* device memory held by the renderer */
-    int64_t shadowStreamPriority; /* HIP priority of the renderer's shadow-walk stream: another
-                                     priority than the render stream's (0), so the two never share a
-                                     hardware queue whatever streams the process created before */
+    int64_t shadowStreamConcurrent; /* 1: the shadow walks run on their own stream beside the render
+                                       chain (checked at mrt_create: the two streams' kernels overlap
+                                       in time, i.e. they feed different hardware queues, whatever
+                                       streams the process created before); 0: serialised */
+    int64_t shadowStreamsTried;     /* shadow streams created until one ran concurrently */
 } mrt_scene_info;
 
 typedef struct mrt_frame_stats {
@@ -122,6 +124,7 @@ typedef struct mrt_frame_stats {
                                       not in traceMs / shadeMs) */
     int64_t fusedLaunches;         /* fused level-1 launches of the frame (counted in shadeLaunches too) */
     uint64_t levelShadedVertices[16]; /* counting pass only: shadedVertices of depth 1..16 */
+    uint64_t shadowOccluded;       /* counting pass only: occluded shadow rays */
 } mrt_frame_stats;
 
 /* A named byte buffer (a map_Kd texture file handed over by the Android front end). */

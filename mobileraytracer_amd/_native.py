@@ -55,7 +55,7 @@ class MrtBlob(ctypes.Structure):
 class MrtSceneInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "triangles", "lights", "planes", "spheres", "materials", "triangleNodes", "triangleBvhDepth",
-        "pixelSlots", "pixelSlotsMax", "deviceBytes", "shadowStreamPriority")]
+        "pixelSlots", "pixelSlotsMax", "deviceBytes", "shadowStreamConcurrent", "shadowStreamsTried")]
 
 
 class MrtFrameStats(ctypes.Structure):
@@ -75,6 +75,7 @@ class MrtFrameStats(ctypes.Structure):
         ("levelLeafRecords", ctypes.c_uint64 * 16),
         ("fusedMs", ctypes.c_double), ("fusedLaunches", ctypes.c_int64),
         ("levelShadedVertices", ctypes.c_uint64 * 16),
+        ("shadowOccluded", ctypes.c_uint64),
     ]
 
 

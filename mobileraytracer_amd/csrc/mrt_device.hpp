@@ -334,6 +334,7 @@ struct TravCount {
     uint32_t rayStart = 0;  // nodes at the current ray's fetch (per-ray maximum, counting builds)
     uint32_t rayMax = 0;
     uint32_t rays = 0;      // rays this lane fetched (the wave log of counting builds)
+    uint32_t occluded = 0;  // any hit: occluded rays
 };
 
 // Generic BVH walk.  kKind selects the leaf routine.  Returns true on an any-hit.

@@ -295,6 +295,9 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, 
     }
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodesShadow, kStatTrisShadow, kStatLeavesShadow);
+        unsigned long long occl = cnt.occluded;
+        for (int off = 32; off > 0; off >>= 1) occl += __shfl_down(occl, off, 64);
+        if (laneId() == 0) atomicAdd(stats + kStatOccluded, occl);
         waveLog(cnt, stats, 1, level, t0);
     }
 }
@@ -941,6 +944,24 @@ __global__ __launch_bounds__(256) void k_dump_hits(Level lv, int n, int32_t* kin
     kind[i] = static_cast<int32_t>(primKind(code));
     index[i] = primKind(code) == kMiss ? -1 : static_cast<int32_t>(primIndex(code));
     t[i] = h.x;
+}
+
+// One lane records the real-time counter (100 MHz) before and after a bounded spin of `ticks`: two
+// launches on two streams overlap in time iff the streams feed different hardware queues.
+__global__ void k_spin(unsigned long long* out, int slot, unsigned long long ticks) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t = t0;
+    for (int i = 0; i < (1 << 20) && t - t0 < ticks; ++i) {
+        __builtin_amdgcn_s_sleep(8);
+        t = __builtin_amdgcn_s_memrealtime();
+    }
+    out[2 * slot] = t0;
+    out[2 * slot + 1] = t;
+}
+
+void launchSpin(unsigned long long* out, int slot, unsigned long long ticks, hipStream_t st) {
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, st, out, slot, ticks);
 }
 
 __global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats, int skippedLevel) {

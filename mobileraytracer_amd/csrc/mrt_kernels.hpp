@@ -52,7 +52,8 @@ constexpr int kStatLevelNodes = kStatLeavesShadow + 1;
 constexpr int kStatLevelTris = kStatLevelNodes + kMaxLevels;
 constexpr int kStatLevelLeaves = kStatLevelTris + kMaxLevels;
 constexpr int kStatLevelShaded = kStatLevelLeaves + kMaxLevels;  // counting pass: kStatShaded per level
-constexpr int kNumStats = kStatLevelShaded + kMaxLevels;
+constexpr int kStatOccluded = kStatLevelShaded + kMaxLevels;  // counting pass: occluded shadow rays
+constexpr int kNumStats = kStatOccluded + 1;
 // counting builds: per walk launch (closest / any-hit x level) and wave {start, end (100 MHz
 // ticks), rays fetched, child records fetched}, after the statistics (mrt_wave_log)
 constexpr int kWaveLogWaves = 8192;
@@ -165,5 +166,7 @@ void launchKatTriangle(const float* tris, const float* orig, const float* dir, i
 void launchLoadRays(const Level& lv, const float* orig, const float* dir, const float* dist, const uint32_t* src, int n,
                     bool any, int* counters, hipStream_t st);
 int traceResidentThreadsPerCU();  // max over the trace walks of resident threads per CU
+// out[2 slot], out[2 slot + 1] = real-time counter (100 MHz) before / after a spin of `ticks`
+void launchSpin(unsigned long long* out, int slot, unsigned long long ticks, hipStream_t st);
 
 }  // namespace mrt

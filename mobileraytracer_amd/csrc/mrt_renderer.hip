@@ -97,7 +97,11 @@ struct mrt_renderer {
     float pixelConst = 0.5F;
     int rankIndex = 0, rankCount = 1;
     int device = 0;
-    int shadowPriority = 0;  // the shadow stream's priority (createShadowStream)
+    int shadowConcurrent = 0;  // the shadow stream runs beside the render stream (createShadowStream)
+    int shadowTries = 0;       // shadow streams created until one did
+    std::vector<hipStream_t> spareStreams;  // earlier candidates (kept: they hold their hardware queues)
+    unsigned long long* spinTimes = nullptr;
+    hipEvent_t joinIn = nullptr, joinOut = nullptr;  // the caller's stream <-> the render stream
 
     // scene
     mrt::GCamera cam{};
@@ -164,6 +168,9 @@ struct mrt_renderer {
         for (hipEvent_t e : pipe.evPool) (void)hipEventDestroy(e);
         for (hipEvent_t e : pipe.syncPool) (void)hipEventDestroy(e);
         if (pipe.shadowStream != nullptr) (void)hipStreamDestroy(pipe.shadowStream);
+        for (hipStream_t s : spareStreams) (void)hipStreamDestroy(s);
+        if (joinIn != nullptr) (void)hipEventDestroy(joinIn);
+        if (joinOut != nullptr) (void)hipEventDestroy(joinOut);
         if (stream != nullptr) (void)hipStreamDestroy(stream);
     }
 };
@@ -532,25 +539,45 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
 }
 
-// The shadow walks' stream.  HIP maps a process's streams onto a few hardware queues (a pool per
-// priority level, GPU_MAX_HW_QUEUES each); two streams on one queue run their kernels one after the
-// other, so a shadow walk on the render stream's queue no longer overlaps the next level (one
-// rank's C4 shard at N = 8: 2.81 -> 3.54 ms when RCCL's streams were created first, DESIGN.md
-// section 6).  A stream of another priority than the caller's (normal-priority) render stream
-// comes from another pool: the least priority where the device has one below normal, else the
-// greatest.  MOBILERT_SHADOW_PRIORITY=normal|least|greatest overrides this (A/B measurements).
-void createShadowStream(mrt_renderer* r) {
-    int least = 0, greatest = 0;
-    MRT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    int prio = least != 0 ? least : greatest;
-    if (const char* e = std::getenv("MOBILERT_SHADOW_PRIORITY")) {
-        const std::string v(e);
-        if (v == "normal") prio = 0;
-        else if (v == "least") prio = least;
-        else if (v == "greatest") prio = greatest;
+// Whether kernels launched on streams a and b run at the same time: two bounded spins, one per
+// stream, overlap in time iff the streams feed different hardware queues.
+bool streamsConcurrent(mrt_renderer* r, hipStream_t a, hipStream_t b) {
+    if (r->spinTimes == nullptr) r->spinTimes = r->sceneMem.alloc<unsigned long long>(4);
+    unsigned long long h[4] = {};
+    for (int round = 0; round < 2; ++round) {  // round 0 warms the queues up (created on first use)
+        mrt::launchSpin(r->spinTimes, 0, round == 0 ? 100 : 20000, a);  // 200 us
+        mrt::launchSpin(r->spinTimes, 1, round == 0 ? 100 : 20000, b);
+        MRT_HIP(hipStreamSynchronize(a));
+        MRT_HIP(hipStreamSynchronize(b));
     }
-    r->shadowPriority = prio;
-    MRT_HIP(hipStreamCreateWithPriority(&r->pipe.shadowStream, hipStreamNonBlocking, prio));
+    MRT_HIP(hipMemcpy(h, r->spinTimes, sizeof(h), hipMemcpyDeviceToHost));
+    return h[2] < h[1] && h[0] < h[3];
+}
+
+// The render chain runs on the renderer's own stream, the shadow walks on a second one, joined to
+// the caller's stream by events.  HIP maps a process's streams onto a few hardware queues
+// (GPU_MAX_HW_QUEUES, 4 by default, shared least-used); two streams on one queue run their kernels
+// one after the other, and the shadow walk of level L no longer overlaps level L + 1 (one rank's C4
+// shard at N = 8: 2.96 -> 3.80 ms with three streams of the front end created before the renderer,
+// DESIGN.md section 6).  So the pair is checked at creation with two timed spins, and the shadow
+// stream is created again (the earlier ones kept: they hold their queues) until the two run
+// concurrently; after kMaxShadowStreams tries the shadow walks are serialised on the render stream
+// (mrt_scene_info.shadowStreamConcurrent = 0).
+constexpr int kMaxShadowStreams = 8;
+void createShadowStream(mrt_renderer* r) {
+    for (int k = 0; k < kMaxShadowStreams; ++k) {
+        hipStream_t s = nullptr;
+        MRT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        if (r->pipe.shadowStream != nullptr) r->spareStreams.push_back(r->pipe.shadowStream);
+        r->pipe.shadowStream = s;
+        r->shadowTries = k + 1;
+        if (streamsConcurrent(r, r->stream, s)) {
+            r->shadowConcurrent = 1;
+            return;
+        }
+    }
+    r->shadowConcurrent = 0;
+    r->overlap = 0;
 }
 
 // Chunk size: every slot of the shard in one pass, within the path budget.
@@ -598,7 +625,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     // Orders: shade(L) -> shadow(L); shadow(L) -> shade(L+2) (shade(L+2) rewrites level L+2's
     // shadow queue only, but the walk kernels share nothing else, so the order is for the spill
     // stacks' sake: one per kernel kind); every shadow(L) -> resolve.
-    hipStream_t sb = r->overlap == 1 ? pp.shadowStream : st;
+    hipStream_t sb = r->overlap == 1 && r->shadowConcurrent != 0 ? pp.shadowStream : st;
     // The last level (depth RayDepthMax + 1) shades to zero whatever its rays hit: shade()
     // returns at the depth cap (PathTracer.cpp:24-26, Whitted.cpp:15-17), so its closest-hit
     // walk is dead work and is skipped.  Not for textured scenes (rayTrace writes the texel Kd
@@ -744,6 +771,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->triTests += hs[kStatTris];
     fs->shadowNodeRecords += hs[kStatNodesShadow];
     fs->shadowTriTests += hs[kStatTrisShadow];
+    fs->shadowOccluded += hs[kStatOccluded];
     fs->leafRecords += hs[kStatLeaves];
     fs->shadowLeafRecords += hs[kStatLeavesShadow];
     for (int l = 0; l < kMaxLevels && l < 16; ++l) {
@@ -838,6 +866,7 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs.shadowNodeRecords += prev.shadowNodeRecords;
                     fs.shadowTriTests += prev.shadowTriTests;
                     fs.leafRecords += prev.leafRecords;
+                    fs.shadowOccluded += prev.shadowOccluded;
                     fs.shadowLeafRecords += prev.shadowLeafRecords;
                     fs.fusedMs += prev.fusedMs;
                     fs.fusedLaunches += prev.fusedLaunches;
@@ -911,7 +940,8 @@ mrt_renderer* createRenderer(const mrt_config* cfg, const MemScene* mem = nullpt
     if (cfg->device >= 0) MRT_HIP(hipSetDevice(cfg->device));
     MRT_HIP(hipGetDevice(&r->device));
     MRT_HIP(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-    createShadowStream(r.get());
+    MRT_HIP(hipEventCreateWithFlags(&r->joinIn, hipEventDisableTiming));
+    MRT_HIP(hipEventCreateWithFlags(&r->joinOut, hipEventDisableTiming));
     hipDeviceProp_t prop;
     MRT_HIP(hipGetDeviceProperties(&prop, r->device));
     r->traceThreads = prop.multiProcessorCount * traceResidentThreadsPerCU();
@@ -944,6 +974,7 @@ mrt_renderer* createRenderer(const mrt_config* cfg, const MemScene* mem = nullpt
         if (!loadCameraFile(r->camPath, ratio, &r->cam, &err)) throw std::runtime_error(err);
     }
     uploadScene(r.get(), sc);
+    createShadowStream(r.get());
     buildUnits(r.get());
     allocQueues(r.get(), chunkFor(r.get()), 2);
     const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
@@ -1074,7 +1105,17 @@ int mrt_render_frame_device(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked,
     return guarded([&] {
         MRT_HIP(hipSetDevice(r->device));
         hipStream_t st = stream != nullptr ? static_cast<hipStream_t>(stream) : r->stream;
-        renderFrameDevice(r, dBitmap, dPacked, st);
+        if (st == r->stream) {
+            renderFrameDevice(r, dBitmap, dPacked, st);
+            return;
+        }
+        // the frame on the renderer's stream (its hardware queue is known to differ from the shadow
+        // stream's), ordered after the caller's work and before the caller's next
+        MRT_HIP(hipEventRecord(r->joinIn, st));
+        MRT_HIP(hipStreamWaitEvent(r->stream, r->joinIn, 0));
+        renderFrameDevice(r, dBitmap, dPacked, r->stream);
+        MRT_HIP(hipEventRecord(r->joinOut, r->stream));
+        MRT_HIP(hipStreamWaitEvent(st, r->joinOut, 0));
     });
 }
 
@@ -1122,7 +1163,8 @@ int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
     info->pixelSlots = r->nSlots;
     info->pixelSlotsMax = r->maxSlots;
     info->deviceBytes = static_cast<int64_t>(r->sceneMem.total + r->queueMem.total + r->frameMem.total);
-    info->shadowStreamPriority = r->shadowPriority;
+    info->shadowStreamConcurrent = r->shadowConcurrent;
+    info->shadowStreamsTried = r->shadowTries;
     return 0;
 }
 

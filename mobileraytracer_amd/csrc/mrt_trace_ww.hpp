@@ -506,6 +506,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             if (kCount) cnt->rayMax = max(cnt->rayMax, cnt->nodes - cnt->rayStart);
             if (kAny) {
                 out[rayIdx].w = occ ? 1.0F : 0.0F;
+                if (kCount) cnt->occluded += occ ? 1u : 0u;
                 occ = false;
             } else {
                 for (int j = 0; j < s.nLights; ++j) {  // Shader.cpp:166-171
@@ -586,6 +587,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                         if (occ) {
                             out[rayIdx].w = 1.0F;
                             rayIdx = -1;
+                            if (kCount) ++cnt->occluded;
                         }
                     } else {
                         src = fbits(d4.w);
@@ -760,6 +762,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 }
             }
             if (kAny && hit) {
+                if (kCount) cnt->occluded += (rayIdx >= 0 && pend == 0) ? 1u : 0u;  // (else counted at the merge)
                 if (rayIdx >= 0 && pend == 0) {
                     out[rayIdx].w = 1.0F;
                     rayIdx = -1;

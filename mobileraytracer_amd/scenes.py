@@ -195,6 +195,128 @@ def generate_conference(path):
     _write_obj(path, objs)
 
 
+# ---------------------------------------------------------------------------------------------
+# a second stand-in with the real Conference's flat character: large flat
+# wall / floor / table triangles, long thin slivers, abutting and overlapping coplanar panels - the
+# shapes that stress a cull bound and the quantized walk tree's margins at full frame, which the
+# rounded furniture of conference() does not
+
+def _box(center, half, ang=0.0, tilt=0.0):
+    """Axis-aligned box rotated by `tilt` about x then `ang` about y: 12 triangles, outward hints."""
+    c = np.asarray(center, dtype=np.float64)
+    h = np.asarray(half, dtype=np.float64)
+    sx = np.array([-1.0, 1.0])
+    corners = np.array([[x, y, z] for x in sx for y in sx for z in sx]) * h
+    ct, st = np.cos(tilt), np.sin(tilt)
+    y, z = corners[:, 1].copy(), corners[:, 2].copy()
+    corners[:, 1], corners[:, 2] = ct * y - st * z, st * y + ct * z
+    corners = _rot_y(corners, ang) + c
+    faces = [(0, 1, 3, 2), (4, 6, 7, 5), (0, 4, 5, 1), (2, 3, 7, 6), (0, 2, 6, 4), (1, 5, 7, 3)]
+    tris = []
+    for a, b, cc, d in faces:
+        tris.append([corners[a], corners[b], corners[cc]])
+        tris.append([corners[a], corners[cc], corners[d]])
+    tris = np.asarray(tris)
+    hints = tris.mean(1) - c
+    return tris, hints
+
+
+def _fan(center, rx, rz, y, n, up):
+    """Elliptic disk as a fan around its centre: n long thin triangles meeting at one point."""
+    a = 2.0 * np.pi * np.arange(n + 1) / n
+    ring = np.stack([center[0] + rx * np.cos(a), np.full(n + 1, y), center[1] + rz * np.sin(a)], 1)
+    ctr = np.array([center[0], y, center[1]])
+    tris = np.stack([np.broadcast_to(ctr, (n, 3)), ring[:-1], ring[1:]], 1)
+    return tris, np.broadcast_to(np.array([0.0, up, 0.0]), (n, 3))
+
+
+def _band(center, rx, rz, y0, y1, n):
+    """The rim of an elliptic disk: n tall thin quads (2n triangles), outward."""
+    a = 2.0 * np.pi * np.arange(n + 1) / n
+    ring = np.stack([center[0] + rx * np.cos(a), np.zeros(n + 1), center[1] + rz * np.sin(a)], 1)
+    lo, hi = ring + [0, y0, 0], ring + [0, y1, 0]
+    tris = np.concatenate([np.stack([lo[:-1], lo[1:], hi[1:]], 1), np.stack([lo[:-1], hi[1:], hi[:-1]], 1)], 0)
+    hints = tris.mean(1) - np.array([center[0], (y0 + y1) / 2, center[1]])
+    hints[:, 1] = 0.0
+    return tris, hints
+
+
+def _conference_flat_objects():
+    objs = []
+    X, Y, Z = 1200.0, 1040.0, 1440.0
+    add = lambda mat, th: objs.append((mat, _orient_and_quantize(*th)))  # noqa: E731
+    # floor: two abutting coplanar carpets with different subdivisions (T-junctions along x = 0)
+    add("mesh21_SG", _grid((-X, 0, -Z), (X, 0, 0), (0, 0, 2 * Z), 40, 60, (0, 1, 0)))
+    add("mesh29_SG", _grid((0, 0, -Z), (X, 0, 0), (0, 0, 2 * Z), 37, 53, (0, 1, 0)))
+    # ceiling: two large triangles, and a coplanar grid of acoustic tiles overlapping them exactly
+    add("mesh16_SG", _grid((-X, Y, -Z), (2 * X, 0, 0), (0, 0, 2 * Z), 1, 1, (0, -1, 0)))
+    add("mesh17_SG", _grid((-X, Y, -Z), (2 * X, 0, 0), (0, 0, 2 * Z), 30, 36, (0, -1, 0)))
+    # walls: two large triangles each, wainscot strips (tall slivers) coplanar in front of them
+    add("mesh19_SG", _grid((-X, 0, -Z), (0, Y, 0), (0, 0, 2 * Z), 1, 1, (1, 0, 0)))
+    add("mesh19_SG", _grid((X, 0, -Z), (0, Y, 0), (0, 0, 2 * Z), 1, 1, (-1, 0, 0)))
+    add("mesh20_SG", _grid((-X, 0, -Z), (2 * X, 0, 0), (0, Y, 0), 1, 1, (0, 0, 1)))
+    add("mesh20_SG", _grid((-X, 0, Z), (2 * X, 0, 0), (0, Y, 0), 1, 1, (0, 0, -1)))
+    add("mesh28_SG", _grid((-X, 0, -Z), (0, 300, 0), (0, 0, 2 * Z), 1, 240, (1, 0, 0)))
+    add("mesh28_SG", _grid((X, 0, -Z), (0, 300, 0), (0, 0, 2 * Z), 1, 240, (-1, 0, 0)))
+    # window blinds on both side walls: tilted slats, thin boxes of long slivers
+    for side in (-1.0, 1.0):
+        for k in range(60):
+            add("mesh9_SG", _box((side * (X - 40), 420 + 8 * k, 0), (2, 0.5, 500), tilt=0.5 * side))
+    # table: a fan-triangulated elliptic top (slivers to its centre), its rim, thin legs (mesh13: Ks)
+    add("mesh13_SG", _fan((0.0, 0.0), 240.0, 720.0, 380.0, 512, 1.0))
+    add("mesh13_SG", _fan((0.0, 0.0), 240.0, 720.0, 372.0, 512, -1.0))
+    add("mesh13_SG", _band((0.0, 0.0), 240.0, 720.0, 372.0, 380.0, 512))
+    for lx in (-150.0, 150.0):
+        for lz in (-600.0, 600.0):
+            add("mesh6_SG", _box((lx, 186, lz), (3, 186, 3)))
+    # paper sheets stacked on the table: parallel planes 1/16 apart, overlapping in plan
+    for k in range(40):
+        cx, cz = -160.0 + 80.0 * (k % 5), -600.0 + 150.0 * (k // 5)
+        for j in range(25):
+            y = 380.0 + (j + 1) / 16.0
+            add("mesh5_SG", _grid((cx - 40 + j, y, cz - 55), (80, 0, 0), (0, 0, 110), 1, 1, (0, 1, 0)))
+    # chairs: frames of thin bars, slatted seats and backs (mesh11 / mesh12: Ks)
+    for side in (-1.0, 1.0):
+        for i in range(8):
+            z = -630.0 + 180.0 * i
+            x = side * 340.0
+            for k in range(20):  # seat slats
+                add("mesh11_SG", _box((x, 230, z - 95 + 10 * k), (100, 2, 4)))
+            for k in range(20):  # back bars
+                add("mesh11_SG", _box((x + side * 100, 400, z - 95 + 10 * k), (2, 150, 3)))
+            for dx in (-90.0, 90.0):
+                for dz in (-90.0, 90.0):
+                    add("mesh12_SG", _box((x + dx, 114, z + dz), (2, 114, 2)))  # legs
+            for dz in (-100.0, 100.0):
+                add("mesh12_SG", _box((x, 300, z + dz), (90, 3, 3)))  # arms
+    return objs
+
+
+def generate_conference_flat(path):
+    objs = _conference_flat_objects()
+    total = sum(len(t) for _, t in objs)
+    rem = CONFERENCE_TRIANGLES - total
+    if rem < 0:
+        raise RuntimeError(f"flat conference stand-in over budget by {-rem} triangles")
+    # the bulk: louvred acoustic panelling on the far wall, 1/2 x 20 slivers (aspect 40), abutting
+    # and coplanar, 40 rows; any remainder as one strip of slivers
+    Z = 1440.0
+    rows = 40
+    cols = (rem // 2) // rows
+    if cols > 0:
+        add_t = _orient_and_quantize(*_grid((-cols / 4.0, 100, Z - 1), (cols / 2.0, 0, 0), (0, 800, 0), cols, rows,
+                                            (0, 0, -1)))
+        objs.append(("mesh20_SG", add_t))
+    rem = CONFERENCE_TRIANGLES - sum(len(t) for _, t in objs)
+    if rem > 0:
+        strip = _orient_and_quantize(*_grid((-600, 920, Z - 2), (1200, 0, 0), (0, 40, 0), rem, 1, (0, 0, -1)))
+        objs.append(("mesh23_SG", strip[:rem]))
+    objs.append(("light", _light_panel()))
+    n = sum(len(t) for m, t in objs if m != "light")
+    assert n == CONFERENCE_TRIANGLES, n
+    _write_obj(path, objs)
+
+
 def file_sha256(path):
     h = hashlib.sha256()
     with open(path, "rb") as f:
@@ -219,5 +341,18 @@ def conference():
     return obj, mtl, cam
 
 
+def conference_flat():
+    """(obj, mtl, cam) of the second, flat-geometry Conference stand-in (generate_conference_flat):
+    the same camera, materials and pinned counts, built from large flat triangles, slivers and
+    coplanar panels."""
+    d = os.path.join(SCENES, "conference")
+    obj = os.path.join(d, "conference_flat_standin.obj")
+    if not os.path.exists(obj):
+        tmp = obj + ".tmp.%d" % os.getpid()
+        generate_conference_flat(tmp)
+        os.replace(tmp, obj)
+    return obj, os.path.join(d, "conference.mtl"), os.path.join(d, "conference.cam")
+
+
 def is_standin(obj_path):
-    return os.path.basename(obj_path) == "conference_standin.obj"
+    return os.path.basename(obj_path) in ("conference_standin.obj", "conference_flat_standin.obj")

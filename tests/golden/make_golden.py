@@ -80,6 +80,7 @@ def main():
         print(name, out[name]["rays"])
     conf = scenes.conference()[0]
     out["conference_standin_obj_sha256"] = scenes.file_sha256(conf) if scenes.is_standin(conf) else None
+    out["conference_flat_standin_obj_sha256"] = scenes.file_sha256(scenes.conference_flat()[0])
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

@@ -335,3 +335,112 @@ def test_packet_walk_grazing_bundles(oracle_mod):
     o_.close()
     assert np.array_equal(ok, ref[0][sel]) and np.array_equal(oi, ref[1][sel])
     assert np.array_equal(ot.view(np.int32), ref[2][sel].view(np.int32))
+
+
+# ---- the flat-geometry stand-in (scenes.conference_flat): large flat triangles, slivers, abutting
+# and overlapping coplanar panels - the shapes that stress the certified leaf key, the quantized
+# walk tree's margins and the exact-t tie rule at full frame
+@pytest.fixture(scope="module")
+def c3_flat():
+    import mobileraytracer_amd as m
+    cfg = make_cfg(1920, 1080, shader=1, scene="conference_flat")
+    out = {}
+    with m.Renderer(cfg) as r:
+        for cull in (3, 0, 1):
+            r.set_tuning(2, cull)
+            bm = np.full(1920 * 1080, SENTINEL, np.int32)
+            r.render_frame(bm)
+            out[cull] = (bm, r.frame_stats(), r.primary_hits())
+    return cfg, out
+
+
+def test_flat_c3_primary_hits_and_bitmap_full_frame(oracle_mod, c3_flat):
+    cfg, out = c3_flat
+    bm, st, (k, i, t) = out[3]
+    o = oracle_for(oracle_mod, cfg)
+    ok, oi, ot = o.primary_hits()
+    o.close()
+    assert (ok >= 0).sum() == 1920 * 1072
+    assert np.array_equal(k, ok) and np.array_equal(i, oi)
+    assert np.array_equal(t.view(np.int32), ot.view(np.int32))
+    ref, ref_rays = oracle_full(oracle_mod, cfg)
+    assert np.array_equal(bm, ref), int((bm != ref).sum())
+    assert st["rays"] + st["shadowRays"] == ref_rays
+    for cull in (0,):  # no cull: the reference's visit set, the same image
+        assert np.array_equal(out[cull][0], bm) and all(np.array_equal(a, b) for a, b in zip(out[cull][2], out[3][2]))
+
+
+def test_flat_c4_pathtracer_full_frame(oracle_mod):
+    import mobileraytracer_amd as m
+    cfg = make_cfg(1920, 1080, shader=2, scene="conference_flat", spp=4, max_depth=5)
+    outs = {}
+    with m.Renderer(cfg) as r:
+        for cull in (3, 0):
+            r.set_tuning(2, cull)
+            bm = np.full(1920 * 1080, SENTINEL, np.int32)
+            r.render_frame(bm)
+            outs[cull] = (bm, r.frame_stats())
+    bm, st = outs[3]
+    assert st["primaryRays"] == 4 * 1920 * 1072
+    ref, ref_rays = oracle_full(oracle_mod, cfg)
+    assert np.array_equal(bm, ref), int((bm != ref).sum())
+    assert st["rays"] + st["shadowRays"] == ref_rays
+    assert np.array_equal(outs[0][0], bm)
+
+
+def test_flat_grazing_rays_along_surfaces(oracle_mod):
+    """Rays starting ON the flat stand-in's triangles (walls, floor panels, table, paper sheets,
+    slivers) and leaving at 1e-6 .. 1e-2 rad from their plane, with the triangle as the source
+    primitive (self-exclusion, Triangle.cpp:64-66): the grazing, nearly coplanar case in which
+    Moller-Trumbore's t can fall before a triangle's box entry.  Closest hit and shadow test equal
+    the reference walk in every cull mode except the documented inexact one, and a sample the oracle."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, shader=1, scene="conference_flat")
+    from mobileraytracer_amd import scenes
+    obj = scenes.conference_flat()[0]
+    verts, faces = [], []
+    with open(obj) as f:
+        for line in f:
+            if line.startswith("v "):
+                verts.append([float(x) for x in line.split()[1:4]])
+            elif line.startswith("f "):
+                faces.append([int(x) - 1 for x in line.split()[1:4]])
+    V = np.asarray(verts, np.float64)
+    V[:, 0] = -V[:, 0]  # the loader negates X (OBJLoader.cpp:139-141)
+    F = np.asarray(faces)[:-2]  # the last two faces are the light panel
+    rng = np.random.default_rng(31)
+    n = 200_000
+    pick = rng.integers(0, len(F), n)
+    A, B, C = V[F[pick, 0]], V[F[pick, 1]], V[F[pick, 2]]
+    w = rng.random((n, 2))
+    w[w.sum(1) > 1] = 1 - w[w.sum(1) > 1]
+    o = A + w[:, :1] * (B - A) + w[:, 1:] * (C - A)
+    nrm = np.cross(B - A, C - A)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    tang = rng.normal(size=(n, 3))
+    tang -= (tang * nrm).sum(1, keepdims=True) * nrm
+    tang /= np.linalg.norm(tang, axis=1, keepdims=True)
+    ang = 10.0 ** rng.uniform(-6, -2, n) * rng.choice([-1.0, 1.0], n)
+    d = tang * np.cos(ang)[:, None] + nrm * np.sin(ang)[:, None]
+    o32, d32 = o.astype(np.float32), (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    src = np.stack([np.full(n, 3), pick], 1).astype(np.int32)  # (kind triangle, input index)
+    dist = (rng.random(n) * 3000.0).astype(np.float32)
+    res = {}
+    with m.Renderer(cfg) as r:
+        for walk, cull in ((0, 0), (1, 0), (1, 2), (1, 3)):
+            r.set_tuning(1, walk)
+            r.set_tuning(2, cull)
+            res[(walk, cull)] = (r.trace_rays(o32, d32, src=src), r.trace_rays(o32, d32, dist=dist, src=src, any_hit=True)[0])
+    ref_hits, ref_occ = res[(0, 0)]
+    assert (ref_hits[0] == 3).mean() > 0.5
+    for key, (hits, occ) in res.items():
+        assert all(np.array_equal(x, y) for x, y in zip(hits, ref_hits)), key
+        assert np.array_equal(occ, ref_occ), key
+    ob = oracle_for(oracle_mod, cfg)
+    sel = np.arange(0, n, 20)
+    ok, oi, ot = ob.trace_rays(o32[sel], d32[sel], src=src[sel])
+    oocc = ob.trace_rays(o32[sel], d32[sel], dist=dist[sel], src=src[sel], any_hit=True)[0]
+    ob.close()
+    assert np.array_equal(ok, ref_hits[0][sel]) and np.array_equal(oi, ref_hits[1][sel])
+    assert np.array_equal(ot.view(np.int32), ref_hits[2][sel].view(np.int32))
+    assert np.array_equal(oocc, ref_occ[sel])

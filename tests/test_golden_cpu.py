@@ -61,6 +61,30 @@ def test_conference_standin_is_pinned(golden):
     assert scenes.file_sha256(obj) == golden["conference_standin_obj_sha256"]
 
 
+def test_conference_flat_standin_is_pinned(golden):
+    """The flat-geometry stand-in (scenes.conference_flat): pinned bytes, and the counts the
+    reference pins for the real Conference (scripts/test/docker/dockerfile.sh:118-119: 331,179
+    triangles, 2 lights), read back through the product's own loader and BVH build (host only)."""
+    import mobileraytracer_amd as m
+    from mobileraytracer_amd import scenes
+    obj, mtl, cam = scenes.conference_flat()
+    assert scenes.file_sha256(obj) == golden["conference_flat_standin_obj_sha256"]
+    cfg = m.Config(width=64, height=64, shader=1, sceneIndex=-1, objFilePath=obj, mtlFilePath=mtl, camFilePath=cam)
+    _, _, cnt, order = m.triangle_bvh(cfg)
+    assert len(order) == scenes.CONFERENCE_TRIANGLES
+    assert cnt.sum() == scenes.CONFERENCE_TRIANGLES
+    faces = light = 0
+    group = None
+    with open(obj) as f:
+        for line in f:
+            if line.startswith("usemtl "):
+                group = line.split()[1]
+            elif line.startswith("f "):
+                faces += 1
+                light += group == "light"
+    assert faces - light == scenes.CONFERENCE_TRIANGLES and light == scenes.CONFERENCE_LIGHTS
+
+
 def _declared_symbols():
     names = set()
     for hdr in ("mobilert_amd.h", "mobilert_amd.hpp"):

@@ -22,7 +22,8 @@ SENTINEL = np.int32(0x12345678)  # alpha 0x12: never produced by incrementalAvg 
 
 def scene_paths(name):
     from mobileraytracer_amd import scenes
-    return {"water": scenes.cornell_water, "teapot": scenes.teapot, "conference": scenes.conference}[name]()
+    return {"water": scenes.cornell_water, "teapot": scenes.teapot, "conference": scenes.conference,
+            "conference_flat": scenes.conference_flat}[name]()
 
 
 def make_cfg(width, height, shader=1, scene=None, spp=1, spl=1, max_depth=6, **kw):
@@ -596,23 +597,26 @@ def test_shard_assembly_is_identical_to_single_gpu():
 
 
 def test_shadow_overlap_survives_rccl_streams():
-    """The renderer keeps its shadow walks on a stream of another priority than the render stream,
-    so the two never share a hardware queue, whatever streams the process created before it: one
-    rank's C4 shard at N = 8 renders as fast with an RCCL process group (and its streams) created
-    BEFORE the renderer as without one (round 3 measured 3.54 against 2.81 ms when they shared a
-    queue).  Two fresh processes (tools/stream_probe.py), HIP's default hardware-queue count."""
+    """The renderer checks at creation that its shadow stream runs beside its render stream (two
+    timed spins overlap: different hardware queues) and creates it again until it does, so the
+    overlap holds whatever streams the process created before: one rank's C4 shard at N = 8 renders
+    as fast with an RCCL process group and three front-end streams created BEFORE the renderer as
+    without them (round 4 measured 3.80 against 2.96 ms when the two shared a queue).  Fresh
+    processes (tools/stream_probe.py), HIP's default hardware-queue count."""
     import json, subprocess, sys
     env = dict(os.environ)
     env.pop("GPU_MAX_HW_QUEUES", None)
     probe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "stream_probe.py")
     out = {}
-    for first in (False, True):
-        cmd = [sys.executable, probe, "--frames", "30"] + (["--pg-first"] if first else [])
+    cases = {"direct": [], "extra3": ["--extra-streams", "3"], "pg+extra3": ["--pg-first", "--extra-streams", "3"]}
+    for name, extra in cases.items():
+        cmd = [sys.executable, probe, "--frames", "30"] + extra
         res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
         assert res.returncode == 0, res.stderr[-2000:]
-        out[first] = json.loads(res.stdout.strip().splitlines()[-1])
-    assert out[True]["shadow_stream_priority"] != 0
-    assert out[True]["ms_per_frame"] < 1.08 * out[False]["ms_per_frame"], out
+        out[name] = json.loads(res.stdout.strip().splitlines()[-1])
+    for name in cases:
+        assert out[name]["shadow_stream_concurrent"] == 1, out
+        assert out[name]["ms_per_frame"] < 1.08 * out["direct"]["ms_per_frame"], out
 
 
 def test_shard_assembly_over_many_ranks():

@@ -28,6 +28,7 @@ def profiled_workload(extra):
     for k, v in (("--width", 1920), ("--height", 1080), ("--spp", 4), ("--max-depth", 5), ("--shader", 2),
                  ("--shard-of", 0)):
         p.add_argument(k, type=int, default=v)
+    p.add_argument("--scene", default="conference")
     a, _ = p.parse_known_args(extra)
     return workload_key(a, a.shard_of if a.shard_of > 1 else 0)
 

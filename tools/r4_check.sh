@@ -13,10 +13,8 @@ timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench.log 2>&1 || { e
 tail -1 $OUT/bench.log > $OUT/bench.json; cut -c1-400 $OUT/bench.json
 if [ "${PROBE:-1}" = "1" ]; then
   unset GPU_MAX_HW_QUEUES
-  for p in normal least greatest; do
-    for f in "" "--pg-first"; do
-      MOBILERT_SHADOW_PRIORITY=$p timeout -k 10 120 python tools/stream_probe.py $f >> $OUT/probe.log 2>&1 || { echo probe failed; tail $OUT/probe.log; exit 5; }
-      echo "$p $f $(tail -1 $OUT/probe.log)"
-    done
+  for f in "" "--pg-first" "--extra-streams 1" "--extra-streams 2" "--extra-streams 3" "--pg-first --extra-streams 3"; do
+    timeout -k 10 120 python tools/stream_probe.py $f >> $OUT/probe.log 2>&1 || { echo probe failed; tail $OUT/probe.log; exit 5; }
+    echo "$f $(tail -1 $OUT/probe.log)"
   done
 fi

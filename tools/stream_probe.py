@@ -20,6 +20,10 @@ def main():
     p.add_argument("--pg-first", action="store_true")
     p.add_argument("--ranks", type=int, default=8)
     p.add_argument("--frames", type=int, default=20)
+    # normal-priority streams created (and used) before the renderer, as a front end's own streams
+    # would be: with HIP's 4 hardware queues per pool they make a later normal-priority stream share
+    # a queue with the render stream
+    p.add_argument("--extra-streams", type=int, default=0)
     a = p.parse_args()
     import torch
     import torch.distributed as dist
@@ -35,6 +39,11 @@ def main():
         packed0 = torch.zeros(1 << 20, dtype=torch.int32, device="cuda")
         dist.gather(packed0, [torch.empty_like(packed0)], dst=0)
         torch.cuda.synchronize()
+    extra = [torch.cuda.Stream() for _ in range(a.extra_streams)]
+    for st in extra:
+        with torch.cuda.stream(st):
+            torch.ones(1024, device="cuda").sum()
+    torch.cuda.synchronize()
     o, l, c = scenes.conference()
     cfg = m.Config(width=1920, height=1080, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5, objFilePath=o,
                    mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=a.ranks, device=0)
@@ -49,8 +58,9 @@ def main():
         r.render_frame_device(0, packed.data_ptr(), sh)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / a.frames * 1e3
-    print(json.dumps({"pg_first": a.pg_first, "ranks": a.ranks, "ms_per_frame": ms,
-                      "shadow_stream_priority": r.scene_info()["shadowStreamPriority"],
+    print(json.dumps({"pg_first": a.pg_first, "extra_streams": a.extra_streams, "ranks": a.ranks, "ms_per_frame": ms,
+                      "shadow_stream_concurrent": r.scene_info()["shadowStreamConcurrent"],
+                      "shadow_streams_tried": r.scene_info()["shadowStreamsTried"],
                       "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}), flush=True)
     r.close()
     if a.pg_first:

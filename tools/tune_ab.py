@@ -49,6 +49,19 @@ def main():
         print(f"setting {k}: frame {np.median(res[k]):.3f} ms (min {np.min(res[k]):.3f})", flush=True)
     for k in variants[1:]:
         print(f"setting {k} identical image:", torch.equal(bufs[variants[0]], bufs[k]))
+    if os.environ.get("COUNT") == "1":  # one counting frame per setting: walk statistics
+        for k, r in rs.items():
+            bm, pk = (bufs[k].data_ptr(), 0) if ranks == 1 else (0, bufs[k].data_ptr())
+            r.set_profiling(counting=True)
+            r.render_frame_device(bm, pk, sh)
+            torch.cuda.synchronize()
+            f = r.frame_stats()
+            r.set_profiling()
+            sr = max(1, f["shadowRays"])
+            print(f"counts {k}: closest records/ray {f['nodeRecords'] / max(1, f['walkedRays']):.2f} "
+                  f"tris/ray {f['triTests'] / max(1, f['walkedRays']):.2f} | shadow records/ray "
+                  f"{f['shadowNodeRecords'] / sr:.2f} tris/ray {f['shadowTriTests'] / sr:.2f} leaves/ray "
+                  f"{f['shadowLeafRecords'] / sr:.2f} occluded {f['shadowOccluded'] / sr:.3f}", flush=True)
 
 
 main()
