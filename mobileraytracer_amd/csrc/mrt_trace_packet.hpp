@@ -8,9 +8,14 @@
 // still decides its own leaves exactly as the per-lane walk does (traceWhileWhile): its own test
 // of the reference leaf box, the certified leaf cull of the exact mode, and its own triangle
 // tests (triangle records again scalar loads).  The packet visits a superset of each lane's
-// nodes and its lanes test exactly the leaves they would test alone; betterThan is a total order,
-// so each lane's closest hit is the per-lane walk's, bit for bit (tested: full frames and random
-// rays in tests/).  No lane diverges inside the loop, so VALU lanes stay busy on coherent rays.
+// inner nodes.  Its lanes test exactly the leaves they would test alone PROVIDED every quantized
+// box on the path to a leaf holds that leaf's exact box as the slab test computes it, for every
+// lane's ray (the Quantizer's one-grid-step margin): then a lane reaches a
+// leaf in the packet iff its own walk would, and the exact leaf-box test and the certified leaf key
+// decide as they do alone.  betterThan is a total order, so each lane's closest hit is the per-lane
+// walk's, bit for bit (tested: full frames, random rays, and coherent 64-ray bundles grazing
+// leaf-box corners, edges and faces in tests/test_full_frame.py).  No lane diverges inside the
+// loop, so VALU lanes stay busy on coherent rays.
 // Cull modes 0 (none) and 3 (exact) only: neither culls an inner node.
 #pragma once
 

@@ -2,21 +2,25 @@
 //
 // Same reachability, culling and tie rules as traverse<> in mrt_device.hpp (so results are
 // identical, tested), organised for SIMD efficiency on CDNA's 64-lane waves:
-//   * inner nodes are walked until EVERY active lane has found a leaf (leaves are postponed
-//     one at a time), then all lanes test their leaves together: inner-node and leaf code no
-//     longer alternate inside one wave iteration;
-//   * lanes whose ray has finished take a new ray (one wave-aggregated atomic per refill, once
-//     kRefill lanes are idle) instead of idling until the slowest ray of a 64-ray batch is done;
-//   * 8 work cursors per level, one per XCD group of workgroups (blockIdx % 8), each over a
-//     contiguous eighth of the queue (adjacent rays are spatially coherent, so an XCD's L2 sees
-//     one region of the scene); a drained eighth is left for the next;
+//   * the walk tree is the reference's leaves regrouped and collapsed to a quantized 4-wide tree
+//     (QNode4: 16-bit grid boxes rounded outward, exact leaf boxes tested before the triangles);
+//   * inner nodes are walked while lanes look for a leaf (one leaf is postponed per lane), then the
+//     lanes test their leaves together.  The inner phase ends once fewer than kInnerExit lanes still
+//     look for a leaf and the leaf phase once fewer than kLeafExit lanes hold one: the others keep
+//     their leaf or their place in the walk for the next round, so every lane visits the same nodes
+//     and tests the same leaves in the same order as without the early exits;
+//   * lanes whose ray has finished take a new one from the walk's queue policy (LevelQueue: one
+//     wave-aggregated atomic per refill on 8 per-XCD-group cursors, once DScene::refill lanes are
+//     idle; a wave-private pool for the tile kernel) instead of idling until the slowest ray of a
+//     64-ray batch is done;
+//   * in a queue's tail, idle lanes take pending subtrees of walking lanes of their wave (donation);
 //   * the top kTopNodes inner nodes (breadth-first numbering) are read from an LDS copy;
 //   * node and triangle gathers are buffer loads of exact width with 32-bit offsets.
 // Planes / spheres (tiny BVHs, empty for OBJ scenes) are tested at ray fetch with the simple
 // walker, area lights when the triangle walk ends, in the reference's category order.
 //
-// Measured alternatives (removed from the build after A/B on MI355X): 4-wide
-// nodes, compressed 32-B nodes, tail assist, trimmed grids, last-occluder shadow test, one
+// Measured alternatives (removed after A/B on MI355X): 8-wide nodes, packed
+// 32-B nodes, binary16 grid indices, tail assist, trimmed grids, a last-occluder shadow probe, one
 // launch for all levels, ray sorting, concurrent chunk pipelines - all result-invariant and all
 // slower than this walk on the C4 frame.
 #pragma once
@@ -406,13 +410,62 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
     __syncthreads();
 }
 
-// kAny = false: closest hit -> out[i] = (t, u, v, primitive code);
-// kAny = true:  shadow any-hit -> out[i].w = occluded flag.
-// fetch: kWalkShards cursors, kFetchStride ints apart.
-template <bool kAny, bool kCount, int kCull, class Stack>
-__device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
-                                                const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                Stack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest) {
+// The rays a walk takes: a queue policy.
+//   o(i), d(i)      ray i's origin / direction records;
+//   hit(i, h)       the closest hit (t, u, v, primitive code); occ(i, f): the occluded flag;
+//   take(pending)   called by every lane of the wave (wave-uniform control flow) with the mask of
+//                   lanes wanting a ray: this lane's ray index, or -1 (none left for it);
+//   drained()       wave-uniform: the queue has no ray left for this wave.
+// LevelQueue: a level's queue arrays, rays [0, count), fetched through kWalkShards cursors
+// (kFetchStride ints apart), one per XCD group of workgroups (blockIdx % 8), each over a contiguous
+// eighth of the queue; a drained eighth is left for the next (speed only: any placement gives the
+// same results).
+struct LevelQueue {
+    const float4* __restrict__ rO;
+    const float4* __restrict__ rD;
+    float4* out;
+    int count;
+    int* fetch;
+    int seg = static_cast<int>(blockIdx.x % kWalkShards);  // wave-uniform cursor state
+    int segsLeft = kWalkShards;
+    __device__ __forceinline__ LevelQueue(const float4* o_, const float4* d_, float4* out_, int count_, int* fetch_)
+        : rO(o_), rD(d_), out(out_), count(count_), fetch(fetch_) {}
+    __device__ __forceinline__ float4 o(int i) const { return rO[i]; }
+    __device__ __forceinline__ float4 d(int i) const { return rD[i]; }
+    __device__ __forceinline__ void hit(int i, float4 h) const { out[i] = h; }
+    __device__ __forceinline__ void occ(int i, float f) const { out[i].w = f; }
+    __device__ __forceinline__ bool drained() const { return segsLeft == 0; }
+    __device__ __forceinline__ int take(uint64_t pending) {
+        const int lane = static_cast<int>(threadIdx.x & 63u);
+        int got = -1;
+        while (pending != 0 && segsLeft > 0) {
+            const int n = __popcll(pending);
+            const int leader = __ffsll(static_cast<unsigned long long>(pending)) - 1;
+            const int segStart = static_cast<int>((static_cast<long long>(count) * seg) / kWalkShards);
+            const int segEnd = static_cast<int>((static_cast<long long>(count) * (seg + 1)) / kWalkShards);
+            int base = 0;
+            if (lane == leader) base = atomicAdd(fetch + seg * kFetchStride, n);
+            base = __shfl(base, leader, 64);
+            const bool mine = ((pending >> lane) & 1ull) != 0;
+            if (mine) {
+                const int idx = segStart + base + lanesBelowIn(pending);
+                if (idx < segEnd) got = idx;
+            }
+            pending = __ballot(mine && got < 0);
+            if (pending != 0) {
+                seg = (seg + 1) % kWalkShards;
+                --segsLeft;
+            }
+        }
+        return got;
+    }
+};
+
+// kAny = false: closest hit -> q.hit(i, (t, u, v, primitive code));
+// kAny = true:  shadow any-hit -> q.occ(i, occluded flag).
+template <bool kAny, bool kCount, int kCull, class Stack, class Queue>
+__device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stack& st, TravCount* cnt,
+                                                 const QNode4* ldsTop, int* tailBest) {
     constexpr int kHelper = -2;  // rayIdx of a lane walking a subtree given by another lane
     const bool donate = s.tailDonate != 0;
     const int top = min(kWalkTop, s.triTop);
@@ -435,8 +488,6 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
     uint32_t bcode = kNoPrim;
     int ref = kRefDone;
     int leaf = 0;  // < 0: a postponed leaf
-    int seg = static_cast<int>(blockIdx.x % kWalkShards);  // wave-uniform cursor state
-    int segsLeft = kWalkShards;
     // tail donation (DScene::tailDonate): a helper lane walks a subtree of its owner's ray and
     // hands its best hit (closest) or occlusion (any) back; the owner finishes when all its
     // helpers have.  Exact: the owner and its helpers visit the owner's subtrees between them,
@@ -505,7 +556,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         if (doneLane && runDone) {
             if (kCount) cnt->rayMax = max(cnt->rayMax, cnt->nodes - cnt->rayStart);
             if (kAny) {
-                out[rayIdx].w = occ ? 1.0F : 0.0F;
+                q.occ(rayIdx, occ ? 1.0F : 0.0F);
                 if (kCount) cnt->occluded += occ ? 1u : 0u;
                 occ = false;
             } else {
@@ -528,7 +579,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                     const float4* g = kind == kTriangle ? s.triGeom + 3 * primIndex(bcode) : s.lights + 4 * primIndex(bcode);
                     (void)triTest(g[0], g[1], g[2], o, d, &t, &u, &v);
                 }
-                out[rayIdx] = make_float4(bt, u, v, bitsf(bcode));
+                q.hit(rayIdx, make_float4(bt, u, v, bitsf(bcode)));
             }
             rayIdx = -1;
         }
@@ -541,29 +592,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             needMask = 0;
         }
         if (needMask != 0) {
-            int got = -1;
-            // per-XCD-group cursors over contiguous ray ranges; an empty range is left for the
-            // next one (speed only: any placement gives the same results)
-            uint64_t pending = needMask;
-            while (pending != 0 && segsLeft > 0) {
-                const int n = __popcll(pending);
-                const int leader = __ffsll(static_cast<unsigned long long>(pending)) - 1;
-                const int segStart = static_cast<int>((static_cast<long long>(count) * seg) / kWalkShards);
-                const int segEnd = static_cast<int>((static_cast<long long>(count) * (seg + 1)) / kWalkShards);
-                int base = 0;
-                if (lane == leader) base = atomicAdd(fetch + seg * kFetchStride, n);
-                base = __shfl(base, leader, 64);
-                const bool mine = ((pending >> lane) & 1ull) != 0;
-                if (mine) {
-                    const int idx = segStart + base + lanesBelowIn(pending);
-                    if (idx < segEnd) got = idx;
-                }
-                pending = __ballot(mine && got < 0);
-                if (pending != 0) {
-                    seg = (seg + 1) % kWalkShards;
-                    --segsLeft;
-                }
-            }
+            const int got = q.take(needMask);
             if (need) {
                 rayIdx = got;
                 if (kCount) {
@@ -573,8 +602,8 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                 if (rayIdx < 0) {
                     exhausted = true;
                 } else {
-                    const float4 o4 = rOs[rayIdx];
-                    const float4 d4 = rDs[rayIdx];
+                    const float4 o4 = q.o(rayIdx);
+                    const float4 d4 = q.d(rayIdx);
                     o = xyz(o4);
                     d = xyz(d4);
                     inv = v3{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
@@ -585,7 +614,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
                         bool occ = traverse<kPlane, true>(s, s.planeNodes, s.planeRoot, o, d, inv, src, &b, st, cnt);
                         occ = occ || traverse<kSphere, true>(s, s.sphereNodes, s.sphereRoot, o, d, inv, src, &b, st, cnt);
                         if (occ) {
-                            out[rayIdx].w = 1.0F;
+                            q.occ(rayIdx, 1.0F);
                             rayIdx = -1;
                             if (kCount) ++cnt->occluded;
                         }
@@ -623,7 +652,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
         }
         // ---- a level's tail: idle lanes take the next pending subtree of a walking lane ----
         if (donate) {
-            uint64_t idle = __ballot(rayIdx == -1 && (exhausted || segsLeft == 0));
+            uint64_t idle = __ballot(rayIdx == -1 && (exhausted || q.drained()));
             if (idle != 0 && !tailMode) {  // the owners' shared words
                 tailMode = true;
                 if (rayIdx >= 0) waveBest[lane] = kAny ? 0x7FFFFFFF : __float_as_int(bt);
@@ -764,7 +793,7 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             if (kAny && hit) {
                 if (kCount) cnt->occluded += (rayIdx >= 0 && pend == 0) ? 1u : 0u;  // (else counted at the merge)
                 if (rayIdx >= 0 && pend == 0) {
-                    out[rayIdx].w = 1.0F;
+                    q.occ(rayIdx, 1.0F);
                     rayIdx = -1;
                 } else {  // a helper, or an owner waiting for helpers: the merge writes it
                     occ = true;
@@ -785,6 +814,15 @@ __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* _
             if (__popcll(__ballot(leaf < 0)) < kLeafExit) break;
         }
     }
+}
+
+// A level's queue arrays (k_trace / k_shadow): rays [0, count) of rOs / rDs, results into out.
+template <bool kAny, bool kCount, int kCull, class Stack>
+__device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
+                                                const float4* __restrict__ rDs, float4* out, int count, int* fetch,
+                                                Stack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest) {
+    LevelQueue q(rOs, rDs, out, count, fetch);
+    traceWhileWhileQ<kAny, kCount, kCull>(s, q, st, cnt, ldsTop, tailBest);
 }
 
 }  // namespace mrt
