@@ -125,6 +125,8 @@ typedef struct mrt_frame_stats {
     int64_t fusedLaunches;         /* fused level-1 launches of the frame (counted in shadeLaunches too) */
     uint64_t levelShadedVertices[16]; /* counting pass only: shadedVertices of depth 1..16 */
     uint64_t shadowOccluded;       /* counting pass only: occluded shadow rays */
+    double tileMs;                 /* profiling: duration of the tile kernel launches (k_tiles) */
+    int64_t tileLaunches;          /* tile kernel launches of the frame (0: the level kernels ran) */
 } mrt_frame_stats;
 
 /* A named byte buffer (a map_Kd texture file handed over by the Android front end). */

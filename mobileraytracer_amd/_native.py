@@ -75,7 +75,7 @@ class MrtFrameStats(ctypes.Structure):
         ("levelLeafRecords", ctypes.c_uint64 * 16),
         ("fusedMs", ctypes.c_double), ("fusedLaunches", ctypes.c_int64),
         ("levelShadedVertices", ctypes.c_uint64 * 16),
-        ("shadowOccluded", ctypes.c_uint64),
+        ("shadowOccluded", ctypes.c_uint64), ("tileMs", ctypes.c_double), ("tileLaunches", ctypes.c_int64),
     ]
 
 

@@ -148,6 +148,15 @@ struct mrt_renderer {
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
     bool fusedL1 = false;                // the last pass ran level 1 as k_trace_packet_shade
+    bool tilePass = false;               // the last pass ran the tile kernel (k_tiles)
+    bool tileOverflowed = false;         // a tile pass overflowed its per-tile queues: level kernels from then on
+    int tileGrowth = 2;                  // tile queue capacity per level: growth x 64 rays (tuning key 23)
+    int tileMaxNew = 2;                  // tiles a wave claims per round at most (tuning key 20)
+    int tilePoolTarget = 256;            // ... while its next walk pool has fewer rays (tuning key 21)
+    int tileRefill = 8;                  // the tile walks' refill threshold (tuning key 22)
+    DeviceMem tileMem;                   // the tile kernel's per-wave arenas
+    size_t tileArenaBytes = 0;
+    char* tileArena = nullptr;
     unsigned long long* hostStats = nullptr;  // pinned: the per-pass statistics read back by DMA
 
     // host copies for the GL preview of the Android front end (mrt_preview_arrays; kept only for
@@ -638,6 +647,64 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     // every material is finite (Ks * 0 and Kd * 0 added to sums that start at +0), and the
     // parents write no payload for them (only their count)
     const bool skipLastShade = skipLast && nLevels >= 2 && r->ds.matsFinite != 0;
+    // The tile kernel (k_tiles: every wave renders whole tiles through their ray trees, no grid-wide
+    // barrier per level) where it applies: the whole pass in one launch.
+    r->tilePass = false;
+    if (skipLastShade && !r->tileOverflowed && canTile(shader, r->ds, sa, spp) && !r->stopFlag.load()) {
+        r->tilePass = true;
+        r->fusedL1 = false;
+        const int grid = tileGrid(shader, r->ds, r->traceThreads);
+        const int tilePixels = std::max(1, 64 / spp);
+        const int capN = 64 * r->tileGrowth;
+        const long long slotBytes = tileSlotBytes(64, capN, spl, r->maxDepth);
+        const size_t need = static_cast<size_t>(grid) * (kBlock / 64) * kTileSlots * static_cast<size_t>(slotBytes);
+        if (r->tileArenaBytes < need) {
+            r->tileMem.release();
+            r->tileArena = r->tileMem.alloc<char>(need);
+            r->tileArenaBytes = need;
+        }
+        MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
+        TileArgs ta{};
+        ta.ra.cam = r->cam;
+        ta.ra.map = map;
+        ta.ra.tables = r->ds.tables;
+        ta.ra.jitter = r->ds.jitterDraws;
+        ta.ra.width = r->cfg.width;
+        ta.ra.height = r->cfg.height;
+        ta.ra.slotBase = 0;
+        ta.ra.nPaths = r->nSlots * spp;
+        ta.ra.spp = spp;
+        ta.ra.sppTotal = r->cfg.samplesPixel;
+        setPixelSampler(r, &ta.ra);
+        ta.ra.sampleBase = sampleBase;
+        ta.sa = sa;
+        ta.aa.map = map;
+        ta.aa.width = r->cfg.width;
+        ta.aa.slotBase = 0;
+        ta.aa.nSlots = r->nSlots;
+        ta.aa.spp = spp;
+        ta.aa.sampleBase = sampleBase;
+        ta.bitmap = dBitmap;
+        ta.packed = dPacked;
+        ta.arena = r->tileArena;
+        ta.slotBytes = slotBytes;
+        ta.cap1 = 64;
+        ta.capN = capN;
+        ta.spl = spl;
+        ta.tilePixels = tilePixels;
+        ta.nSlots = r->nSlots;
+        ta.nTiles = (r->nSlots + tilePixels - 1) / tilePixels;
+        ta.maxNew = r->tileMaxNew;
+        ta.poolTarget = r->tilePoolTarget;
+        ta.claim = pp.counters + kCntFetchShards;  // level 0's cursors (the walks use levels >= 1)
+        ta.counters = pp.counters;
+        r->ds.refill = r->tileRefill;
+        if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
+        launchTiles(shader, r->ds, ta, grid, pp.gstack, r->gdepth, st);
+        if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
+        launchTally(pp.counters, nLevels, pp.stats, st, skipLast ? nLevels : 0);
+        return;
+    }
     for (int slot0 = 0; slot0 < r->nSlots && !r->stopFlag.load(); slot0 += r->chunkSlots) {
         const int nChunk = std::min(r->chunkSlots, r->nSlots - slot0);
         MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
@@ -762,7 +829,10 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     unsigned long long hs[kNumStats];
     std::memcpy(hs, r->hostStats, sizeof(hs));
     const auto t1 = std::chrono::steady_clock::now();
-    if (hs[kStatOverflow] != 0) return false;
+    if (hs[kStatOverflow] != 0) {
+        if (r->tilePass) r->tileOverflowed = true;  // (the retry renders with the level kernels)
+        return false;
+    }
     fs->rays += hs[kStatRays];
     fs->shadowRays += hs[kStatShadowRays];
     fs->walkedRays += hs[kStatRays] - hs[kStatSkipped];
@@ -788,7 +858,12 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
         fs->levelShadowRays[l] += hs[kStatLevelShadows + l];
     }
     fs->frameMs += std::chrono::duration<double, std::milli>(t1 - t0).count();
-    if (r->profileFlags & 1) {
+    if ((r->profileFlags & 1) && r->tilePass) {
+        float ms = 0.0F;
+        MRT_HIP(hipEventElapsedTime(&ms, r->pipe.evPool[0], r->pipe.evPool[1]));
+        fs->tileMs += ms;
+        fs->tileLaunches += 1;
+    } else if (r->profileFlags & 1) {
         const mrt_renderer::Pipe& pp = r->pipe;
         for (size_t e = 0; e + 4 < pp.evCount; e += 5) {
             float ta = 0.0F, tb = 0.0F, tc = 0.0F;
@@ -869,6 +944,8 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs.shadowOccluded += prev.shadowOccluded;
                     fs.shadowLeafRecords += prev.shadowLeafRecords;
                     fs.fusedMs += prev.fusedMs;
+                    fs.tileMs += prev.tileMs;
+                    fs.tileLaunches += prev.tileLaunches;
                     fs.fusedLaunches += prev.fusedLaunches;
                     fs.maxNodeRecordsPerRay = std::max(fs.maxNodeRecordsPerRay, prev.maxNodeRecordsPerRay);
                     fs.shadedVertices += prev.shadedVertices;
@@ -1163,6 +1240,7 @@ int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
     info->pixelSlots = r->nSlots;
     info->pixelSlotsMax = r->maxSlots;
     info->deviceBytes = static_cast<int64_t>(r->sceneMem.total + r->queueMem.total + r->frameMem.total);
+    info->deviceBytes += static_cast<int64_t>(r->tileMem.total);
     info->shadowStreamConcurrent = r->shadowConcurrent;
     info->shadowStreamsTried = r->shadowTries;
     return 0;
@@ -1276,6 +1354,27 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
     }
     if (key == 17 && (value == 0 || value == 1)) {
         r->ds.fuseShade = value;
+        return 0;
+    }
+    if (key == 19 && (value == 0 || value == 1)) {
+        r->ds.tiles = value;
+        if (value == 1) r->tileOverflowed = false;
+        return 0;
+    }
+    if (key == 20 && value >= 1 && value <= mrt::kTileSlots) {
+        r->tileMaxNew = value;
+        return 0;
+    }
+    if (key == 21 && value >= 0 && value <= 4096) {
+        r->tilePoolTarget = value;
+        return 0;
+    }
+    if (key == 22 && value >= 1 && value <= 64) {
+        r->tileRefill = value;
+        return 0;
+    }
+    if (key == 23 && value >= 1 && value <= 8) {
+        r->tileGrowth = value;
         return 0;
     }
     if (key == 6 && value >= 0 && value <= 100) {
@@ -1447,6 +1546,11 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 11: *value = r->shadeGridPerCU; return 0;
         case 16: *value = r->ds.packet; return 0;
         case 17: *value = r->ds.fuseShade; return 0;
+        case 19: *value = r->ds.tiles; return 0;
+        case 20: *value = r->tileMaxNew; return 0;
+        case 21: *value = r->tilePoolTarget; return 0;
+        case 22: *value = r->tileRefill; return 0;
+        case 23: *value = r->tileGrowth; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

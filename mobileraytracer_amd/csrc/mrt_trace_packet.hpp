@@ -77,20 +77,31 @@ struct NoPost {
 struct NoRays {
     __device__ __forceinline__ void operator()(int, float4*, float4*) const {}
 };
-template <bool kCount, int kCull, class Stack, class Post = NoPost, class Rays = NoRays>
-__device__ __forceinline__ void tracePacket(const DScene& s, const float4* __restrict__ rOs,
-                                            const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                            Stack& st, TravCount* cnt, int* waveStack, Post post = Post(),
-                                            Rays rays = Rays()) {
+// next(): the first ray index of the wave's next packet (wave-uniform); >= count ends the walk
+struct PacketFetch {  // the level queue: 64 rays per atomic
+    int* fetch;
+    __device__ __forceinline__ int next() const {
+        int base = 0;
+        if ((threadIdx.x & 63u) == 0) base = atomicAdd(fetch, 64);
+        return __shfl(base, 0, 64);
+    }
+};
+struct OnePacket {  // one packet: rays [0, count) (the tile kernel's camera rays)
+    int done = 0;
+    __device__ __forceinline__ int next() { return done++ == 0 ? 0 : 64; }
+};
+template <bool kCount, int kCull, class Stack, class Post = NoPost, class Rays = NoRays, class Fetch = PacketFetch>
+__device__ __forceinline__ void tracePacketF(const DScene& s, const float4* __restrict__ rOs,
+                                             const float4* __restrict__ rDs, float4* out, int count, Fetch fetch,
+                                             Stack& st, TravCount* cnt, int* waveStack, Post post = Post(),
+                                             Rays rays = Rays()) {
     static_assert(kCull == kCullNone || kCull == kCullExact, "packet walk: cull modes 0 and 3");
     ConstU32* const qnf = (ConstU32*)(s.triQNodesF);  // NOLINT: address-space casts
     ConstU32* const tg = (ConstU32*)(s.triGeom);      // NOLINT
     ConstU32* const lb = (ConstU32*)(s.leafBoxes);    // NOLINT
     const int lane = static_cast<int>(threadIdx.x & 63u);
     while (true) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(fetch, 64);
-        base = uniformInt(__shfl(base, 0, 64));
+        const int base = uniformInt(fetch.next());
         if (base >= count) break;
         const int i = base + lane;
         const bool valid = i < count;
@@ -274,6 +285,14 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
         }
         post(i, valid, o4, d4, hit);
     }
+}
+
+template <bool kCount, int kCull, class Stack, class Post = NoPost, class Rays = NoRays>
+__device__ __forceinline__ void tracePacket(const DScene& s, const float4* __restrict__ rOs,
+                                            const float4* __restrict__ rDs, float4* out, int count, int* fetch,
+                                            Stack& st, TravCount* cnt, int* waveStack, Post post = Post(),
+                                            Rays rays = Rays()) {
+    tracePacketF<kCount, kCull>(s, rOs, rDs, out, count, PacketFetch{fetch}, st, cnt, waveStack, post, rays);
 }
 
 }  // namespace mrt
