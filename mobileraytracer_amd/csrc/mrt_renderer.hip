@@ -150,6 +150,7 @@ struct mrt_renderer {
     bool walkSkipped = false;            // the last pass skipped that walk
     bool fusedL1 = false;                // the last pass ran level 1 as k_trace_packet_shade
     bool tilePass = false;               // the last pass ran the tile kernel (k_tiles)
+    bool deepFused[mrt::kMaxLevels] = {};  // the last pass ran level l as k_trace_shade
     bool tileOverflowed = false;         // a tile pass overflowed its per-tile queues: level kernels from then on
     int deepWait = 1;                    // tuning key 25: k_trace_shade(l) waits for shadow(l - 2)
     int tileGrowth = 2;                  // tile queue capacity per level: growth x 64 rays (tuning key 23)
@@ -654,6 +655,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     // The tile kernel (k_tiles: every wave renders whole tiles through their ray trees, no grid-wide
     // barrier per level) where it applies: the whole pass in one launch.
     r->tilePass = false;
+    std::fill(std::begin(r->deepFused), std::end(r->deepFused), false);
     if (skipLastShade && !r->tileOverflowed && canTile(shader, r->ds, sa, spp) && !r->stopFlag.load()) {
         r->tilePass = true;
         r->fusedL1 = false;
@@ -777,6 +779,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             // (k_trace_shade writes level l's shadow queue, which shadow(l - 2) no longer reads, and
             // shares no spill stack with the shadow walk: the wait below comes first)
             if (fusedDeep && r->deepWait != 0 && sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
+            r->deepFused[l] = fusedDeep;
             if (fusedDeep) {
                 launchTraceShade(shader, r->ds, pp.levels[l], pp.dLevels, pp.counters, l, sa, pp.gstack, r->gdepth,
                                  r->traceThreads, st, skipLastShade && l + 1 == nLevels);
@@ -889,6 +892,9 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
             if (lvl == 0 && r->fusedL1) {  // one launch: ray generation, walk and shading of level 1
                 fs->fusedMs += ta;
                 fs->fusedLaunches += 1;
+            } else if (r->deepFused[lvl + 1]) {  // one launch: the level's walk and shading
+                fs->deepMs += ta;
+                fs->deepLaunches += 1;
             } else {
                 fs->traceMs += ta;
                 fs->shadeMs += tc;
@@ -897,7 +903,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
             fs->levelTraceMs[lvl] += ta;
             fs->levelShadowMs[lvl] += tb;
             const bool last = lvl + 1 == static_cast<size_t>(r->nLevels);
-            if (!(r->walkSkipped && last) && !(lvl == 0 && r->fusedL1)) fs->traceLaunches += 1;
+            if (!(r->walkSkipped && last) && !(lvl == 0 && r->fusedL1) && !r->deepFused[lvl + 1]) fs->traceLaunches += 1;
             if (!last) fs->shadowLaunches += 1;  // the last level builds no shadow rays
         }
     }
@@ -960,6 +966,8 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs.shadowLeafRecords += prev.shadowLeafRecords;
                     fs.fusedMs += prev.fusedMs;
                     fs.tileMs += prev.tileMs;
+                    fs.deepMs += prev.deepMs;
+                    fs.deepLaunches += prev.deepLaunches;
                     fs.tileLaunches += prev.tileLaunches;
                     fs.fusedLaunches += prev.fusedLaunches;
                     fs.maxNodeRecordsPerRay = std::max(fs.maxNodeRecordsPerRay, prev.maxNodeRecordsPerRay);
