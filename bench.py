@@ -188,7 +188,7 @@ def kernel_roofline(r, step):
     r.set_tuning(3, 0)  # shadow rays on the render stream: every launch timed alone
     r.set_profiling(timing=True)
     keys = ("traceMs", "shadowMs", "shadeMs", "fusedMs", "traceLaunches", "shadowLaunches", "shadeLaunches",
-            "fusedLaunches", "deepMs", "deepLaunches")
+            "fusedLaunches")
     t = dict.fromkeys(keys, 0)
     frames = 2
     for _ in range(frames):
@@ -204,7 +204,6 @@ def kernel_roofline(r, step):
     nodes, tris, leaves = c["levelNodeRecords"], c["levelTriTests"], c["levelLeafRecords"]
     shaded = c["levelShadedVertices"]
     fused = t["fusedLaunches"] > 0
-    deep = t["deepLaunches"] > 0  # depths 2 .. maxDepth walked and shaded in one launch (k_trace_shade)
     walk_levels = range(1 if fused else 0, md)  # k_trace: depths 2 (1 unfused) .. maxDepth
     # k_trace: per ray 32 (ray read: origin, direction) + 16 (hit write) + 32 per node record + 36 per
     # triangle test; `fetched`: the bytes the load instructions request - 16 per child
@@ -256,18 +255,9 @@ def kernel_roofline(r, step):
                "shadow_tris": c["shadowTriTests"] / max(1, n_sh),
                "shadow_leaves": c["shadowLeafRecords"] / max(1, n_sh), "shaded_vertices": c["shadedVertices"]}
     lv = lambda rng: [l + 1 for l in rng]  # noqa: E731
-    out = {"k_shadow": entry(shadow_b, t["shadowMs"], t["shadowLaunches"], shadow_f)}
-    if deep:
-        # k_trace_shade: the walk's gathers with no hit record written (32 B ray read per ray), then the
-        # shading of the finished rays without k_shade's ray / hit reads (the key and tree code, 8 B)
-        deep_b = sum(32.0 * rays[l] + 32.0 * nodes[l] + 36.0 * tris[l] - 68.0 * rays[l] + 8.0 * rays[l] + shade_bytes(l)
-                     for l in walk_levels)
-        deep_f = sum(32.0 * rays[l] + 16.0 * nodes[l] + 48.0 * leaves[l] + 36.0 * tris[l] - 68.0 * rays[l] + 8.0 * rays[l]
-                     + shade_bytes(l) for l in walk_levels)
-        out["k_trace_shade"] = entry(deep_b, t["deepMs"], t["deepLaunches"], deep_f, lv(walk_levels))
-    else:
-        out["k_trace"] = entry(trace_b, t["traceMs"], t["traceLaunches"], trace_f, lv(walk_levels))
-        out["k_shade"] = entry(shade_b, t["shadeMs"], t["shadeLaunches"] - t["fusedLaunches"], None, lv(shade_levels))
+    out = {"k_trace": entry(trace_b, t["traceMs"], t["traceLaunches"], trace_f, lv(walk_levels)),
+           "k_shadow": entry(shadow_b, t["shadowMs"], t["shadowLaunches"], shadow_f),
+           "k_shade": entry(shade_b, t["shadeMs"], t["shadeLaunches"] - t["fusedLaunches"], None, lv(shade_levels))}
     if fused:
         out["k_trace_packet_shade"] = entry(fused_b, t["fusedMs"], t["fusedLaunches"], fused_f, [1])
     return out, per_ray
@@ -414,8 +404,7 @@ def main():
         tb = traffic.get(name)
         e["traffic"] = tb
         e["hbm_frac"] = (tb / (e["avg_launch_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS) if tb and e["avg_launch_ms"] > 0 else None
-    dom_name = "k_trace_shade" if "k_trace_shade" in kernels else "k_trace"
-    dom = kernels[dom_name]
+    dom = kernels["k_trace"]
     out = {
         "metric": BASELINE_METRIC,
         "value": walked / elapsed / 1e6,
@@ -461,8 +450,7 @@ def main():
             # cache-resident scene (PMC: texture-data unit busy ~92 %, bytes beyond L2 ~11 % of the
             # algorithmic bytes; profiles/), not by HBM
             "bound": "vmem-gather",
-            "kernel": ("k_trace_shade (closest hit + shading" if dom_name == "k_trace_shade" else "k_trace (closest hit") +
-                      ", per-lane walk of depths %s)" % dom.get("depths"),
+            "kernel": "k_trace (closest hit, per-lane walk of depths %s)" % dom.get("depths"),
             "achieved": dom["achieved"],
             "peak": PEAK_VMEM_GBS,
             "unit": "GB/s",

@@ -127,9 +127,6 @@ typedef struct mrt_frame_stats {
     uint64_t shadowOccluded;       /* counting pass only: occluded shadow rays */
     double tileMs;                 /* profiling: duration of the tile kernel launches (k_tiles) */
     int64_t tileLaunches;          /* tile kernel launches of the frame (0: the level kernels ran) */
-    double deepMs;                 /* profiling: summed duration of the fused walk + shading launches of
-                                      levels 2 .. maxDepth (k_trace_shade; not in traceMs / shadeMs) */
-    int64_t deepLaunches;          /* k_trace_shade launches of the frame (counted in shadeLaunches too) */
 } mrt_frame_stats;
 
 /* A named byte buffer (a map_Kd texture file handed over by the Android front end). */

@@ -748,63 +748,6 @@ __global__ __launch_bounds__(kWalkThreads, MRT_FUSED_WAVES) void k_trace_packet_
                               PacketRays{&ra});
 }
 
-// Levels 2 .. maxDepth fused: the per-lane walk shades its finished rays where it would write their
-// hits (the lanes the walk completes together, >= DScene::refill of them or the queue's last),
-// allocating their children and shadow rays with one 64-bit atomic per wave and batch
-// (waveAllocPair) - k_shade's work without its launch, its grid-wide barrier and the hit records'
-// write and read.  Same vertex records, shadow and child rays as k_shade (queue order differs, as
-// it does between launches).
-template <int kShader>
-struct ShadeQueue : LevelQueue {
-    static constexpr bool kShades = true;
-    const DScene* s;
-    const Level* levels;  // the pass's level table in device memory: read (scalar loads) per shading batch,
-    int* counters;        // so the walk does not hold two Level records in registers
-    int level;
-    const ShadeArgs* a;
-    bool dead;
-    __device__ __forceinline__ ShadeQueue(const DScene* s_, const Level* levels_, int* counters_, int level_,
-                                          const ShadeArgs* a_, bool dead_, const Level& lv, int count_, int* fetch_)
-        : LevelQueue(lv.rO, lv.rD, lv.hit, count_, fetch_), s(s_), levels(levels_), counters(counters_), level(level_),
-          a(a_), dead(dead_) {}
-    __device__ __forceinline__ void shade(int i, bool valid, v3 o, v3 d, uint32_t src, float4 h) const {
-        const Level& lv = levels[level];  // (references: fields loaded where used)
-        const Level& nx = levels[level + 1];
-        ShadeState v{};
-        if (valid) {
-            const float4 o4 = make_float4(o.x, o.y, o.z, lv.rO[i].w);  // w: the path key
-            const float4 d4 = make_float4(d.x, d.y, d.z, bitsf(src));
-            v = shadePrepare<kShader>(*s, o4, d4, h, lv.tree[i], level, *a, make_float4(0.0F, 0.0F, 0.0F, -1.0F), s->mats,
-                                      s->lights);
-            if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
-        }
-        int childBase, shadowBase;
-        waveAllocPair(reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1)), valid ? v.nChild : 0,
-                      valid ? v.nShadow : 0, &childBase, &shadowBase);
-        if (valid) shadeEmit(*s, v, i, lv, nx, shadowBase, childBase, counters, *a, dead, s->lights);
-    }
-};
-
-#ifndef MRT_TRACE_SHADE_WAVES
-#define MRT_TRACE_SHADE_WAVES 6
-#endif
-template <int kShader, int kCull>
-__global__ __launch_bounds__(kWalkThreads, MRT_TRACE_SHADE_WAVES) void k_trace_shade(DScene s, Level lv, const Level* levels,
-                                                                                     int* counters, int level,
-                                                                                     ShadeArgs a, int deadNext,
-                                                                                     int2* gstack, int gdepth) {
-    __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
-    __shared__ QNode4 ldsTop[kWalkTop];
-    __shared__ int tailBest[kWalkThreads];
-    auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
-    const int count = min(counters[cntRays(level)], lv.cap);
-    int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
-    stageTop<kWalkThreads>(s, ldsTop);
-    ShadeQueue<kShader> q(&s, levels, counters, level, &a, deadNext != 0, lv, count, fetch);
-    TravCount cnt{0u, 0u};
-    traceWhileWhileQ<false, false, kCull>(s, q, st, &cnt, ldsTop, tailBest);
-}
-
 // Single-level shaders: the camera ray's shade() spawns no rays, so the result is final here.
 //   DepthMap (DepthMap.cpp:13-18), DiffuseMaterial (DiffuseMaterial.cpp:12-28),
 //   NoShadows (NoShadows.cpp:13-44: direct light without shadow rays + ambient).
@@ -1680,31 +1623,6 @@ void launchTiles(int shader, const DScene& s, const TileArgs& a, int grid, int2*
         else
             hipLaunchKernelGGL((k_tiles<kShaderWhitted, kCullNone>), dim3(grid), dim3(kWalkThreads), 0, st, s, a, gstack, gdepth);
     }
-}
-
-bool canFuseDeep(int shader, const DScene& s, const ShadeArgs& a) {
-    return s.fuseDeep != 0 && s.accel == kAccBVH && s.variant == 1 && (s.cull == kCullNone || s.cull == kCullExact) &&
-           (shader == kShaderWhitted || shader == kShaderPathTracer) && s.textured == 0 && a.stats == nullptr &&
-           s.leanShade != 0;
-}
-
-void launchTraceShade(int shader, const DScene& s, const Level& lv, const Level* levels, int* counters, int level,
-                      const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext) {
-    const int dead = deadNext ? 1 : 0;
-#define MRT_LAUNCH_TS(SH, C, SLOT)                                                                              \
-    do {                                                                                                       \
-        const int g = std::max(1, persistentGrid(k_trace_shade<SH, C>, SLOT, maxThreads));                    \
-        hipLaunchKernelGGL((k_trace_shade<SH, C>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, levels, counters, level, a, \
-                           dead, gstack, gdepth);                                                              \
-    } while (0)
-    if (shader == kShaderPathTracer) {
-        if (s.cull == kCullExact) MRT_LAUNCH_TS(kShaderPathTracer, kCullExact, 18);
-        else MRT_LAUNCH_TS(kShaderPathTracer, kCullNone, 19);
-    } else {
-        if (s.cull == kCullExact) MRT_LAUNCH_TS(kShaderWhitted, kCullExact, 20);
-        else MRT_LAUNCH_TS(kShaderWhitted, kCullNone, 21);
-    }
-#undef MRT_LAUNCH_TS
 }
 
 }  // namespace mrt

@@ -168,13 +168,6 @@ bool canFuseLevel1(int shader, const DScene& s, const ShadeArgs& a);
 void launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                            const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext,
                            const RaygenArgs& ra);
-// Levels 2 .. maxDepth: the per-lane closest-hit walk shading its finished rays (k_trace_shade) where
-// it applies (canFuseDeep: DScene::fuseDeep, Whitted / PathTracer, untextured, lean shading, no
-// counting); it replaces launchTrace + launchShade of the level.
-bool canFuseDeep(int shader, const DScene& s, const ShadeArgs& a);
-// levels: the pass's Level table (kMaxLevels entries) in device memory
-void launchTraceShade(int shader, const DScene& s, const Level& lv, const Level* levels, int* counters, int level,
-                      const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext);
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                  const ShadeArgs& a, int grid, hipStream_t st, bool deadNext = false);
 // deadChildren: level + 1 is the depth-capped last level, whose results are all zero; its

@@ -122,7 +122,6 @@ struct mrt_renderer {
     // The wavefront queues of one chunk of pixel slots, and the two streams it runs on.
     struct Pipe {
         mrt::Level levels[mrt::kMaxLevels]{};
-        mrt::Level* dLevels = nullptr;  // a device copy of levels (k_trace_shade reads it per shading batch)
         int* counters = nullptr;
         unsigned long long* stats = nullptr;
         int2* gstack = nullptr;        // spill stacks of the closest-hit kernel ...
@@ -150,9 +149,7 @@ struct mrt_renderer {
     bool walkSkipped = false;            // the last pass skipped that walk
     bool fusedL1 = false;                // the last pass ran level 1 as k_trace_packet_shade
     bool tilePass = false;               // the last pass ran the tile kernel (k_tiles)
-    bool deepFused[mrt::kMaxLevels] = {};  // the last pass ran level l as k_trace_shade
     bool tileOverflowed = false;         // a tile pass overflowed its per-tile queues: level kernels from then on
-    int deepWait = 1;                    // tuning key 25: k_trace_shade(l) waits for shadow(l - 2)
     int tileGrowth = 2;                  // tile queue capacity per level: growth x 64 rays (tuning key 23)
     int tileMaxNew = 2;                  // tiles a wave claims per round at most (tuning key 20)
     int tilePoolTarget = 256;            // ... while its next walk pool has fewer rays (tuning key 21)
@@ -545,8 +542,6 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
         lv.kd = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
         lv.last = tex ? r->queueMem.alloc<float4>(cap) : nullptr;
     }
-    pp.dLevels = r->queueMem.alloc<Level>(kMaxLevels);
-    MRT_HIP(hipMemcpy(pp.dLevels, pp.levels, sizeof(pp.levels), hipMemcpyHostToDevice));
     pp.counters = r->queueMem.alloc<int>(kNumCounters);
     pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats + kWaveLogEntries);
     pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
@@ -655,7 +650,6 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     // The tile kernel (k_tiles: every wave renders whole tiles through their ray trees, no grid-wide
     // barrier per level) where it applies: the whole pass in one launch.
     r->tilePass = false;
-    std::fill(std::begin(r->deepFused), std::end(r->deepFused), false);
     if (skipLastShade && !r->tileOverflowed && canTile(shader, r->ds, sa, spp) && !r->stopFlag.load()) {
         r->tilePass = true;
         r->fusedL1 = false;
@@ -773,24 +767,12 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                                       r->gdepth, r->traceThreads, st, skipLastShade && l + 1 == nLevels, ra);
                 ++r->shadeLaunches;
             }
-            // levels 2 .. maxDepth: the walk shades its own hits where that applies (k_trace_shade)
-            const bool fusedDeep = !fused && l >= 2 && !(skipLast && l == nLevels) && !(skipLastShade && l == nLevels) &&
-                                   canFuseDeep(shader, r->ds, sa);
-            // (k_trace_shade writes level l's shadow queue, which shadow(l - 2) no longer reads, and
-            // shares no spill stack with the shadow walk: the wait below comes first)
-            if (fusedDeep && r->deepWait != 0 && sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
-            r->deepFused[l] = fusedDeep;
-            if (fusedDeep) {
-                launchTraceShade(shader, r->ds, pp.levels[l], pp.dLevels, pp.counters, l, sa, pp.gstack, r->gdepth,
-                                 r->traceThreads, st, skipLastShade && l + 1 == nLevels);
-                ++r->shadeLaunches;
-            } else if (!fused && !(skipLast && l == nLevels)) {
+            if (!fused && !(skipLast && l == nLevels))
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting,
                             r->traceThreads, st);
-            }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-            if (!fusedDeep && sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
-            if (!fused && !fusedDeep && !(skipLastShade && l == nLevels)) {
+            if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
+            if (!fused && !(skipLastShade && l == nLevels)) {
                 launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa,
                             shadePerCU > 0 ? r->cus * shadePerCU : r->workGrid, st,
                             skipLastShade && l + 1 == nLevels);
@@ -892,9 +874,6 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
             if (lvl == 0 && r->fusedL1) {  // one launch: ray generation, walk and shading of level 1
                 fs->fusedMs += ta;
                 fs->fusedLaunches += 1;
-            } else if (r->deepFused[lvl + 1]) {  // one launch: the level's walk and shading
-                fs->deepMs += ta;
-                fs->deepLaunches += 1;
             } else {
                 fs->traceMs += ta;
                 fs->shadeMs += tc;
@@ -903,7 +882,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
             fs->levelTraceMs[lvl] += ta;
             fs->levelShadowMs[lvl] += tb;
             const bool last = lvl + 1 == static_cast<size_t>(r->nLevels);
-            if (!(r->walkSkipped && last) && !(lvl == 0 && r->fusedL1) && !r->deepFused[lvl + 1]) fs->traceLaunches += 1;
+            if (!(r->walkSkipped && last) && !(lvl == 0 && r->fusedL1)) fs->traceLaunches += 1;
             if (!last) fs->shadowLaunches += 1;  // the last level builds no shadow rays
         }
     }
@@ -966,8 +945,6 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs.shadowLeafRecords += prev.shadowLeafRecords;
                     fs.fusedMs += prev.fusedMs;
                     fs.tileMs += prev.tileMs;
-                    fs.deepMs += prev.deepMs;
-                    fs.deepLaunches += prev.deepLaunches;
                     fs.tileLaunches += prev.tileLaunches;
                     fs.fusedLaunches += prev.fusedLaunches;
                     fs.maxNodeRecordsPerRay = std::max(fs.maxNodeRecordsPerRay, prev.maxNodeRecordsPerRay);
@@ -1379,14 +1356,6 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.fuseShade = value;
         return 0;
     }
-    if (key == 25 && (value == 0 || value == 1)) {
-        r->deepWait = value;
-        return 0;
-    }
-    if (key == 24 && (value == 0 || value == 1)) {
-        r->ds.fuseDeep = value;
-        return 0;
-    }
     if (key == 19 && (value == 0 || value == 1)) {
         r->ds.tiles = value;
         if (value == 1) r->tileOverflowed = false;
@@ -1578,7 +1547,6 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 16: *value = r->ds.packet; return 0;
         case 17: *value = r->ds.fuseShade; return 0;
         case 19: *value = r->ds.tiles; return 0;
-        case 24: *value = r->ds.fuseDeep; return 0;
         case 20: *value = r->tileMaxNew; return 0;
         case 21: *value = r->tilePoolTarget; return 0;
         case 22: *value = r->tileRefill; return 0;

@@ -58,6 +58,10 @@ constexpr int kInnerExitAny = MRT_INNER_EXIT_ANY;
 #endif
 constexpr int kLeafExitClosest = MRT_LEAF_EXIT;
 constexpr int kLeafExitAny = MRT_LEAF_EXIT_ANY;
+// ... both scaled by the wave's lanes holding a ray (traceWhileWhileQ)
+#ifndef MRT_SCALED_EXIT
+#define MRT_SCALED_EXIT 1
+#endif
 
 // Buffer loads for the scene gathers: exact widths (the 8-byte child-reference load is not
 // widened to 16 bytes, which costs texture-data cycles), a 32-bit VGPR offset instead of a
@@ -722,10 +726,24 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
                 if (lane == dOwner) ++pend;
             }
         }
-        if (__ballot(rayIdx != -1) == 0) {
+        const uint64_t activeMask = __ballot(rayIdx != -1);
+        if (activeMask == 0) {
             if (__ballot(!exhausted) == 0) break;
             continue;
         }
+        // The phases' early exits scale with the lanes that hold a ray: in a queue's tail, with a few
+        // rays left in the wave, a fixed threshold would end each phase after one step and pay the
+        // outer loop's refill / donation bookkeeping per node visit (scheduling only: every lane visits
+        // the same nodes and tests the same leaves in the same order).
+        constexpr int kExit = kAny ? kInnerExitAny : kInnerExitClosest;
+        constexpr int kLeafExit = kAny ? kLeafExitAny : kLeafExitClosest;
+#if MRT_SCALED_EXIT
+        const int nActive = __popcll(activeMask);
+        const int innerExit = max(1, (kExit * nActive + 63) >> 6);
+        const int leafExit = max(1, (kLeafExit * nActive + 63) >> 6);
+#else
+        const int innerExit = kExit, leafExit = kLeafExit;
+#endif
         // ---- inner nodes until every active lane holds a postponed leaf ----
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
             const float curLim = cullLimit<kInner>(fminf(bt, shT));
@@ -740,8 +758,7 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
             }
             // leave for the leaf phase once fewer than kInnerExit lanes are still looking for a
             // leaf (the rest wait one phase; waiting for the very last costs more)
-            constexpr int kExit = kAny ? kInnerExitAny : kInnerExitClosest;
-            if (__popcll(__ballot(leaf >= 0 && static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone))) < kExit)
+            if (__popcll(__ballot(leaf >= 0 && static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone))) < innerExit)
                 break;
         }
         // ---- leaves ----
@@ -821,8 +838,7 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
             }
             // back to the inner phase once fewer than kLeafExit lanes hold a leaf: the others keep
             // theirs (tested first when the leaf phase resumes, so each lane's order is unchanged)
-            constexpr int kLeafExit = kAny ? kLeafExitAny : kLeafExitClosest;
-            if (__popcll(__ballot(leaf < 0)) < kLeafExit) break;
+            if (__popcll(__ballot(leaf < 0)) < leafExit) break;
         }
     }
 }

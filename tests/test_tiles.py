@@ -90,16 +90,3 @@ def test_tiles_queue_overflow_falls_back():
     a, ra, _ = render(cfg, 0)
     b, rb, sb = render(cfg, 1, keys=((23, 1),))
     assert np.array_equal(a, b) and ra == rb
-
-
-@pytest.mark.parametrize("name", ["conference_pt_spp3", "water_whitted", "water_pt_spp4", "flat_pt_spp4",
-                                  "cornell_pt_spp2", "conference_whitted_spp1"])
-def test_deep_levels_fused_shading_is_invariant(name):
-    """Levels 2 .. maxDepth with the walk shading its own finished rays (k_trace_shade, tuning key
-    24) give the separate k_trace + k_shade launches' bitmaps and ray counts, with and without the
-    wait for the shadow walk two levels back (key 25)."""
-    cfg = make_cfg(**CASES[name])
-    outs = [render(cfg, 0, keys=keys) for keys in (((24, 0),), ((24, 1),), ((24, 1), (25, 0)))]
-    for bm, rays, st in outs[1:]:
-        assert np.array_equal(bm, outs[0][0]), int((bm != outs[0][0]).sum())
-        assert rays == outs[0][1] and st["levelRays"] == outs[0][2]["levelRays"]

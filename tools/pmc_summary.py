@@ -16,7 +16,6 @@ from collections import defaultdict
 # roofline names them: level 1 fused (k_trace_packet_shade), the per-lane closest-hit walk of the
 # deeper levels, the shadow walk and the lean PathTracer shading kernel
 PRODUCT = {"k_trace": (r"k_trace<false, 1, 3>",), "k_trace_packet_shade": (r"k_trace_packet_shade<2, 3>",),
-           "k_trace_shade": (r"k_trace_shade<2, 3>",),
            "k_shadow": (r"k_shadow<false, 1, 3>",), "k_shade": (r"k_shade<2, false>",)}
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import kernel_source_stamp, workload_key  # noqa: E402
