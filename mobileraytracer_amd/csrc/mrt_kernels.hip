@@ -1130,7 +1130,6 @@ __device__ __forceinline__ void waveSync() { __builtin_amdgcn_fence(__ATOMIC_SEQ
 // cursor (no atomics: only this wave takes from it).
 template <bool kAny>
 struct TileQueue {
-    static constexpr bool kShades = false;
     const TileArgs* a;
     char* arena;
     const TileWave* w;
@@ -1163,7 +1162,6 @@ struct TileQueue {
         const int e = entry(v);
         level(e).sC[v - w->poolPre[e]].w = f;
     }
-    __device__ __forceinline__ void shade(int, bool, v3, v3, uint32_t, float4) const {}
     __device__ __forceinline__ bool drained() const { return cursor >= count; }
     __device__ __forceinline__ int take(uint64_t pending) {
         const int idx = cursor + lanesBelowIn(pending);

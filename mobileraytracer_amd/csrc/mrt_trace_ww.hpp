@@ -419,15 +419,12 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
 //   hit(i, h)       the closest hit (t, u, v, primitive code); occ(i, f): the occluded flag;
 //   take(pending)   called by every lane of the wave (wave-uniform control flow) with the mask of
 //                   lanes wanting a ray: this lane's ray index, or -1 (none left for it);
-//   drained()       wave-uniform: the queue has no ray left for this wave;
-//   kShades         the finished closest hits go to shade(i, finished, o, d, source primitive, hit),
-//                   called by every lane of the wave (wave-level slot allocation), not to hit(i, h).
+//   drained()       wave-uniform: the queue has no ray left for this wave.
 // LevelQueue: a level's queue arrays, rays [0, count), fetched through kWalkShards cursors
 // (kFetchStride ints apart), one per XCD group of workgroups (blockIdx % 8), each over a contiguous
 // eighth of the queue; a drained eighth is left for the next (speed only: any placement gives the
 // same results).
 struct LevelQueue {
-    static constexpr bool kShades = false;  // true: shade(i, ...) takes a finished closest hit instead of hit(i, h)
     const float4* __restrict__ rO;
     const float4* __restrict__ rD;
     float4* out;
@@ -441,7 +438,6 @@ struct LevelQueue {
     __device__ __forceinline__ float4 d(int i) const { return rD[i]; }
     __device__ __forceinline__ void hit(int i, float4 h) const { out[i] = h; }
     __device__ __forceinline__ void occ(int i, float f) const { out[i].w = f; }
-    __device__ __forceinline__ void shade(int, bool, v3, v3, uint32_t, float4) const {}
     __device__ __forceinline__ bool drained() const { return segsLeft == 0; }
     __device__ __forceinline__ int take(uint64_t pending) {
         const int lane = static_cast<int>(threadIdx.x & 63u);
@@ -561,9 +557,7 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
             const int nReady = __popcll(__ballot(doneLane || (rayIdx == -1 && !exhausted)));
             runDone = nReady >= s.refill || __ballot(rayIdx >= 0 && !doneLane) == 0 || __ballot(exhausted) != 0;
         }
-        const bool fin = doneLane && runDone;
-        float4 hitv = make_float4(0.0F, 0.0F, 0.0F, 0.0F);
-        if (fin) {
+        if (doneLane && runDone) {
             if (kCount) cnt->rayMax = max(cnt->rayMax, cnt->nodes - cnt->rayStart);
             if (kAny) {
                 q.occ(rayIdx, occ ? 1.0F : 0.0F);
@@ -589,14 +583,9 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
                     const float4* g = kind == kTriangle ? s.triGeom + 3 * primIndex(bcode) : s.lights + 4 * primIndex(bcode);
                     (void)triTest(g[0], g[1], g[2], o, d, &t, &u, &v);
                 }
-                hitv = make_float4(bt, u, v, bitsf(bcode));
-                if constexpr (!Queue::kShades) q.hit(rayIdx, hitv);
+                q.hit(rayIdx, make_float4(bt, u, v, bitsf(bcode)));
             }
-            if (kAny || !Queue::kShades) rayIdx = -1;
-        }
-        if constexpr (!kAny && Queue::kShades) {  // the finished lanes' hits shaded together, in the walk
-            if (__ballot(fin) != 0) q.shade(rayIdx, fin, o, d, src, hitv);
-            if (fin) rayIdx = -1;
+            rayIdx = -1;
         }
         // ---- refill lanes without a ray (one atomic per wave and cursor) ----
         bool need = rayIdx == -1 && !exhausted;
