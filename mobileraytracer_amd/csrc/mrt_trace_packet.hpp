@@ -78,14 +78,45 @@ struct NoRays {
     __device__ __forceinline__ void operator()(int, float4*, float4*) const {}
 };
 // next(): the first ray index of the wave's next packet (wave-uniform); >= count ends the walk
-struct PacketFetch {  // the level queue: 64 rays per atomic
+#ifndef MRT_PACKET_SEGMENTS
+#define MRT_PACKET_SEGMENTS 1
+#endif
+#if MRT_PACKET_SEGMENTS
+// the level queue's packets in kWalkShards contiguous ranges, one cursor each (kFetchStride ints
+// apart), a workgroup starting on its XCD group's range (blockIdx % 8) and trying MRT_WALK_SEGMENTS
+// of them: an XCD's L2 sees one eighth of the image, and the exhausted-queue polls spread over 8
+// addresses instead of one
+struct PacketFetch {
     int* fetch;
+    int count;
+    int seg = static_cast<int>(blockIdx.x % kWalkShards);
+    int segsLeft = MRT_WALK_SEGMENTS;
+    __device__ __forceinline__ int next() {
+        const int packets = (count + 63) >> 6;
+        while (segsLeft > 0) {
+            const int first = static_cast<int>((static_cast<long long>(packets) * seg) / kWalkShards);
+            const int last = static_cast<int>((static_cast<long long>(packets) * (seg + 1)) / kWalkShards);
+            int p = 0;
+            if ((threadIdx.x & 63u) == 0) p = atomicAdd(fetch + seg * kFetchStride, 1);
+            p = __shfl(p, 0, 64);
+            if (first + p < last) return (first + p) << 6;
+            seg = (seg + 1) % kWalkShards;
+            --segsLeft;
+        }
+        return count;
+    }
+};
+#else
+struct PacketFetch {  // the level queue: 64 rays per atomic on one cursor
+    int* fetch;
+    int count;
     __device__ __forceinline__ int next() const {
         int base = 0;
         if ((threadIdx.x & 63u) == 0) base = atomicAdd(fetch, 64);
         return __shfl(base, 0, 64);
     }
 };
+#endif
 struct OnePacket {  // one packet: rays [0, count) (the tile kernel's camera rays)
     int done = 0;
     __device__ __forceinline__ int next() { return done++ == 0 ? 0 : 64; }
@@ -292,7 +323,7 @@ __device__ __forceinline__ void tracePacket(const DScene& s, const float4* __res
                                             const float4* __restrict__ rDs, float4* out, int count, int* fetch,
                                             Stack& st, TravCount* cnt, int* waveStack, Post post = Post(),
                                             Rays rays = Rays()) {
-    tracePacketF<kCount, kCull>(s, rOs, rDs, out, count, PacketFetch{fetch}, st, cnt, waveStack, post, rays);
+    tracePacketF<kCount, kCull>(s, rOs, rDs, out, count, PacketFetch{fetch, count}, st, cnt, waveStack, post, rays);
 }
 
 }  // namespace mrt

@@ -33,6 +33,15 @@ namespace mrt {
 constexpr int kRefDone = 0x7FFFFFFF;  // sentinel: no node (never a valid inner index)
 constexpr int kWalkRefill = 32;       // idle lanes before a wave fetches new rays (DScene::refill at upload; frames set it by paths per lane)
 constexpr int kWalkShards = 8;        // work cursors per level (one per XCD group of workgroups)
+// Cursors a wave tries (its own XCD group's first) before it stops fetching.  When a level's queue
+// runs dry every resident wave polls the cursors it has left with an atomic each, and same-address
+// atomics serialise at the memory side: a walk launch with no rays to walk took 100 us with 8
+// (every wave polling every cursor), 19 us with 1 (profiles/r04_latency_probe.txt).  4 keeps most
+// of the load balancing between the XCD groups: C4 15.40 -> 15.22 ms, N = 8 shard 2.88 -> 2.85 ms
+// (2: 15.28 / 2.88, 1: 15.96 / 2.91).
+#ifndef MRT_WALK_SEGMENTS
+#define MRT_WALK_SEGMENTS 4
+#endif
 constexpr int kWalkStack = kLdsStackMin;  // LDS stack entries per thread (deeper ones spill)
 constexpr int kWalkTop = kTopNodesMax;
 // The while-while walk's inner phase ends when fewer than this many lanes still look for a leaf
@@ -431,7 +440,7 @@ struct LevelQueue {
     int count;
     int* fetch;
     int seg = static_cast<int>(blockIdx.x % kWalkShards);  // wave-uniform cursor state
-    int segsLeft = kWalkShards;
+    int segsLeft = MRT_WALK_SEGMENTS;
     __device__ __forceinline__ LevelQueue(const float4* o_, const float4* d_, float4* out_, int count_, int* fetch_)
         : rO(o_), rD(d_), out(out_), count(count_), fetch(fetch_) {}
     __device__ __forceinline__ float4 o(int i) const { return rO[i]; }

@@ -45,8 +45,10 @@ def main():
                 r.render_frame_device(bm, pk, sh)
             torch.cuda.synchronize()
             res[k].append((time.perf_counter() - t0) / 5 * 1e3)
+    import zlib
     for k in rs:
-        print(f"setting {k}: frame {np.median(res[k]):.3f} ms (min {np.min(res[k]):.3f})", flush=True)
+        crc = zlib.crc32(bufs[k].cpu().numpy().tobytes())
+        print(f"setting {k}: frame {np.median(res[k]):.3f} ms (min {np.min(res[k]):.3f}) crc {crc:08x}", flush=True)
     for k in variants[1:]:
         print(f"setting {k} identical image:", torch.equal(bufs[variants[0]], bufs[k]))
     if os.environ.get("COUNT") == "1":  # one counting frame per setting: walk statistics
