@@ -474,6 +474,8 @@ def main():
             "kernels": kernels,
         },
         "cpu_baseline": None,
+        # the loaded library was built from the sources in this tree (Makefile stamp)
+        "library_build_current": m._native.build_is_current(),
     }
     if world == 1 and not shard_of and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, scene)

@@ -137,6 +137,9 @@ typedef struct mrt_blob {
 } mrt_blob;
 
 const char *mrt_last_error(void);
+/* digest of the sources the library was built from (Makefile: sha256 of the csrc sources and
+ * headers, first 16 hex digits, then any extra compile flags) */
+const char *mrt_build_stamp(void);
 int mrt_create(const mrt_config *cfg, mrt_renderer **out);
 /* mrt_create with the OBJ / MTL / CAM given as text and the textures as named blobs, as the
  * Android front end hands them over (MainActivity.readFile -> JNI readFile, JNI_layer.cpp:994-1063,

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("MOBILERT_LIB") or os.path.join(_HERE, "libmobilert_am
 
 # Symbols the C-ABI exports (include/mobilert_amd.h + mobilert_amd.hpp).
 EXPORTED_SYMBOLS = (
-    "mrt_last_error", "mrt_create", "mrt_destroy", "mrt_render_frame", "mrt_render_frame_device",
+    "mrt_last_error", "mrt_build_stamp", "mrt_create", "mrt_destroy", "mrt_render_frame", "mrt_render_frame_device",
     "mrt_unpack_gathered", "mrt_stop_render", "mrt_get_sample", "mrt_get_total_casted_rays",
     "mrt_get_scene_info", "mrt_set_profiling", "mrt_get_frame_stats", "mrt_primary_hits", "mrt_set_tuning",
     "mrt_get_tuning", "mrt_triangle_bvh", "mrt_walk_tree", "mrt_decode_texture", "mrt_kat_slab", "mrt_kat_triangle",
@@ -103,6 +103,7 @@ def load_library(path=LIB_PATH):
     vp = ctypes.c_void_p
     sig = {
         "mrt_last_error": (ctypes.c_char_p, []),
+        "mrt_build_stamp": (ctypes.c_char_p, []),
         "mrt_create": (ctypes.c_int, [P(MrtConfig), P(vp)]),
         "mrt_destroy": (None, [vp]),
         "mrt_render_frame": (ctypes.c_int, [vp, vp]),
@@ -170,6 +171,26 @@ def lib():
     if _LIB is None:
         _LIB = load_library()
     return _LIB
+
+
+def source_stamp():
+    """The digest the Makefile embeds (mrt_build_stamp) for the csrc sources in this tree."""
+    import hashlib
+    d = os.path.join(_HERE, "csrc")
+    srcs = ["mrt_scene.cpp", "mrt_grid.cpp", "mrt_texture.cpp", "mrt_android.cpp", "mrt_kernels.hip", "mrt_renderer.hip",
+            "mrt_common.hpp", "mrt_device.hpp", "mrt_kernels.hpp", "mrt_trace_ww.hpp", "mrt_trace_packet.hpp",
+            "mrt_scene.hpp", "../../include/mobilert_amd.h", "../../include/mobilert_amd.hpp",
+            "../../include/mobilert_android.h"]
+    h = hashlib.sha256()
+    for f in srcs:
+        with open(os.path.join(d, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_is_current(library=None):
+    """True when the loaded library was built from this tree's sources (no extra flags)."""
+    return (library or lib()).mrt_build_stamp().decode() == source_stamp()
 
 
 def check(rc):

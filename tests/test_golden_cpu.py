@@ -107,6 +107,14 @@ def test_library_exports_every_declared_symbol(native_lib_path):
     assert set(_native.EXPORTED_SYMBOLS) <= exported
 
 
+def test_library_built_from_these_sources(native_lib_path):
+    """The in-tree library (the one the GPU box loads) was built from the sources in the tree."""
+    from mobileraytracer_amd import _native
+    if os.environ.get("MOBILERT_LIB"):
+        pytest.skip("another build was requested")
+    assert _native.build_is_current(_native.load_library(native_lib_path)), "stale libmobilert_amd.so: run make"
+
+
 def test_library_loads_without_gpu(native_lib_path):
     from mobileraytracer_amd import _native
     lib = _native.load_library(native_lib_path)

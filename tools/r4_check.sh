@@ -4,6 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; R=$(pwd)
 OUT=$R/gpurun_out/${1:-r4}; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
+python -c "from mobileraytracer_amd import _native as n; assert n.build_is_current(), 'stale libmobilert_amd.so'" || exit 2
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread ${2:+-k "$2"} > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" $OUT/pytest_gpu.log | tail -15

@@ -5,6 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; R=$(pwd)
 N=${1:-r4final}; OUT=$R/gpurun_out/$N; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
+python -c "from mobileraytracer_amd import _native as n; assert n.build_is_current(), 'stale libmobilert_amd.so'" || exit 2
 bash tools/pmc_run.sh ${N}_pmc > $OUT/pmc.log 2>&1 || { tail $OUT/pmc.log; exit 3; }
 tail -1 $OUT/pmc.log
 cp $R/gpurun_out/${N}_pmc/pmc_traffic.json $R/profiles/r04_pmc_traffic.json
