@@ -161,7 +161,7 @@ class Renderer:
         out["levelShadowRays"] = list(s.levelShadowRays)
         out["levelTraceMs"] = list(s.levelTraceMs)
         out["levelShadowMs"] = list(s.levelShadowMs)
-        for k in ("levelNodeRecords", "levelTriTests", "levelLeafRecords", "levelShadedVertices"):
+        for k in ("levelNodeRecords", "levelTriTests", "levelLeafRecords", "levelShadedVertices", "walkPhases"):
             out[k] = list(getattr(s, k))
         return out
 

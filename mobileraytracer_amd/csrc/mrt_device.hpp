@@ -336,6 +336,9 @@ struct TravCount {
     uint32_t rayMax = 0;
     uint32_t rays = 0;      // rays this lane fetched (the wave log of counting builds)
     uint32_t occluded = 0;  // any hit: occluded rays
+    // walk phases (wave iterations counted once per wave, by its first active lane): inner-node
+    // visits, leaf tests, triangle tests, and the lanes active in them
+    uint32_t innerIters = 0, innerLanes = 0, leafIters = 0, leafLanes = 0, triIters = 0, triLanes = 0;
 };
 
 // Generic BVH walk.  kKind selects the leaf routine.  Returns true on an any-hit.

@@ -182,6 +182,17 @@ __device__ __forceinline__ void reduceCounts(const TravCount& cnt, unsigned long
     }
 }
 
+// counting builds: the walk phases' wave iterations and active lanes (kind 0 closest, 1 any hit)
+__device__ __forceinline__ void reducePhases(const TravCount& cnt, unsigned long long* stats, int kind) {
+    const uint32_t v[6] = {cnt.innerIters, cnt.innerLanes, cnt.leafIters, cnt.leafLanes, cnt.triIters, cnt.triLanes};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        unsigned long long x = v[k];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+        if (laneId() == 0 && x != 0) atomicAdd(stats + kStatPhases + 6 * kind + k, x);
+    }
+}
+
 // counting builds: this wave's entry of the wave log (kWaveLogWaves)
 __device__ __forceinline__ void waveLog(const TravCount& cnt, unsigned long long* stats, int kind, int level,
                                         unsigned long long t0) {
@@ -241,6 +252,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, i
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris, kStatLeaves);
         reduceCounts<kCount>(cnt, stats, kStatLevelNodes + level - 1, kStatLevelTris + level - 1, kStatLevelLeaves + level - 1);
+        reducePhases(cnt, stats, 0);
         atomicMax(stats + kStatMaxNodesRay, static_cast<unsigned long long>(cnt.rayMax));
         waveLog(cnt, stats, 0, level, t0);
     }
@@ -295,6 +307,7 @@ __global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, 
     }
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodesShadow, kStatTrisShadow, kStatLeavesShadow);
+        reducePhases(cnt, stats, 1);
         unsigned long long occl = cnt.occluded;
         for (int off = 32; off > 0; off >>= 1) occl += __shfl_down(occl, off, 64);
         if (laneId() == 0) atomicAdd(stats + kStatOccluded, occl);

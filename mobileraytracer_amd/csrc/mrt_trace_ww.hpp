@@ -93,6 +93,16 @@ __device__ __forceinline__ int4 bload4i(BufRes r, uint32_t off) {
     return __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+// counting builds: one wave iteration of a walk phase and the lanes executing it (added by the
+// first of them)
+__device__ __forceinline__ void phaseCount(uint32_t* iters, uint32_t* lanes) {
+    const uint64_t act = __ballot(true);
+    if (__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(act >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(act), 0u)) == 0) {
+        *iters += 1u;
+        *lanes += static_cast<uint32_t>(__popcll(act));
+    }
+}
+
 // number of set bits of a wave mask below this lane
 __device__ __forceinline__ int lanesBelowIn(uint64_t m) {
     return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
@@ -744,6 +754,7 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
 #endif
         // ---- inner nodes until every active lane holds a postponed leaf ----
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
+            if (kCount) phaseCount(&cnt->innerIters, &cnt->innerLanes);
             const float curLim = cullLimit<kInner>(fminf(bt, shT));
             const bool finite = __ballot(!finiteInv(inv)) == 0;
             const int order = kAny ? s.anyOrder : 0;
@@ -761,6 +772,7 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
         }
         // ---- leaves ----
         while (leaf < 0) {
+            if (kCount) phaseCount(&cnt->leafIters, &cnt->leafLanes);
             const int first = leafFirst(leaf);
             int nprim = leafCount(leaf);
             // the first triangle's loads go out with the leaf box's (one round trip, not two)
@@ -795,6 +807,7 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
             }
             bool hit = false;
             for (int k = 0; k < nprim; ++k) {
+                if (kCount) phaseCount(&cnt->triIters, &cnt->triLanes);
                 const int j = first + k;
                 const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
                 if (code == src) continue;

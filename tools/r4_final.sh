@@ -22,4 +22,6 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); cp $f $OUT/kernel_stats.csv; head -8 $OUT/kernel_stats.csv | cut -c1-150
 cd $R && bash tools/timeline.sh ${N}_tl > $OUT/tl.log 2>&1 || { tail $OUT/tl.log; exit 9; }
 cp $R/gpurun_out/${N}_tl/n1.timeline $R/gpurun_out/${N}_tl/n8.timeline $OUT/ 2>/dev/null
+timeout -k 10 200 python tools/phase_occupancy.py > $OUT/phases.jsonl 2>$OUT/phases.err || { tail $OUT/phases.err; exit 10; }
+cp $OUT/phases.jsonl $R/profiles/r04_walk_phase_occupancy.jsonl; cat $OUT/phases.jsonl | cut -c1-400
 echo final-done
