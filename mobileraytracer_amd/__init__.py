@@ -122,7 +122,8 @@ class Renderer:
         threshold of the walk waves, 10 = lean k_shade instantiation, 11 = k_shade workgroups per CU,
         16 = the camera rays' packet walk (cull modes 0 and 3; refused when the walk tree needs a
         deeper stack than the packet walk's), 17 = level 1 fused (camera rays generated,
-        packet-walked and shaded in one launch).  Results are identical for every value, except
+        packet-walked and shaded in one launch), 19-23 = the tile kernel and its knobs, 27 = the
+        last shadow walk on the render stream.  Results are identical for every value, except
         key 2 = 1 (documented inexact)."""
         _native.check(self._lib.mrt_set_tuning(self._h, key, value))
 

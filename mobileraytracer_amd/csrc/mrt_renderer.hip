@@ -154,6 +154,7 @@ struct mrt_renderer {
     int tileMaxNew = 2;                  // tiles a wave claims per round at most (tuning key 20)
     int tilePoolTarget = 256;            // ... while its next walk pool has fewer rays (tuning key 21)
     int tileRefill = 8;                  // the tile walks' refill threshold (tuning key 22)
+    int lastShadowRender = 1;            // tuning key 27: the last shadow walk on the render stream
     DeviceMem tileMem;                   // the tile kernel's per-wave arenas
     size_t tileArenaBytes = 0;
     char* tileArena = nullptr;
@@ -751,7 +752,14 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // 3.14 ms; N = 1 24 / 32 / 36 -> 16.60 / 16.52 / 16.54 ms)
         r->ds.refill = r->refill > 0 ? r->refill : pathsPerLane < 4.0 ? 48 : 32;
         size_t sync = 0;
-        hipEvent_t shadowDone[kMaxLevels] = {};
+        hipEvent_t shadowDone[kMaxLevels + 1] = {};
+        // The last shadow walk (level nLevels - 1) runs on the render stream, right after its
+        // level's shading and before the resolves that wait for it: no cross-stream hand-off at
+        // either end (each cost 15-30 us on the critical path, profiles/r04_frame_timeline_*).  It
+        // uses the closest-hit spill stacks, idle from then on (the depth-capped last level's walk
+        // is skipped, or follows it on the same stream), so it may overlap the previous level's
+        // shadow walk, still running on the shadow stream.
+        const bool lastOnRender = r->lastShadowRender != 0 && sb != st && nLevels >= 2;
         if (sb != st) {
             const hipEvent_t start = syncEvent(pp, sync++);
             MRT_HIP(hipEventRecord(start, st));
@@ -779,27 +787,31 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 ++r->shadeLaunches;
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-            if (sb != st) {
+            const bool onRender = lastOnRender && l + 1 >= nLevels;  // the last shadow walk, and the level after it
+            const hipStream_t ss = onRender ? st : sb;
+            if (sb != st && !onRender) {
                 const hipEvent_t shaded = syncEvent(pp, sync++);
                 MRT_HIP(hipEventRecord(shaded, st));
                 MRT_HIP(hipStreamWaitEvent(sb, shaded, 0));
             }
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ss));
             // the last level (depth > RayDepthMax) shades nothing: no shadow rays
             if (l < nLevels) {
                 // the last shadow walk runs alone: a large shard gives it the full grid (C4 N = 1:
                 // 13.34 -> 13.29 ms); a small one keeps the narrow grid (N = 8: 2.53 vs 2.55 ms)
                 const bool lastAlone = l + 1 == nLevels && r->shadowGridPct == 0 && pathsPerLane >= 8.0;
-                launchShadow(r->ds, pp.levels[l], pp.counters, l, pp.gstackShadow, r->gdepth, pp.stats, counting,
-                             r->traceThreads, sb, lastAlone ? 100 : shadowPct);
+                launchShadow(r->ds, pp.levels[l], pp.counters, l, onRender ? pp.gstack : pp.gstackShadow, r->gdepth,
+                             pp.stats, counting, r->traceThreads, ss, lastAlone ? 100 : shadowPct);
             }
-            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), sb));
-            if (sb != st) {
+            if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ss));
+            if (sb != st && !onRender) {
                 shadowDone[l] = syncEvent(pp, sync++);
                 MRT_HIP(hipEventRecord(shadowDone[l], sb));
             }
         }
-        if (sb != st) MRT_HIP(hipStreamWaitEvent(st, shadowDone[nLevels], 0));
+        // the resolves wait for every shadow walk on the shadow stream
+        const int lastOnShadowStream = lastOnRender ? nLevels - 2 : nLevels;
+        if (sb != st && lastOnShadowStream >= 1) MRT_HIP(hipStreamWaitEvent(st, shadowDone[lastOnShadowStream], 0));
         for (int l = skipLastShade ? nLevels - 1 : nLevels; l >= 1; --l) {
             launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, st,
                           skipLastShade && l == nLevels - 1);
@@ -1379,6 +1391,10 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->tileGrowth = value;
         return 0;
     }
+    if (key == 27 && (value == 0 || value == 1)) {
+        r->lastShadowRender = value;
+        return 0;
+    }
     if (key == 6 && value >= 0 && value <= 100) {
         r->shadowGridPct = value;
         return 0;
@@ -1553,6 +1569,7 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 21: *value = r->tilePoolTarget; return 0;
         case 22: *value = r->tileRefill; return 0;
         case 23: *value = r->tileGrowth; return 0;
+        case 27: *value = r->lastShadowRender; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

@@ -418,6 +418,38 @@ def test_fused_level1_shading_is_invariant():
             assert all(np.array_equal(a, b) for a, b in zip(outs[0][4], other[4])), cfg
 
 
+def test_last_shadow_walk_on_render_stream_is_invariant(oracle_mod):
+    """The last shadow walk on the render stream with the closest-hit spill stacks (tuning key 27,
+    on by default) instead of the shadow stream: the same bitmap and ray counts with the key off,
+    with the shadow stream off (key 3), with per-launch timing, for two-level frames (the last
+    shadow walk is level 1's), a textured scene (its depth-capped last level is walked after the
+    shadow walk, on the same stream) and Whitted with 2 light samples; and the oracle's bitmap."""
+    import mobileraytracer_amd as m
+    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+             make_cfg(96, 96, shader=2, scene="water", spp=2, max_depth=1),
+             make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3),
+             make_cfg(96, 96, shader=1, scene="water", max_depth=4, spl=2))
+    for cfg in cases:
+        outs = []
+        with m.Renderer(cfg) as r:
+            assert r.get_tuning(27) == 1
+            for key, val, timing in ((27, 1, False), (27, 0, False), (3, 0, False), (27, 1, True)):
+                r.set_tuning(27, 1)
+                r.set_tuning(3, 1)
+                r.set_tuning(key, val)
+                r.set_profiling(timing=timing)
+                bm = np.zeros(cfg.width * cfg.height, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"])))
+                if timing:
+                    assert st["shadowMs"] > 0.0 and st["shadowLaunches"] >= 1, st
+        for other in outs[1:]:
+            assert np.array_equal(outs[0][0], other[0]), cfg
+            assert outs[0][1:] == other[1:], cfg
+        assert np.array_equal(outs[0][0], oracle_render(oracle_mod, cfg)[0]), cfg
+
+
 def test_python_plugin_setters():
     """Renderer.set_camera / set_pixel_sampler (mrt_set_camera, mrt_set_pixel_sampler, the C++
     facade's plugins): re-setting the built-in camera (Scenes.cpp: spheres' orthographic,
