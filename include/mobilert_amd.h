@@ -127,9 +127,11 @@ typedef struct mrt_frame_stats {
     uint64_t shadowOccluded;       /* counting pass only: occluded shadow rays */
     double tileMs;                 /* profiling: duration of the tile kernel launches (k_tiles) */
     int64_t tileLaunches;          /* tile kernel launches of the frame (0: the level kernels ran) */
-    uint64_t walkPhases[12];       /* counting pass only, the persistent walks (closest hit, then any hit):
+    uint64_t walkPhases[16];       /* counting pass only, the persistent walks (closest hit, then any hit):
                                       wave iterations and the lanes active in them of the inner-node phase,
-                                      the leaf phase and the triangle loop: {iters, lanes} x 3 x 2 */
+                                      the leaf phase and the triangle loop: {iters, lanes} x 3 x 2; then per
+                                      walk, summed over inner iterations, the wave's lanes without a ray
+                                      and with a finished one: {idle, done} x 2 */
 } mrt_frame_stats;
 
 /* A named byte buffer (a map_Kd texture file handed over by the Android front end). */

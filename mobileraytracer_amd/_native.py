@@ -76,7 +76,7 @@ class MrtFrameStats(ctypes.Structure):
         ("fusedMs", ctypes.c_double), ("fusedLaunches", ctypes.c_int64),
         ("levelShadedVertices", ctypes.c_uint64 * 16),
         ("shadowOccluded", ctypes.c_uint64), ("tileMs", ctypes.c_double), ("tileLaunches", ctypes.c_int64),
-        ("walkPhases", ctypes.c_uint64 * 12),
+        ("walkPhases", ctypes.c_uint64 * 16),
     ]
 
 

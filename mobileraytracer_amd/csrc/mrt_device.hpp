@@ -339,6 +339,7 @@ struct TravCount {
     // walk phases (wave iterations counted once per wave, by its first active lane): inner-node
     // visits, leaf tests, triangle tests, and the lanes active in them
     uint32_t innerIters = 0, innerLanes = 0, leafIters = 0, leafLanes = 0, triIters = 0, triLanes = 0;
+    uint32_t innerIdle = 0, innerDone = 0;  // per inner iteration: lanes without a ray / with a finished one
 };
 
 // Generic BVH walk.  kKind selects the leaf routine.  Returns true on an any-hit.

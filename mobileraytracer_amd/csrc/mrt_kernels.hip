@@ -191,6 +191,13 @@ __device__ __forceinline__ void reducePhases(const TravCount& cnt, unsigned long
         for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
         if (laneId() == 0 && x != 0) atomicAdd(stats + kStatPhases + 6 * kind + k, x);
     }
+    const uint32_t w[2] = {cnt.innerIdle, cnt.innerDone};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        unsigned long long x = w[k];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+        if (laneId() == 0 && x != 0) atomicAdd(stats + kStatPhases + 12 + 2 * kind + k, x);
+    }
 }
 
 // counting builds: this wave's entry of the wave log (kWaveLogWaves)

@@ -53,8 +53,9 @@ constexpr int kStatLevelTris = kStatLevelNodes + kMaxLevels;
 constexpr int kStatLevelLeaves = kStatLevelTris + kMaxLevels;
 constexpr int kStatLevelShaded = kStatLevelLeaves + kMaxLevels;  // counting pass: kStatShaded per level
 constexpr int kStatOccluded = kStatLevelShaded + kMaxLevels;  // counting pass: occluded shadow rays
-constexpr int kStatPhases = kStatOccluded + 1;  // counting pass: 2 walks x {inner, leaf, triangle} x {iterations, lanes}
-constexpr int kNumStats = kStatPhases + 12;
+constexpr int kStatPhases = kStatOccluded + 1;  // counting pass: 2 walks x {inner, leaf, triangle} x {iterations, lanes},
+                                                // then 2 walks x inner {idle, done} lanes
+constexpr int kNumStats = kStatPhases + 16;
 // counting builds: per walk launch (closest / any-hit x level) and wave {start, end (100 MHz
 // ticks), rays fetched, child records fetched}, after the statistics (mrt_wave_log)
 constexpr int kWaveLogWaves = 8192;

@@ -854,7 +854,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->shadowNodeRecords += hs[kStatNodesShadow];
     fs->shadowTriTests += hs[kStatTrisShadow];
     fs->shadowOccluded += hs[kStatOccluded];
-    for (int k = 0; k < 12; ++k) fs->walkPhases[k] += hs[kStatPhases + k];
+    for (int k = 0; k < 16; ++k) fs->walkPhases[k] += hs[kStatPhases + k];
     fs->leafRecords += hs[kStatLeaves];
     fs->shadowLeafRecords += hs[kStatLeavesShadow];
     for (int l = 0; l < kMaxLevels && l < 16; ++l) {
@@ -955,7 +955,7 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
                     fs.shadowTriTests += prev.shadowTriTests;
                     fs.leafRecords += prev.leafRecords;
                     fs.shadowOccluded += prev.shadowOccluded;
-                    for (int k = 0; k < 12; ++k) fs.walkPhases[k] += prev.walkPhases[k];
+                    for (int k = 0; k < 16; ++k) fs.walkPhases[k] += prev.walkPhases[k];
                     fs.shadowLeafRecords += prev.shadowLeafRecords;
                     fs.fusedMs += prev.fusedMs;
                     fs.tileMs += prev.tileMs;

@@ -103,6 +103,9 @@ __device__ __forceinline__ void phaseCount(uint32_t* iters, uint32_t* lanes) {
     }
 }
 
+// a lane's walk is over (no node left, no postponed leaf)
+__device__ __forceinline__ bool over2(int ref, int leaf) { return ref == kRefDone && leaf >= 0; }
+
 // number of set bits of a wave mask below this lane
 __device__ __forceinline__ int lanesBelowIn(uint64_t m) {
     return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
@@ -753,8 +756,17 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
         const int innerExit = kExit, leafExit = kLeafExit;
 #endif
         // ---- inner nodes until every active lane holds a postponed leaf ----
+        // (counting builds: the wave's lanes without a ray and with a finished one, per inner iteration)
+        const uint32_t idleLanes = kCount ? static_cast<uint32_t>(__popcll(__ballot(rayIdx == -1))) : 0u;
+        const uint32_t doneLanes = kCount ? static_cast<uint32_t>(__popcll(__ballot(rayIdx != -1 && over2(ref, leaf)))) : 0u;
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
-            if (kCount) phaseCount(&cnt->innerIters, &cnt->innerLanes);
+            if (kCount) {
+                phaseCount(&cnt->innerIters, &cnt->innerLanes);
+                if (lanesBelowIn(__ballot(true)) == 0) {
+                    cnt->innerIdle += idleLanes;
+                    cnt->innerDone += doneLanes;
+                }
+            }
             const float curLim = cullLimit<kInner>(fminf(bt, shT));
             const bool finite = __ballot(!finiteInv(inv)) == 0;
             const int order = kAny ? s.anyOrder : 0;

@@ -32,6 +32,9 @@ def run(ranks):
             out[f"{name}_{ph}_iters"] = it
             out[f"{name}_{ph}_lanes_mean"] = round(ln / max(1, it), 2)
             out[f"{name}_{ph}_occupancy"] = round(ln / max(1, it) / 64, 4)
+        it = max(1, p[6 * w])
+        out[f"{name}_inner_idle_lanes_mean"] = round(p[12 + 2 * w] / it, 2)   # no ray (waiting for a refill)
+        out[f"{name}_inner_done_lanes_mean"] = round(p[13 + 2 * w] / it, 2)   # ray finished, not yet written
     return out
 
 
