@@ -564,6 +564,15 @@ def test_walk_knobs_are_invariant_and_wave_log_is_consistent():
     ran = log[:, :, :, 1] > 0
     assert (log[:, :, :, 1][ran] >= log[:, :, :, 0][ran]).all()
     assert log[0, 1, :, 3].sum() > 0  # child records of level 1
+    # the walks' phase counters (profiles/r04_walk_phase_occupancy.jsonl): every phase ran, at most
+    # 64 lanes per wave iteration, and the lanes without a ray or with a finished one fit beside
+    # the active ones
+    ph = [int(x) for x in st["walkPhases"]]
+    for w in range(2):
+        for k in range(3):
+            it, ln = ph[6 * w + 2 * k], ph[6 * w + 2 * k + 1]
+            assert 0 < it <= ln <= 64 * it, (w, k, it, ln)
+        assert ph[6 * w + 1] + ph[12 + 2 * w] + ph[13 + 2 * w] <= 64 * ph[6 * w], (w, ph)
 
 
 def test_last_level_walk_skip_is_invariant():
