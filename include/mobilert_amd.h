@@ -210,8 +210,14 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  *          the packet walk's LDS stack (kPacketStack),
  * key 17 = level 1 fused: camera rays generated, packet-walked and shaded in one launch (1, default,
  *          where it applies: BVH, packet walk, Whitted / PathTracer, untextured, lean shading, no
- *          counting) or the separate raygen / walk / shade launches (0).
- * (Keys 4, 12-15 - binned emission, queue sorting, graph replay - measured slower and were removed.) */
+ *          counting) or the separate raygen / walk / shade launches (0),
+ * key 19 = the tile kernel k_tiles (every wave renders whole tiles through their ray trees, no
+ *          grid-wide barrier per level; 0 default, measured slower), keys
+ *          20-23 = its tiles claimed per round, pool target, refill threshold and queue growth,
+ * key 27 = the last shadow walk of a pass on the render stream with the closest-hit spill stacks
+ *          (1, default) or on the shadow stream (0).
+ * (Keys 4, 12-15, 18, 24, 25 - binned emission, queue sorting, graph replay, a shadow-occluder
+ * probe, the deeper levels' walk and shading in one launch - measured slower and were removed.) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /
