@@ -82,10 +82,9 @@ struct NoRays {
 #define MRT_PACKET_SEGMENTS 1
 #endif
 #if MRT_PACKET_SEGMENTS
-// the level queue's packets in kWalkShards contiguous ranges, one cursor each (kFetchStride ints
-// apart), a workgroup starting on its XCD group's range (blockIdx % 8) and trying MRT_WALK_SEGMENTS
-// of them: an XCD's L2 sees one eighth of the image, and the exhausted-queue polls spread over 8
-// addresses instead of one
+// the level queue's packets over kWalkShards cursors (kFetchStride ints apart; each serving its
+// interleaved chunks, mrt_trace_ww.hpp), a workgroup starting on its XCD group's cursor (blockIdx %
+// 8) and trying MRT_WALK_SEGMENTS of them: the exhausted-queue polls spread over 8 addresses
 struct PacketFetch {
     int* fetch;
     int count;
@@ -99,7 +98,15 @@ struct PacketFetch {
             int p = 0;
             if ((threadIdx.x & 63u) == 0) p = atomicAdd(fetch + seg * kFetchStride, 1);
             p = __shfl(p, 0, 64);
+#if MRT_SEG_INTERLEAVE
+            // the walk cursors' interleaved chunks (mrt_trace_ww.hpp), in 64-ray packets
+            (void)first;
+            (void)last;
+            const int q = interleavedIndex(p, seg, segChunkShift(packets, kSegChunkLog - 6));
+            if (q < packets) return q << 6;
+#else
             if (first + p < last) return (first + p) << 6;
+#endif
             seg = (seg + 1) % kWalkShards;
             --segsLeft;
         }

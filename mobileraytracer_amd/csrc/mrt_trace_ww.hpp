@@ -36,11 +36,14 @@ constexpr int kWalkShards = 8;        // work cursors per level (one per XCD gro
 // Cursors a wave tries (its own XCD group's first) before it stops fetching.  When a level's queue
 // runs dry every resident wave polls the cursors it has left with an atomic each, and same-address
 // atomics serialise at the memory side: a walk launch with no rays to walk took 100 us with 8
-// (every wave polling every cursor), 19 us with 1 (profiles/r04_latency_probe.txt).  4 keeps most
-// of the load balancing between the XCD groups: C4 15.40 -> 15.22 ms, N = 8 shard 2.88 -> 2.85 ms
-// (2: 15.28 / 2.88, 1: 15.96 / 2.91).
+// (every wave polling every cursor), 19 us with 1 (profiles/r04_latency_probe.txt).  With each
+// cursor over a contiguous eighth of the queue, 4 kept most of the load balancing between the XCD
+// groups (C4 15.40 -> 15.22 ms, N = 8 shard 2.88 -> 2.85 ms; 2: 15.28 / 2.88).  With the cursors'
+// interleaved chunks (below) every cursor holds a mix of cheap and costly regions, and 2 suffice:
+// C4 15.06-15.10 -> 15.02-15.04 ms, N = 8 shard 2.78 -> 2.71-2.73 ms (4: 15.04 / 2.72; 1: 15.09 /
+// 2.70; profiles/r04_cursor_interleave_ab.txt).
 #ifndef MRT_WALK_SEGMENTS
-#define MRT_WALK_SEGMENTS 4
+#define MRT_WALK_SEGMENTS 2
 #endif
 constexpr int kWalkStack = kLdsStackMin;  // LDS stack entries per thread (deeper ones spill)
 constexpr int kWalkTop = kTopNodesMax;
@@ -436,6 +439,29 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
     __syncthreads();
 }
 
+// The work cursors' layout (round 4).  Cursor s serves the chunks s, s + 8, s + 16, ... of 2^shift
+// queue entries, not a contiguous eighth of the queue: adjacent entries are spatially coherent, so
+// a contiguous eighth is one region of the image, and the regions' costs differ - a cursor over
+// cheap pixels ran dry early, and the waves that had drained their cursors ended while the others
+// still walked (at the N = 8 shard a level's waves ended between 38 % and 74 % of it).  Chunks of
+// 4,096 rays keep a wave's rays coherent; at least 8 chunks per cursor keep small queues spread.
+#ifndef MRT_SEG_INTERLEAVE
+#define MRT_SEG_INTERLEAVE 1
+#endif
+#ifndef MRT_SEG_CHUNK_LOG
+#define MRT_SEG_CHUNK_LOG 12
+#endif
+constexpr int kSegChunkLog = MRT_SEG_CHUNK_LOG;  // rays per chunk: 2^12
+// log2 of the chunk size for n entries: maxLog, or smaller so that every cursor has >= 8 chunks
+__device__ __forceinline__ int segChunkShift(int n, int maxLog) {
+    const int per = max(n >> 6, 1);  // n / (8 cursors x 8 chunks)
+    return min(maxLog, 31 - __clz(per));
+}
+// the queue entry of cursor seg's j-th claim
+__device__ __forceinline__ int interleavedIndex(int j, int seg, int shift) {
+    return ((((j >> shift) * kWalkShards) + seg) << shift) + (j & ((1 << shift) - 1));
+}
+
 // The rays a walk takes: a queue policy.
 //   o(i), d(i)      ray i's origin / direction records;
 //   hit(i, h)       the closest hit (t, u, v, primitive code); occ(i, f): the occluded flag;
@@ -443,9 +469,9 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
 //                   lanes wanting a ray: this lane's ray index, or -1 (none left for it);
 //   drained()       wave-uniform: the queue has no ray left for this wave.
 // LevelQueue: a level's queue arrays, rays [0, count), fetched through kWalkShards cursors
-// (kFetchStride ints apart), one per XCD group of workgroups (blockIdx % 8), each over a contiguous
-// eighth of the queue; a drained eighth is left for the next (speed only: any placement gives the
-// same results).
+// (kFetchStride ints apart), one per XCD group of workgroups (blockIdx % 8), each over its
+// interleaved chunks of the queue (above); a drained cursor is left for the next (speed only: any
+// placement gives the same results).
 struct LevelQueue {
     const float4* __restrict__ rO;
     const float4* __restrict__ rD;
@@ -454,8 +480,9 @@ struct LevelQueue {
     int* fetch;
     int seg = static_cast<int>(blockIdx.x % kWalkShards);  // wave-uniform cursor state
     int segsLeft = MRT_WALK_SEGMENTS;
+    int shift;  // the cursors' chunks: 2^shift rays
     __device__ __forceinline__ LevelQueue(const float4* o_, const float4* d_, float4* out_, int count_, int* fetch_)
-        : rO(o_), rD(d_), out(out_), count(count_), fetch(fetch_) {}
+        : rO(o_), rD(d_), out(out_), count(count_), fetch(fetch_), shift(segChunkShift(count_, kSegChunkLog)) {}
     __device__ __forceinline__ float4 o(int i) const { return rO[i]; }
     __device__ __forceinline__ float4 d(int i) const { return rD[i]; }
     __device__ __forceinline__ void hit(int i, float4 h) const { out[i] = h; }
@@ -474,8 +501,15 @@ struct LevelQueue {
             base = __shfl(base, leader, 64);
             const bool mine = ((pending >> lane) & 1ull) != 0;
             if (mine) {
+#if MRT_SEG_INTERLEAVE
+                (void)segStart;
+                (void)segEnd;
+                const int idx = interleavedIndex(base + lanesBelowIn(pending), seg, shift);
+                if (idx < count) got = idx;
+#else
                 const int idx = segStart + base + lanesBelowIn(pending);
                 if (idx < segEnd) got = idx;
+#endif
             }
             pending = __ballot(mine && got < 0);
             if (pending != 0) {
