@@ -4,6 +4,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Both forms run N ranks, one process per GPU.  Without a launcher (WORLD_SIZE unset) and N > 1,
+this process starts the N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT set, before anything touches the GPU), forwards their output (rank 0 prints the
+line) and exits with the worst of their return codes.  It refuses, non-zero and before any GPU
+call, N larger than the visible GPUs (RCCL: one GPU per rank) and, under a launcher, N != WORLD_SIZE.
+
 Workload (BASELINE.json metric, configs[3] = C4): the Conference scene at 1920x1080,
 4 samples per pixel, PathTracer, RayDepthMax 5 (camera ray + 4 bounces), samplesLight 1.
 A step is one Renderer::renderFrame (all 4 samples).  `value` is WALKED Mrays/s: every ray
@@ -62,6 +68,61 @@ def parse():
     return p.parse_args()
 
 
+def launch_plan(gpus, env, device_count):
+    """What `bench.py --gpus N` does in this process: ("run", None) renders here (one rank, or one
+    rank of a launcher's world); ("spawn", N) starts N rank processes; ("error", message).  Decided
+    from the environment and the device count alone (torch.cuda.device_count() does not initialise
+    the GPU), so the parent of spawned ranks never touches the GPU."""
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    backend = env.get("MRT_BENCH_BACKEND", "nccl")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            return "error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
+        local_world = int(env.get("LOCAL_WORLD_SIZE", world))
+        if backend == "nccl" and local_world > device_count:
+            return "error", (f"{local_world} ranks on this node but {device_count} visible GPU(s): "
+                             "RCCL needs one GPU per rank")
+        return "run", None
+    if gpus > 1 and backend == "nccl" and gpus > device_count:
+        return "error", f"--gpus {gpus} but {device_count} visible GPU(s): RCCL needs one GPU per rank"
+    return ("spawn", gpus) if gpus > 1 else ("run", None)
+
+
+def spawn_ranks(n, argv):
+    """Start n rank processes of this script (one per GPU; the torch.distributed.run environment)
+    and wait for them.  A rank that fails ends the others (their own PIDs); returns the worst code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for rank in range(n):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    worst = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0:
+                worst = worst or rc
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        rc = p.wait()
+        if rc != 0 and worst == 0:
+            worst = rc
+    return worst
+
+
 def effective_cores():
     """Host threads this process may use: its CPU affinity, capped by a cgroup CPU quota."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
@@ -94,11 +155,21 @@ def cpu_baseline(args, scene):
     o = O.Oracle(args.width, args.height, args.shader, -1, args.spp, 1, args.max_depth,
                  obj=scene[0], mtl=scene[1], cam=scene[2])
     o.set_faithful(True)
+    load_before = os.getloadavg() if hasattr(os, "getloadavg") else None
+    c0 = time.process_time()
     t0 = time.perf_counter()
     _, rays = o.render(threads=threads)
     dt = time.perf_counter() - t0
+    cpu_s = time.process_time() - c0
+    load_after = os.getloadavg() if hasattr(os, "getloadavg") else None
     o.close()
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            # the box's load explains the baseline's box-to-box swing: the per-core rate is the rays over
+            # the CPU seconds this process got, and utilisation is how many of `cores` it actually ran on
+            "per_core_value": rays / cpu_s / 1e6 if cpu_s > 0 else None,
+            "utilisation": cpu_s / dt / threads if dt > 0 else None,
+            "loadavg_1_5_15_before": load_before, "loadavg_1_5_15_after": load_after,
+            "host_cpus_visible": os.cpu_count(),
             "cpu_model": cpu_model(),
             "sample": f"full frame (all 256 reference tiles, {args.spp} spp), {rays} rays built, {dt:.1f} s; "
                       "timing-faithful draws (shared atomic sampler cursors)",
@@ -266,6 +337,12 @@ def kernel_roofline(r, step):
 def main():
     args = parse()
     import torch
+    action, what = launch_plan(args.gpus, os.environ, torch.cuda.device_count())
+    if action == "error":
+        print(f"bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if action == "spawn":
+        sys.exit(spawn_ranks(what, sys.argv[1:]))
     import torch.distributed as dist
     import mobileraytracer_amd as m
     from mobileraytracer_amd import scenes

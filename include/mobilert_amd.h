@@ -69,6 +69,15 @@ typedef struct mrt_config {
     int32_t progressive;  /* 1: one pass per sample; bitmap and mrt_get_sample() updated after
                            * each (Renderer.cpp:53-88).  0: all samples in flight at once.
                            * The final bitmap is the same. */
+    /* A device group (Renderer::renderFrame spreading one frame over its workers,
+     * Renderer.cpp:62-82, with the workers on GPUs): deviceCount > 1 renders every frame as
+     * deviceCount screen-tile shards, shard i on HIP device devices[i] from a host thread of its
+     * own, assembled on devices[0] (peer copies over xGMI, then one unpack launch), which holds
+     * the device bitmap of mrt_render_frame_device.  A repeated ordinal puts several shards on
+     * one GPU.  The bitmap and the ray counts equal the single-GPU frame's.  `device`, rankIndex
+     * and rankCount must be left at their defaults (-1 / 0 / <= 1).  deviceCount <= 1: one GPU. */
+    const int32_t *devices;
+    int32_t deviceCount;
 } mrt_config;
 
 typedef struct mrt_scene_info {
@@ -87,6 +96,7 @@ typedef struct mrt_scene_info {
                                        in time, i.e. they feed different hardware queues, whatever
                                        streams the process created before); 0: serialised */
     int64_t shadowStreamsTried;     /* shadow streams created until one ran concurrently */
+    int64_t deviceCount;            /* GPUs of the renderer's device group (1: a single GPU) */
 } mrt_scene_info;
 
 typedef struct mrt_frame_stats {
@@ -125,8 +135,6 @@ typedef struct mrt_frame_stats {
     int64_t fusedLaunches;         /* fused level-1 launches of the frame (counted in shadeLaunches too) */
     uint64_t levelShadedVertices[16]; /* counting pass only: shadedVertices of depth 1..16 */
     uint64_t shadowOccluded;       /* counting pass only: occluded shadow rays */
-    double tileMs;                 /* profiling: duration of the tile kernel launches (k_tiles) */
-    int64_t tileLaunches;          /* tile kernel launches of the frame (0: the level kernels ran) */
     uint64_t walkPhases[16];       /* counting pass only, the persistent walks (closest hit, then any hit):
                                       wave iterations and the lanes active in them of the inner-node phase,
                                       the leaf phase and the triangle loop: {iters, lanes} x 3 x 2; then per
@@ -211,13 +219,13 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  * key 17 = level 1 fused: camera rays generated, packet-walked and shaded in one launch (1, default,
  *          where it applies: BVH, packet walk, Whitted / PathTracer, untextured, lean shading, no
  *          counting) or the separate raygen / walk / shade launches (0),
- * key 19 = the tile kernel k_tiles (every wave renders whole tiles through their ray trees, no
- *          grid-wide barrier per level; 0 default, measured slower), keys
- *          20-23 = its tiles claimed per round, pool target, refill threshold and queue growth,
  * key 27 = the last shadow walk of a pass on the render stream with the closest-hit spill stacks
- *          (1, default) or on the shadow stream (0).
- * (Keys 4, 12-15, 18, 24, 25 - binned emission, queue sorting, graph replay, a shadow-occluder
- * probe, the deeper levels' walk and shading in one launch - measured slower and were removed.) */
+ *          (1, default) or on the shadow stream (0),
+ * key 28 = at most this many workgroups per walk launch (0, default: the occupancy grid; 1-65536):
+ *          a test knob, every grid size walks every ray.
+ * (Keys 4, 12-15, 18, 19-25 - binned emission, queue sorting, graph replay, the tile kernel, a
+ * shadow-occluder probe, the deeper levels' walk and shading in one launch - measured slower and
+ * were removed.) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /

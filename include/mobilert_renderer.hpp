@@ -145,6 +145,25 @@ public:
         c.maxDepth = md != nullptr ? std::atoi(md) : 0;
         c.rankCount = 1;
         c.device = -1;
+        // MOBILERT_DEVICES=0,1,...: the frame sharded over these GPUs (mrt_config.devices; the
+        // reference's renderFrame spreads a frame over its workers, Renderer.cpp:62-82)
+        std::vector<std::int32_t> devices;
+        if (const char* dl = std::getenv("MOBILERT_DEVICES")) {
+            std::string item;
+            for (const char* q = dl;; ++q) {
+                if (*q == ',' || *q == '\0') {
+                    if (!item.empty()) devices.push_back(static_cast<std::int32_t>(std::stoi(item)));
+                    item.clear();
+                    if (*q == '\0') break;
+                } else {
+                    item.push_back(*q);
+                }
+            }
+        }
+        if (devices.size() > 1) {
+            c.devices = devices.data();
+            c.deviceCount = static_cast<std::int32_t>(devices.size());
+        }
         c.cull = 3;         // exact for every input
         c.progressive = 1;  // the bitmap and getSample() advance sample by sample (Renderer.cpp:53-88)
         // a camera given as parameters is set after creation; a loaded definition is parsed there

@@ -52,6 +52,9 @@ class Config:
     cull: int = 3
     maxPathsPerPass: int = 0
     progressive: int = 0
+    # a device group: one screen-tile shard per listed HIP device, assembled on devices[0]
+    # (mrt_config.devices; empty or one entry: a single GPU, `device`)
+    devices: List[int] = dataclasses.field(default_factory=list)
 
     def to_c(self):
         c = _native.MrtConfig()
@@ -62,6 +65,10 @@ class Config:
         c.printStdOut = int(bool(self.printStdOut))
         self._keep = [s.encode() for s in (self.objFilePath, self.mtlFilePath, self.camFilePath)]
         c.objFilePath, c.mtlFilePath, c.camFilePath = self._keep
+        if len(self.devices) > 1:
+            self._keep_devices = (ctypes.c_int32 * len(self.devices))(*[int(d) for d in self.devices])
+            c.devices = self._keep_devices
+            c.deviceCount = len(self.devices)
         return c
 
 

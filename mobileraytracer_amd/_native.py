@@ -38,7 +38,7 @@ class MrtConfig(ctypes.Structure):
         ("objFilePath", ctypes.c_char_p), ("mtlFilePath", ctypes.c_char_p), ("camFilePath", ctypes.c_char_p),
         ("maxDepth", ctypes.c_int32), ("rankIndex", ctypes.c_int32), ("rankCount", ctypes.c_int32),
         ("device", ctypes.c_int32), ("cull", ctypes.c_int32), ("maxPathsPerPass", ctypes.c_int32),
-        ("progressive", ctypes.c_int32),
+        ("progressive", ctypes.c_int32), ("devices", ctypes.POINTER(ctypes.c_int32)), ("deviceCount", ctypes.c_int32),
     ]
 
 
@@ -55,7 +55,7 @@ class MrtBlob(ctypes.Structure):
 class MrtSceneInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "triangles", "lights", "planes", "spheres", "materials", "triangleNodes", "triangleBvhDepth",
-        "pixelSlots", "pixelSlotsMax", "deviceBytes", "shadowStreamConcurrent", "shadowStreamsTried")]
+        "pixelSlots", "pixelSlotsMax", "deviceBytes", "shadowStreamConcurrent", "shadowStreamsTried", "deviceCount")]
 
 
 class MrtFrameStats(ctypes.Structure):
@@ -75,7 +75,7 @@ class MrtFrameStats(ctypes.Structure):
         ("levelLeafRecords", ctypes.c_uint64 * 16),
         ("fusedMs", ctypes.c_double), ("fusedLaunches", ctypes.c_int64),
         ("levelShadedVertices", ctypes.c_uint64 * 16),
-        ("shadowOccluded", ctypes.c_uint64), ("tileMs", ctypes.c_double), ("tileLaunches", ctypes.c_int64),
+        ("shadowOccluded", ctypes.c_uint64),
         ("walkPhases", ctypes.c_uint64 * 16),
     ]
 

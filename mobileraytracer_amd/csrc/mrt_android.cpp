@@ -10,8 +10,10 @@
 // interval runs from the clock's epoch, :391-404).
 #include "mobilert_amd.h"
 #include "mobilert_android.h"
+#include "mrt_scene.hpp"
 
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <condition_variable>
 #include <map>
@@ -114,6 +116,12 @@ int32_t mrt_android_initialize(const mrt_android_config* config) {
         c.device = -1;
         c.cull = 3;  // exact for every input
         c.progressive = 1;  // the bitmap fills sample by sample while RenderTask polls it
+        // MOBILERT_DEVICES=0,1,...: the frame sharded over these GPUs (a device group)
+        const std::vector<int32_t> devices = mrt::parseDeviceList(std::getenv("MOBILERT_DEVICES"));
+        if (devices.size() > 1) {
+            c.devices = devices.data();
+            c.deviceCount = static_cast<int32_t>(devices.size());
+        }
         const bool builtin = config->scene >= 0 && config->scene <= 3;
         mrt_renderer* r = nullptr;
         const auto t0 = std::chrono::steady_clock::now();

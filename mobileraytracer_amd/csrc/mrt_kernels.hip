@@ -21,6 +21,7 @@
 #include "mrt_trace_packet.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <utility>
 
 namespace mrt {
@@ -1082,340 +1083,6 @@ void launchLoadRays(const Level& lv, const float* orig, const float* dir, const 
 }
 
 // ---------------------------------------------------------------------------------------
-// The tile kernel: per-tile ray trees, wave-local queues, no grid-wide barrier per level.
-//
-// The reference renders a tile's pixels through their whole ray trees before claiming the next tile
-// from an atomic counter (Renderer.cpp:62-82, 107-170, 189-197); the level kernels above instead
-// walk, shade and wait for every ray of a level of the whole frame before the next level starts,
-// so each level ends in a tail in which most lanes of the GPU idle.  Here every wave is an
-// independent renderer of tiles (64 / spp pixels x spp samples: its camera rays are exactly one
-// 64-ray packet).  A wave keeps up to kTileSlots tiles in flight at different depths, their
-// records in a wave-private arena (slot-major; per slot the level arrays of the level kernels) and
-// their queue counters in LDS, and runs rounds of
-//   claim    up to maxNew tiles from kWalkShards per-XCD-group cursors (while the next pool is small);
-//   camera   each new tile: ray generation, the packet walk and shading in the wave (as
-//            k_trace_packet_shade; slots allocated by one LDS atomic per packet);
-//   walk     the closest-hit rays of every tile of the wave at its current level, as ONE pool
-//            (traceWhileWhileQ over a wave-private cursor: refill and tail donation as in k_trace);
-//   shadow   the shadow rays its tiles' last shading emitted, as one pool (any hit);
-//   shade    the walked rays (shadePrepare / shadeEmit: children and shadow rays allocated per lane
-//            by 64-bit LDS atomics on the tile's counter pair);
-//   finish   tiles with nothing left in flight: bottom-up resolve of their levels and
-//            incrementalAvg of their pixels (resolveVertex / accumulatePixel).
-// The waves never wait for one another: a wave whose walk is in its tail shares the SIMD with waves
-// in other phases and at other depths.  Results equal the level kernels' bit for bit: every path
-// draws from its own key (sampleIndex), the walks and shading are the same functions, and children
-// are linked by index.
-struct alignas(8) TileWave {
-    int cnt[kTileSlots][kTileCnt];  // per slot: cntRays(l) / cntShadows(l) (the pair {l + 1, l} 8-aligned)
-    int tile[kTileSlots];           // tile of the slot, -1 free
-    int level[kTileSlots];          // the level whose closest-hit rays are walked next
-    int shadowLevel[kTileSlots];    // the level whose shadow rays wait for the next shadow walk (0 none)
-    int poolSlot[kTileSlots];       // the current walk pool: entry e = (slot, level), rays from poolPre[e]
-    int poolLevel[kTileSlots];
-    int poolPre[kTileSlots + 1];
-    int nPool;
-};
-
-__device__ __forceinline__ long long tileLevelBytes(int cap, int spl) {
-    return static_cast<long long>(cap) * 84 + static_cast<long long>(cap) * spl * 48;
-}
-// Level l's arrays of the tile slot at slotBase (tileSlotBytes' layout)
-__device__ __forceinline__ Level tileLevel(const TileArgs& a, char* slotBase, int l) {
-    const int cap = l == 1 ? a.cap1 : a.capN;
-    const int capS = cap * a.spl;
-    char* b = slotBase + (l == 1 ? 0ll : tileLevelBytes(a.cap1, a.spl) + (l - 2) * tileLevelBytes(a.capN, a.spl));
-    Level L{};
-    L.rO = reinterpret_cast<float4*>(b);
-    L.rD = L.rO + cap;
-    L.hit = L.rD + cap;
-    L.vtx = reinterpret_cast<int4*>(L.hit + cap);
-    L.res = reinterpret_cast<float4*>(L.vtx + cap);
-    L.sO = L.res + cap;
-    L.sD = L.sO + capS;
-    L.sC = L.sD + capS;
-    L.tree = reinterpret_cast<uint32_t*>(L.sC + capS);
-    L.kd = nullptr;
-    L.last = nullptr;
-    L.cap = cap;
-    L.shadowCap = capS;
-    return L;
-}
-
-// the wave's records and LDS state become visible to all its lanes (between phases)
-__device__ __forceinline__ void waveSync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
-
-// A walk pool: the rays of every entry (slot, level) of TileWave::pool*, closest-hit rays (kAny
-// false: rO / rD -> hit) or shadow rays (true: sO / sD -> sC.w), taken in order from a wave-private
-// cursor (no atomics: only this wave takes from it).
-template <bool kAny>
-struct TileQueue {
-    const TileArgs* a;
-    char* arena;
-    const TileWave* w;
-    int count;
-    int cursor = 0;
-    __device__ __forceinline__ int entry(int v) const {
-        int e = 0;
-#pragma unroll
-        for (int k = 1; k < kTileSlots; ++k) e = (k < w->nPool && v >= w->poolPre[k]) ? k : e;
-        return e;
-    }
-    __device__ __forceinline__ Level level(int e) const {
-        return tileLevel(*a, arena + static_cast<long long>(w->poolSlot[e]) * a->slotBytes, w->poolLevel[e]);
-    }
-    __device__ __forceinline__ float4 o(int v) const {
-        const int e = entry(v);
-        const Level L = level(e);
-        return kAny ? L.sO[v - w->poolPre[e]] : L.rO[v - w->poolPre[e]];
-    }
-    __device__ __forceinline__ float4 d(int v) const {
-        const int e = entry(v);
-        const Level L = level(e);
-        return kAny ? L.sD[v - w->poolPre[e]] : L.rD[v - w->poolPre[e]];
-    }
-    __device__ __forceinline__ void hit(int v, float4 h) const {
-        const int e = entry(v);
-        level(e).hit[v - w->poolPre[e]] = h;
-    }
-    __device__ __forceinline__ void occ(int v, float f) const {
-        const int e = entry(v);
-        level(e).sC[v - w->poolPre[e]].w = f;
-    }
-    __device__ __forceinline__ bool drained() const { return cursor >= count; }
-    __device__ __forceinline__ int take(uint64_t pending) {
-        const int idx = cursor + lanesBelowIn(pending);
-        cursor = min(count, cursor + __popcll(pending));
-        return ((pending >> laneId()) & 1ull) != 0 && idx < count ? idx : -1;
-    }
-};
-
-// Builds the wave's pool (lane 0 writes; then waveSync): kAny false - every tile's closest-hit rays
-// at its current level (levels 2 .. maxDepth; level maxDepth + 1 is depth-capped, never walked);
-// true - every tile's pending shadow rays.  Returns the pool's ray count (wave-uniform).
-template <bool kAny>
-__device__ __forceinline__ int buildPool(const TileArgs& a, TileWave& w) {
-    int n = 0, e = 0;
-    for (int k = 0; k < kTileSlots; ++k) {
-        if (w.tile[k] < 0) continue;
-        const int l = kAny ? w.shadowLevel[k] : w.level[k];
-        if (kAny ? l <= 0 : (l < 2 || l > a.sa.maxDepth)) continue;
-        const int cap = (l == 1 ? a.cap1 : a.capN) * (kAny ? a.spl : 1);
-        const int c = min(w.cnt[k][kAny ? cntShadows(l) : cntRays(l)], cap);
-        if (c <= 0) continue;
-        if (laneId() == 0) {
-            w.poolSlot[e] = k;
-            w.poolLevel[e] = l;
-            w.poolPre[e] = n;
-        }
-        ++e;
-        n += c;
-    }
-    if (laneId() == 0) {
-        w.poolPre[e] = n;
-        w.nPool = e;
-    }
-    waveSync();
-    return n;
-}
-
-// The camera packet of a new tile: k_trace_packet_shade's shading, into the tile's level 1 / 2
-// arrays, its slots allocated on the tile's LDS counter pair {rays of level 2, shadow rays of 1}.
-template <int kShader>
-struct TilePacketShade {
-    const DScene* s;
-    Level l1, l2;
-    unsigned long long* pair;
-    int* counters;
-    ShadeArgs a;
-    bool dead;
-    __device__ __forceinline__ void operator()(int i, bool valid, float4 o4, float4 d4, float4 h) const {
-        ShadeState v{};
-        if (valid) {
-            v = shadePrepare<kShader>(*s, o4, d4, h, 1u, 1, a, make_float4(0.0F, 0.0F, 0.0F, -1.0F), s->mats, s->lights);
-            if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
-        }
-        int childBase, shadowBase;
-        waveAllocPair(pair, valid ? v.nChild : 0, valid ? v.nShadow : 0, &childBase, &shadowBase);
-        if (valid) shadeEmit(*s, v, i, l1, l2, shadowBase, childBase, counters, a, dead, s->lights);
-    }
-};
-
-#ifndef MRT_TILE_WAVES
-#define MRT_TILE_WAVES 6
-#endif
-template <int kShader, int kCull>
-__global__ __launch_bounds__(kWalkThreads, MRT_TILE_WAVES) void k_tiles(DScene s, TileArgs a, int2* gstack, int gdepth) {
-    __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
-    __shared__ QNode4 ldsTop[kWalkTop];
-    __shared__ int tailBest[kWalkThreads];
-    __shared__ int waveStacks[kWalkThreads / 64][kPacketStack];
-    __shared__ TileWave waves[kWalkThreads / 64];
-    auto st = makeRefStack<kWalkThreads>(ldsStack, gstack, gdepth);
-    stageTop<kWalkThreads>(s, ldsTop);
-    const int lane = laneId();
-    const int wv = static_cast<int>(threadIdx.x >> 6);
-    TileWave& w = waves[wv];
-    char* const arena = a.arena + static_cast<long long>(blockIdx.x * (kWalkThreads / 64) + wv) * kTileSlots * a.slotBytes;
-    const int D = a.sa.maxDepth;
-    const int spp = a.ra.spp;
-    if (lane < kTileSlots) {
-        w.tile[lane] = -1;
-        w.level[lane] = 0;
-        w.shadowLevel[lane] = 0;
-    }
-    for (int k = lane; k < kTileSlots * kTileCnt; k += 64) (&w.cnt[0][0])[k] = 0;
-    waveSync();
-    TravCount cnt{0u, 0u};
-    int totals = 0;  // lane l < kTileCnt: counter l summed over the wave's finished tiles
-    int seg = static_cast<int>(blockIdx.x % kWalkShards), segsLeft = kWalkShards;
-    while (true) {
-        // ---- claim: up to maxNew tiles while the next closest-hit pool is small ----
-        {
-            int nFree = 0, pending = 0;
-            for (int k = 0; k < kTileSlots; ++k) {
-                if (w.tile[k] < 0) {
-                    ++nFree;
-                } else if (w.level[k] >= 2 && w.level[k] <= D) {
-                    pending += min(w.cnt[k][cntRays(w.level[k])], a.capN);
-                } else if (w.level[k] == 1) {
-                    pending += 64;
-                }
-            }
-            int want = pending < a.poolTarget ? min(nFree, a.maxNew) : 0;
-            while (want > 0 && segsLeft > 0) {
-                const int segStart = static_cast<int>((static_cast<long long>(a.nTiles) * seg) / kWalkShards);
-                const int segEnd = static_cast<int>((static_cast<long long>(a.nTiles) * (seg + 1)) / kWalkShards);
-                int base = 0;
-                if (lane == 0) base = atomicAdd(a.claim + seg * kFetchStride, want);
-                base = __shfl(base, 0, 64);
-                const int first = segStart + base;
-                const int got = max(0, min(want, segEnd - first));
-                if (got < want) {
-                    seg = (seg + 1) % kWalkShards;
-                    --segsLeft;
-                }
-                for (int j = 0, k = 0; j < got && k < kTileSlots; ++k) {  // free slots in order
-                    if (w.tile[k] >= 0) continue;
-                    if (lane == 0) {
-                        w.tile[k] = first + j;
-                        w.level[k] = 1;
-                        w.shadowLevel[k] = 0;
-                    }
-                    waveSync();
-                    ++j;
-                }
-                want -= got;
-            }
-        }
-        // ---- camera rays of the new tiles: one packet each, walked and shaded in the wave ----
-        for (int k = 0; k < kTileSlots; ++k) {
-            if (w.tile[k] < 0 || w.level[k] != 1) continue;
-            const int q0 = w.tile[k] * a.tilePixels;
-            const int nq = min(a.tilePixels, a.nSlots - q0);
-            RaygenArgs ra = a.ra;
-            ra.slotBase = a.ra.slotBase + q0;
-            ra.nPaths = nq * spp;
-            char* const sb = arena + static_cast<long long>(k) * a.slotBytes;
-            const TilePacketShade<kShader> post{&s, tileLevel(a, sb, 1), tileLevel(a, sb, D >= 2 ? 2 : 1),
-                                                reinterpret_cast<unsigned long long*>(&w.cnt[k][cntRays(2)]), a.counters,
-                                                a.sa, D < 2};
-            tracePacketF<false, kCull>(s, nullptr, nullptr, nullptr, ra.nPaths, OnePacket{}, st, &cnt, waveStacks[wv], post,
-                                       PacketRays{&ra});
-            if (lane == 0) {
-                w.cnt[k][cntRays(1)] = ra.nPaths;
-                w.level[k] = 2;
-                w.shadowLevel[k] = 1;
-            }
-            waveSync();
-        }
-        // ---- the closest-hit walk of every tile's current level, one pool ----
-        const int nClosest = buildPool<false>(a, w);
-        if (nClosest > 0) {
-            TileQueue<false> q{&a, arena, &w, nClosest};
-            traceWhileWhileQ<false, false, kCull>(s, q, st, &cnt, ldsTop, tailBest);
-            waveSync();
-        }
-        // ---- the shadow rays of every tile's last shaded level, one pool ----
-        const int nShadow = buildPool<true>(a, w);
-        if (nShadow > 0) {
-            TileQueue<true> q{&a, arena, &w, nShadow};
-            traceWhileWhileQ<true, false, kCull>(s, q, st, &cnt, ldsTop, tailBest);
-            waveSync();
-        }
-        if (lane < kTileSlots) w.shadowLevel[lane] = 0;  // (every pending set was in the pool)
-        // ---- shading of the walked rays ----
-        const int nShade = buildPool<false>(a, w);
-        for (int v0 = 0; v0 < nShade; v0 += 64) {
-            const int v = v0 + lane;
-            const bool valid = v < nShade;
-            int e = 0;
-#pragma unroll
-            for (int j = 1; j < kTileSlots; ++j) e = (j < w.nPool && v >= w.poolPre[j]) ? j : e;
-            const int k = w.poolSlot[e], L = w.poolLevel[e], i = v - w.poolPre[e];
-            char* const sb = arena + static_cast<long long>(k) * a.slotBytes;
-            const Level lv = tileLevel(a, sb, L);
-            const bool dead = L + 1 > D;
-            const Level nx = tileLevel(a, sb, dead ? L : L + 1);
-            ShadeState vs{};
-            if (valid) {
-                vs = shadePrepare<kShader>(s, lv.rO[i], lv.rD[i], lv.hit[i], lv.tree[i], L, a.sa,
-                                           make_float4(0.0F, 0.0F, 0.0F, -1.0F), s.mats, s.lights);
-                if (!vs.terminal && vs.nChild > 0 && !dead) vs.dir0 = firstChildDir(vs);
-            }
-            int childBase = 0, shadowBase = 0;
-            const int nC = valid ? vs.nChild : 0, nS = valid ? vs.nShadow : 0;
-            if (nC + nS > 0) {  // {rays of level L + 1, shadow rays of level L}: one 64-bit LDS atomic
-                const unsigned long long add =
-                    (static_cast<unsigned long long>(static_cast<unsigned>(nS)) << 32) | static_cast<unsigned>(nC);
-                const unsigned long long old =
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&w.cnt[k][cntRays(L + 1)]), add);
-                childBase = static_cast<int>(static_cast<unsigned>(old & 0xFFFFFFFFull));
-                shadowBase = static_cast<int>(static_cast<unsigned>(old >> 32));
-            }
-            if (valid) shadeEmit(s, vs, i, lv, nx, shadowBase, childBase, a.counters, a.sa, dead, s.lights);
-        }
-        waveSync();
-        if (lane == 0) {
-            for (int e = 0; e < w.nPool; ++e) {
-                const int k = w.poolSlot[e];
-                w.shadowLevel[k] = w.level[k];
-                ++w.level[k];
-            }
-        }
-        waveSync();
-        // ---- finished tiles: resolve bottom-up, accumulate their pixels, free the slot ----
-        bool any = false;
-        for (int k = 0; k < kTileSlots; ++k) {
-            if (w.tile[k] < 0) continue;
-            any = true;
-            const int L = w.level[k];
-            if (w.shadowLevel[k] != 0 || (L <= D && w.cnt[k][cntRays(L)] > 0)) continue;
-            char* const sb = arena + static_cast<long long>(k) * a.slotBytes;
-            for (int l = min(L - 1, D); l >= 1; --l) {
-                const Level lv = tileLevel(a, sb, l);
-                const Level nx = tileLevel(a, sb, l < D ? l + 1 : l);
-                const int n = min(w.cnt[k][cntRays(l)], lv.cap);
-                for (int i = lane; i < n; i += 64) resolveVertex<kShader, false>(s, lv, nx, i, l, a.sa, l == D ? 1 : 0);
-                waveSync();
-            }
-            const int q0 = w.tile[k] * a.tilePixels;
-            AccumArgs aa = a.aa;
-            aa.slotBase = a.aa.slotBase + q0;
-            const Level l1 = tileLevel(a, sb, 1);
-            if (lane < min(a.tilePixels, a.nSlots - q0)) accumulatePixel(aa, l1.res, a.bitmap, a.packed, lane);
-            if (lane < kTileCnt) totals += w.cnt[k][lane];
-            waveSync();
-            if (lane == 0) w.tile[k] = -1;
-            if (lane < kTileCnt) w.cnt[k][lane] = 0;
-            waveSync();
-        }
-        if (!any && segsLeft == 0) break;
-    }
-    if (lane < kTileCnt && totals != 0) atomicAdd(a.counters + lane, totals);
-}
-
-// ---------------------------------------------------------------------------------------
 // launch wrappers
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st) {
     const int blocks = (a.nPaths + 255) / 256;
@@ -1426,17 +1093,24 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
 // spill stacks were sized for.
 template <typename K>
 int persistentGrid(K kernel, int slot, int maxThreads) {
-    static int occ[24] = {};
-    static int cus = 0;
+    // (atomics: the shards of a device group launch from host threads of their own; every thread
+    // computes the same values)
+    static std::atomic<int> occ[24] = {};
+    static std::atomic<int> cusCache{0};
     const int cap = std::max(1, maxThreads / kWalkThreads);
+    int cus = cusCache.load(std::memory_order_relaxed);
     if (cus == 0) {
         hipDeviceProp_t prop;
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return cap;
         cus = prop.multiProcessorCount;
+        cusCache.store(cus, std::memory_order_relaxed);
     }
-    int& o = occ[slot];
-    if (o == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, kWalkThreads, 0) != hipSuccess) o = 0;
+    int o = occ[slot].load(std::memory_order_relaxed);
+    if (o == 0) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, kWalkThreads, 0) != hipSuccess) o = 0;
+        occ[slot].store(o, std::memory_order_relaxed);
+    }
     return o > 0 ? std::min(cap, o * cus) : cap;
 }
 
@@ -1601,46 +1275,13 @@ int traceResidentThreadsPerCU() {
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullNone>),
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullExact>),
                              reinterpret_cast<const void*>(k_trace_packet<false, kCullExact>),
-                             reinterpret_cast<const void*>(k_trace_packet<false, kCullNone>),
-                             reinterpret_cast<const void*>(k_tiles<kShaderPathTracer, kCullExact>),
-                             reinterpret_cast<const void*>(k_tiles<kShaderWhitted, kCullExact>)};
+                             reinterpret_cast<const void*>(k_trace_packet<false, kCullNone>)};
     for (const void* k : kernels) {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWalkThreads, 0) == hipSuccess)
             best = std::max(best, n * kWalkThreads);
     }
     return best;
-}
-
-bool canTile(int shader, const DScene& s, const ShadeArgs& a, int spp) {
-    return s.tiles != 0 && s.accel == kAccBVH && s.packet != 0 && s.variant == 1 &&
-           (s.cull == kCullNone || s.cull == kCullExact) && (shader == kShaderWhitted || shader == kShaderPathTracer) &&
-           s.textured == 0 && s.matsFinite != 0 && a.stats == nullptr && a.maxDepth + 1 <= kTileLevels && spp >= 1 &&
-           spp <= 64;
-}
-
-int tileGrid(int shader, const DScene& s, int maxThreads) {
-    const bool exact = s.cull == kCullExact;
-    if (shader == kShaderPathTracer)
-        return exact ? persistentGrid(k_tiles<kShaderPathTracer, kCullExact>, 14, maxThreads)
-                     : persistentGrid(k_tiles<kShaderPathTracer, kCullNone>, 15, maxThreads);
-    return exact ? persistentGrid(k_tiles<kShaderWhitted, kCullExact>, 16, maxThreads)
-                 : persistentGrid(k_tiles<kShaderWhitted, kCullNone>, 17, maxThreads);
-}
-
-void launchTiles(int shader, const DScene& s, const TileArgs& a, int grid, int2* gstack, int gdepth, hipStream_t st) {
-    const bool exact = s.cull == kCullExact;
-    if (shader == kShaderPathTracer) {
-        if (exact)
-            hipLaunchKernelGGL((k_tiles<kShaderPathTracer, kCullExact>), dim3(grid), dim3(kWalkThreads), 0, st, s, a, gstack, gdepth);
-        else
-            hipLaunchKernelGGL((k_tiles<kShaderPathTracer, kCullNone>), dim3(grid), dim3(kWalkThreads), 0, st, s, a, gstack, gdepth);
-    } else {
-        if (exact)
-            hipLaunchKernelGGL((k_tiles<kShaderWhitted, kCullExact>), dim3(grid), dim3(kWalkThreads), 0, st, s, a, gstack, gdepth);
-        else
-            hipLaunchKernelGGL((k_tiles<kShaderWhitted, kCullNone>), dim3(grid), dim3(kWalkThreads), 0, st, s, a, gstack, gdepth);
-    }
 }
 
 }  // namespace mrt

@@ -126,36 +126,6 @@ struct AccumArgs {
 };
 
 
-// ---- the tile kernel (k_tiles): every wave renders whole tiles of paths ----
-constexpr int kTileSlots = 8;                    // tiles in flight per wave
-constexpr int kTileLevels = 9;                   // levels counted per tile: maxDepth + 1 <= kTileLevels
-constexpr int kTileCnt = 2 * (kTileLevels + 1);  // a tile's cntRays / cntShadows counters (the global layout)
-struct TileArgs {
-    RaygenArgs ra;      // camera, pixel map, spp, sample base, pixel sampler (slotBase: the pass's first slot)
-    ShadeArgs sa;
-    AccumArgs aa;       // map, width, spp, sample base (slotBase set per tile)
-    int32_t* bitmap;
-    int32_t* packed;
-    char* arena;        // per wave (blockIdx.x * 4 + wave of the block): kTileSlots x slotBytes
-    long long slotBytes;
-    int cap1, capN;     // rays per tile at level 1 / at deeper levels (shadow rays: x samplesLight)
-    int spl;
-    int nTiles;         // tiles of the pass
-    int tilePixels;     // pixel slots per tile (64 / spp: a tile's camera rays are one 64-ray packet)
-    int nSlots;         // pixel slots of the pass
-    int maxNew;         // tiles a wave claims per round at most ...
-    int poolTarget;     // ... and only while its next closest-hit pool holds fewer rays than this
-    int* claim;         // kWalkShards tile cursors, kFetchStride ints apart
-    int* counters;      // the pass's counters (each wave adds its tiles' counts at exit), overflow flag
-};
-// bytes of one tile slot's records: level 1 (cap1 rays) and levels 2 .. maxDepth (capN rays each)
-inline long long tileSlotBytes(int cap1, int capN, int spl, int maxDepth) {
-    const auto lvl = [spl](long long cap) { return cap * 84 + cap * spl * 48; };
-    return lvl(cap1) + (maxDepth > 1 ? (maxDepth - 1) * lvl(capN) : 0);
-}
-bool canTile(int shader, const DScene& s, const ShadeArgs& a, int spp);
-void launchTiles(int shader, const DScene& s, const TileArgs& a, int grid, int2* gstack, int gdepth, hipStream_t st);
-int tileGrid(int shader, const DScene& s, int maxThreads);  // persistent grid of k_tiles
 
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -84,6 +85,25 @@ float asFloat(int32_t i) {
 
 }  // namespace
 
+// "0,1,2,3" (MOBILERT_DEVICES) -> {0, 1, 2, 3}; null or empty -> {}.  Throws on anything else.
+std::vector<int32_t> mrt::parseDeviceList(const char* s) {
+    std::vector<int32_t> out;
+    if (s == nullptr) return out;
+    std::string item;
+    std::istringstream in(s);
+    while (std::getline(in, item, ',')) {
+        size_t used = 0;
+        const int v = std::stoi(item, &used);
+        if (used != item.size() || v < 0) throw std::runtime_error(std::string("MOBILERT_DEVICES: bad ordinal '") + item + "'");
+        out.push_back(v);
+    }
+    return out;
+}
+
+namespace {
+
+}  // namespace
+
 struct mrt_renderer {
     mrt_config cfg{};
     std::string objPath, mtlPath, camPath;
@@ -148,16 +168,8 @@ struct mrt_renderer {
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
     bool fusedL1 = false;                // the last pass ran level 1 as k_trace_packet_shade
-    bool tilePass = false;               // the last pass ran the tile kernel (k_tiles)
-    bool tileOverflowed = false;         // a tile pass overflowed its per-tile queues: level kernels from then on
-    int tileGrowth = 2;                  // tile queue capacity per level: growth x 64 rays (tuning key 23)
-    int tileMaxNew = 2;                  // tiles a wave claims per round at most (tuning key 20)
-    int tilePoolTarget = 256;            // ... while its next walk pool has fewer rays (tuning key 21)
-    int tileRefill = 8;                  // the tile walks' refill threshold (tuning key 22)
     int lastShadowRender = 1;            // tuning key 27: the last shadow walk on the render stream
-    DeviceMem tileMem;                   // the tile kernel's per-wave arenas
-    size_t tileArenaBytes = 0;
-    char* tileArena = nullptr;
+    int walkGridCap = 0;                 // tuning key 28: at most this many workgroups per walk launch (0: none)
     unsigned long long* hostStats = nullptr;  // pinned: the per-pass statistics read back by DMA
 
     // host copies for the GL preview of the Android front end (mrt_preview_arrays; kept only for
@@ -172,6 +184,13 @@ struct mrt_renderer {
     std::atomic<uint64_t> totalRays{0};
     int profileFlags = 0;
     mrt_frame_stats last{};
+
+    // device group (mrt_config.devices): this renderer is shard 0 on devices[0] and the group's
+    // head; peers[i - 1] is shard i on devices[i].  Every shard renders into its own packed buffer
+    // (dOwnPacked, on its device); the head gathers them into dGathered and unpacks the frame.
+    std::vector<std::unique_ptr<mrt_renderer>> peers;
+    int32_t* dOwnPacked = nullptr;
+    int32_t* dGathered = nullptr;
 
     ~mrt_renderer() {
         if (hostStats != nullptr) (void)hipHostFree(hostStats);
@@ -648,64 +667,6 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     // every material is finite (Ks * 0 and Kd * 0 added to sums that start at +0), and the
     // parents write no payload for them (only their count)
     const bool skipLastShade = skipLast && nLevels >= 2 && r->ds.matsFinite != 0;
-    // The tile kernel (k_tiles: every wave renders whole tiles through their ray trees, no grid-wide
-    // barrier per level) where it applies: the whole pass in one launch.
-    r->tilePass = false;
-    if (skipLastShade && !r->tileOverflowed && canTile(shader, r->ds, sa, spp) && !r->stopFlag.load()) {
-        r->tilePass = true;
-        r->fusedL1 = false;
-        const int grid = tileGrid(shader, r->ds, r->traceThreads);
-        const int tilePixels = std::max(1, 64 / spp);
-        const int capN = 64 * r->tileGrowth;
-        const long long slotBytes = tileSlotBytes(64, capN, spl, r->maxDepth);
-        const size_t need = static_cast<size_t>(grid) * (kBlock / 64) * kTileSlots * static_cast<size_t>(slotBytes);
-        if (r->tileArenaBytes < need) {
-            r->tileMem.release();
-            r->tileArena = r->tileMem.alloc<char>(need);
-            r->tileArenaBytes = need;
-        }
-        MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
-        TileArgs ta{};
-        ta.ra.cam = r->cam;
-        ta.ra.map = map;
-        ta.ra.tables = r->ds.tables;
-        ta.ra.jitter = r->ds.jitterDraws;
-        ta.ra.width = r->cfg.width;
-        ta.ra.height = r->cfg.height;
-        ta.ra.slotBase = 0;
-        ta.ra.nPaths = r->nSlots * spp;
-        ta.ra.spp = spp;
-        ta.ra.sppTotal = r->cfg.samplesPixel;
-        setPixelSampler(r, &ta.ra);
-        ta.ra.sampleBase = sampleBase;
-        ta.sa = sa;
-        ta.aa.map = map;
-        ta.aa.width = r->cfg.width;
-        ta.aa.slotBase = 0;
-        ta.aa.nSlots = r->nSlots;
-        ta.aa.spp = spp;
-        ta.aa.sampleBase = sampleBase;
-        ta.bitmap = dBitmap;
-        ta.packed = dPacked;
-        ta.arena = r->tileArena;
-        ta.slotBytes = slotBytes;
-        ta.cap1 = 64;
-        ta.capN = capN;
-        ta.spl = spl;
-        ta.tilePixels = tilePixels;
-        ta.nSlots = r->nSlots;
-        ta.nTiles = (r->nSlots + tilePixels - 1) / tilePixels;
-        ta.maxNew = r->tileMaxNew;
-        ta.poolTarget = r->tilePoolTarget;
-        ta.claim = pp.counters + kCntFetchShards;  // level 0's cursors (the walks use levels >= 1)
-        ta.counters = pp.counters;
-        r->ds.refill = r->tileRefill;
-        if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-        launchTiles(shader, r->ds, ta, grid, pp.gstack, r->gdepth, st);
-        if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-        launchTally(pp.counters, nLevels, pp.stats, st, skipLast ? nLevels : 0);
-        return;
-    }
     for (int slot0 = 0; slot0 < r->nSlots && !r->stopFlag.load(); slot0 += r->chunkSlots) {
         const int nChunk = std::min(r->chunkSlots, r->nSlots - slot0);
         MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
@@ -733,6 +694,9 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // a narrower shadow grid leaves them room (C4 shard at N = 8: 2.92 -> 2.83 ms; at N = 1 the
         // full grid is 2.6 % faster).  Results do not depend on the grid.
         const double pathsPerLane = static_cast<double>(ra.nPaths) / std::max(1, r->traceThreads);
+        // the walk launches' thread cap (tuning key 28 narrows it; the spill stacks hold traceThreads)
+        const int walkThreads = r->walkGridCap > 0 ? std::min(r->traceThreads, r->walkGridCap * kBlock)
+                                                   : r->traceThreads;
         // (round 2, 4-wide walk tree: C4 shard at N = 8 60 / 50 % -> 2.55 / 2.50 ms; N = 1 100 / 80 /
         // 70 % with 28 shading workgroups per CU -> 13.48 / 13.34 / 13.34 ms).  With shadow rays on
         // the render stream (key 3 = 0) nothing runs beside the shadow walk: full grid.
@@ -772,12 +736,12 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             const bool fused = fuseL1 && l == 1;
             if (fused) {
                 launchTraceShadeFused(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, pp.gstack,
-                                      r->gdepth, r->traceThreads, st, skipLastShade && l + 1 == nLevels, ra);
+                                      r->gdepth, walkThreads, st, skipLastShade && l + 1 == nLevels, ra);
                 ++r->shadeLaunches;
             }
             if (!fused && !(skipLast && l == nLevels))
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting,
-                            r->traceThreads, st);
+                            walkThreads, st);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             if (!fused && !(skipLastShade && l == nLevels)) {
@@ -801,7 +765,7 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 // 13.34 -> 13.29 ms); a small one keeps the narrow grid (N = 8: 2.53 vs 2.55 ms)
                 const bool lastAlone = l + 1 == nLevels && r->shadowGridPct == 0 && pathsPerLane >= 8.0;
                 launchShadow(r->ds, pp.levels[l], pp.counters, l, onRender ? pp.gstack : pp.gstackShadow, r->gdepth,
-                             pp.stats, counting, r->traceThreads, ss, lastAlone ? 100 : shadowPct);
+                             pp.stats, counting, walkThreads, ss, lastAlone ? 100 : shadowPct);
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ss));
             if (sb != st && !onRender) {
@@ -841,10 +805,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     unsigned long long hs[kNumStats];
     std::memcpy(hs, r->hostStats, sizeof(hs));
     const auto t1 = std::chrono::steady_clock::now();
-    if (hs[kStatOverflow] != 0) {
-        if (r->tilePass) r->tileOverflowed = true;  // (the retry renders with the level kernels)
-        return false;
-    }
+    if (hs[kStatOverflow] != 0) return false;
     fs->rays += hs[kStatRays];
     fs->shadowRays += hs[kStatShadowRays];
     fs->walkedRays += hs[kStatRays] - hs[kStatSkipped];
@@ -871,12 +832,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
         fs->levelShadowRays[l] += hs[kStatLevelShadows + l];
     }
     fs->frameMs += std::chrono::duration<double, std::milli>(t1 - t0).count();
-    if ((r->profileFlags & 1) && r->tilePass) {
-        float ms = 0.0F;
-        MRT_HIP(hipEventElapsedTime(&ms, r->pipe.evPool[0], r->pipe.evPool[1]));
-        fs->tileMs += ms;
-        fs->tileLaunches += 1;
-    } else if (r->profileFlags & 1) {
+    if (r->profileFlags & 1) {
         const mrt_renderer::Pipe& pp = r->pipe;
         for (size_t e = 0; e + 4 < pp.evCount; e += 5) {
             float ta = 0.0F, tb = 0.0F, tc = 0.0F;
@@ -902,15 +858,80 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     return true;
 }
 
+// a += b for every statistic of a frame (the most node records of one ray: the larger)
+void addStats(mrt_frame_stats& a, const mrt_frame_stats& b) {
+    using namespace mrt;
+    a.rays += b.rays;
+    a.shadowRays += b.shadowRays;
+    a.walkedRays += b.walkedRays;
+    a.primaryRays += b.primaryRays;
+    a.nodeRecords += b.nodeRecords;
+    a.triTests += b.triTests;
+    a.shadowNodeRecords += b.shadowNodeRecords;
+    a.shadowTriTests += b.shadowTriTests;
+    a.leafRecords += b.leafRecords;
+    a.shadowOccluded += b.shadowOccluded;
+    for (int k = 0; k < 16; ++k) a.walkPhases[k] += b.walkPhases[k];
+    a.shadowLeafRecords += b.shadowLeafRecords;
+    a.fusedMs += b.fusedMs;
+    a.fusedLaunches += b.fusedLaunches;
+    a.maxNodeRecordsPerRay = std::max(a.maxNodeRecordsPerRay, b.maxNodeRecordsPerRay);
+    a.shadedVertices += b.shadedVertices;
+    a.shadeLaunches += b.shadeLaunches;
+    a.traceMs += b.traceMs;
+    a.shadowMs += b.shadowMs;
+    a.shadeMs += b.shadeMs;
+    a.frameMs += b.frameMs;
+    a.traceLaunches += b.traceLaunches;
+    a.shadowLaunches += b.shadowLaunches;
+    for (int l = 0; l < kMaxLevels && l < 16; ++l) {
+        a.levelRays[l] += b.levelRays[l];
+        a.levelShadowRays[l] += b.levelShadowRays[l];
+        a.levelTraceMs[l] += b.levelTraceMs[l];
+        a.levelShadowMs[l] += b.levelShadowMs[l];
+        a.levelNodeRecords[l] += b.levelNodeRecords[l];
+        a.levelTriTests[l] += b.levelTriTests[l];
+        a.levelLeafRecords[l] += b.levelLeafRecords[l];
+        a.levelShadedVertices[l] += b.levelShadedVertices[l];
+    }
+}
+
+// Progressive mode: sample smp's pass, its statistics added to *fs.  The running average is read
+// by the pass: a copy is kept to redo a pass whose queues overflowed (in smaller chunks).
+void renderProgressiveSample(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st, int smp,
+                             mrt_frame_stats* fs) {
+    const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
+    int32_t* acc = dBitmap != nullptr ? dBitmap : dPacked;
+    const size_t accN = dBitmap != nullptr ? npx : static_cast<size_t>(r->nSlots);
+    if (r->dBackup == nullptr || r->backupN < accN) {
+        r->dBackup = r->frameMem.alloc<int32_t>(accN);
+        r->backupN = accN;
+    }
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        if (acc != nullptr) MRT_HIP(hipMemcpyAsync(r->dBackup, acc, accN * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+        mrt_frame_stats pass{};
+        if (runPass(r, dBitmap, dPacked, st, smp, 1, &pass)) {
+            addStats(*fs, pass);
+            return;
+        }
+        if (acc != nullptr) MRT_HIP(hipMemcpyAsync(acc, r->dBackup, accN * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+        allocQueues(r, std::max(1, r->chunkSlots / 2), 2);
+    }
+    throw std::runtime_error("wavefront queue overflow persists after shrinking the chunk");
+}
+
 // Renderer::renderFrame (Renderer.cpp:53-88): samples 0..spp-1 averaged with incrementalAvg.
 // Default: every sample of the frame in flight at once (one wavefront pass per chunk).
 // cfg.progressive: one pass per sample, the bitmap (and hostBitmap, if given) updated and
 // getSample() advanced after each, stopRender() honoured between samples - the reference's
 // progressive contract for the Qt / Android front ends.  Both give the same final bitmap.
-void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st,
+// One renderer (one GPU, or one shard of a device group).
+void renderFrameSingle(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st,
                        int32_t* hostBitmap = nullptr) {
     using namespace mrt;
-    r->sample.store(0);
+    // (a device group's head is its shard 0 too: the group keeps getSample() itself)
+    const bool groupHead = !r->peers.empty();
+    if (!groupHead) r->sample.store(0);
     if (r->stopFlag.load()) return;  // stopRender zeroes samplesPixel_ (Renderer.cpp:97)
     const int spp = std::max(1, r->cfg.samplesPixel);
     const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
@@ -927,77 +948,151 @@ void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipS
             MRT_HIP(hipMemcpyAsync(hostBitmap, dBitmap, npx * sizeof(int32_t), hipMemcpyDeviceToHost, st));
             MRT_HIP(hipStreamSynchronize(st));
         }
-        if (!r->stopFlag.load()) r->sample.store(r->cfg.samplesPixel);
+        if (!r->stopFlag.load() && !groupHead) r->sample.store(r->cfg.samplesPixel);
     } else {
-        // the running average is read by the next pass: keep a copy to redo an overflowed pass
-        int32_t* acc = dBitmap != nullptr ? dBitmap : dPacked;
-        const size_t accN = dBitmap != nullptr ? npx : static_cast<size_t>(r->nSlots);
-        if (r->dBackup == nullptr || r->backupN < accN) {
-            r->dBackup = r->frameMem.alloc<int32_t>(accN);
-            r->backupN = accN;
-        }
         for (int smp = 0; smp < spp && !r->stopFlag.load(); ++smp) {
-            bool done = false;
-            for (int attempt = 0; attempt < 4 && !done; ++attempt) {
-                if (acc != nullptr) MRT_HIP(hipMemcpyAsync(r->dBackup, acc, accN * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
-                mrt_frame_stats pass{};
-                done = runPass(r, dBitmap, dPacked, st, smp, 1, &pass);
-                if (done) {
-                    const mrt_frame_stats prev = fs;
-                    fs = pass;
-                    fs.rays += prev.rays;
-                    fs.shadowRays += prev.shadowRays;
-                    fs.walkedRays += prev.walkedRays;
-                    fs.primaryRays += prev.primaryRays;
-                    fs.nodeRecords += prev.nodeRecords;
-                    fs.triTests += prev.triTests;
-                    fs.shadowNodeRecords += prev.shadowNodeRecords;
-                    fs.shadowTriTests += prev.shadowTriTests;
-                    fs.leafRecords += prev.leafRecords;
-                    fs.shadowOccluded += prev.shadowOccluded;
-                    for (int k = 0; k < 16; ++k) fs.walkPhases[k] += prev.walkPhases[k];
-                    fs.shadowLeafRecords += prev.shadowLeafRecords;
-                    fs.fusedMs += prev.fusedMs;
-                    fs.tileMs += prev.tileMs;
-                    fs.tileLaunches += prev.tileLaunches;
-                    fs.fusedLaunches += prev.fusedLaunches;
-                    fs.maxNodeRecordsPerRay = std::max(fs.maxNodeRecordsPerRay, prev.maxNodeRecordsPerRay);
-                    fs.shadedVertices += prev.shadedVertices;
-                    fs.shadeLaunches += prev.shadeLaunches;
-                    fs.traceMs += prev.traceMs;
-                    fs.shadowMs += prev.shadowMs;
-                    fs.shadeMs += prev.shadeMs;
-                    fs.frameMs += prev.frameMs;
-                    fs.traceLaunches += prev.traceLaunches;
-                    fs.shadowLaunches += prev.shadowLaunches;
-                    for (int l = 0; l < kMaxLevels; ++l) {
-                        fs.levelRays[l] += prev.levelRays[l];
-                        fs.levelShadowRays[l] += prev.levelShadowRays[l];
-                        fs.levelTraceMs[l] += prev.levelTraceMs[l];
-                        fs.levelShadowMs[l] += prev.levelShadowMs[l];
-                        if (l < 16) {
-                            fs.levelNodeRecords[l] += prev.levelNodeRecords[l];
-                            fs.levelTriTests[l] += prev.levelTriTests[l];
-                            fs.levelLeafRecords[l] += prev.levelLeafRecords[l];
-                            fs.levelShadedVertices[l] += prev.levelShadedVertices[l];
-                        }
-                    }
-                } else {
-                    if (acc != nullptr)
-                        MRT_HIP(hipMemcpyAsync(acc, r->dBackup, accN * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
-                    allocQueues(r, std::max(1, r->chunkSlots / 2), 2);
-                }
-            }
-            if (!done) throw std::runtime_error("wavefront queue overflow persists after shrinking the chunk");
+            renderProgressiveSample(r, dBitmap, dPacked, st, smp, &fs);
             if (hostBitmap != nullptr && dBitmap != nullptr) {
                 MRT_HIP(hipMemcpyAsync(hostBitmap, dBitmap, npx * sizeof(int32_t), hipMemcpyDeviceToHost, st));
                 MRT_HIP(hipStreamSynchronize(st));
             }
-            r->sample.store(smp + 1);  // Renderer.cpp:82-86
+            if (!groupHead) r->sample.store(smp + 1);  // Renderer.cpp:82-86
         }
     }
     r->last = fs;
     r->totalRays.fetch_add(fs.rays + fs.shadowRays);
+}
+
+// The frame's assembly from rankCount packed shards (d_gathered: rankCount slices of maxSlots
+// entries): one k_unpack_ranks launch per kUnpackRanks shards (a launch per shard cost ~8 us each
+// at N = 8).
+void unpackGathered(const mrt_renderer* r, const int32_t* dGathered, int32_t* dBitmap, hipStream_t st) {
+    for (int k0 = 0; k0 < r->rankCount; k0 += mrt::kUnpackRanks) {
+        mrt::UnpackArgs a{};
+        a.width = r->cfg.width;
+        a.first = k0;
+        a.stride = r->maxSlots;
+        const int ranks = std::min(mrt::kUnpackRanks, r->rankCount - k0);
+        int maxN = 0;
+        for (int j = 0; j < ranks; ++j) {
+            const auto k = static_cast<size_t>(k0 + j);
+            const auto& pre = r->prefixByRank[k];
+            const auto& un = r->unitsByRank[k];
+            a.maps[j] = r->mapByRank[k];
+            a.n[j] = un.empty() ? 0 : pre.back() + un.back().z * un.back().w;
+            maxN = std::max(maxN, a.n[j]);
+        }
+        mrt::launchUnpackRanks(a, ranks, maxN, dGathered, dBitmap, st);
+    }
+}
+
+// ---- device groups (mrt_config.devices) ------------------------------------------------------
+// Renderer::renderFrame hands the frame's tiles to its worker threads (Renderer.cpp:62-82); a
+// device group hands its screen-tile shards to its GPUs, one host thread per shard.
+
+mrt_renderer* shardOf(mrt_renderer* r, int i) { return i == 0 ? r : r->peers[static_cast<size_t>(i - 1)].get(); }
+int groupSize(const mrt_renderer* r) { return 1 + static_cast<int>(r->peers.size()); }
+
+// f(shard, i) for every shard of the group, shard i from a host thread with its device current
+// (shard 0 in the calling thread); the first failure is rethrown after all have finished
+template <class F>
+void forEachShard(mrt_renderer* r, F&& f) {
+    const int n = groupSize(r);
+    std::vector<std::exception_ptr> err(static_cast<size_t>(n));
+    std::vector<std::thread> th;
+    for (int i = 1; i < n; ++i)
+        th.emplace_back([&, i] {
+            try {
+                mrt_renderer* p = shardOf(r, i);
+                MRT_HIP(hipSetDevice(p->device));
+                f(p, i);
+            } catch (...) {
+                err[static_cast<size_t>(i)] = std::current_exception();
+            }
+        });
+    try {
+        MRT_HIP(hipSetDevice(r->device));
+        f(r, 0);
+    } catch (...) {
+        err[0] = std::current_exception();
+    }
+    for (std::thread& t : th) t.join();
+    for (const std::exception_ptr& e : err)
+        if (e) std::rethrow_exception(e);
+}
+
+// The shards' packed pixels into the head's gather buffer (peer copies over xGMI; a shard on the
+// head's own GPU: a device-to-device copy), then the frame from them, on the head's stream st.
+// Every shard's render has completed (its passes end with a stream synchronisation).
+void assembleGroup(mrt_renderer* r, int32_t* dBitmap, hipStream_t st) {
+    if (dBitmap == nullptr) return;
+    for (int i = 0; i < groupSize(r); ++i) {
+        const mrt_renderer* p = shardOf(r, i);
+        int32_t* dst = r->dGathered + static_cast<size_t>(i) * static_cast<size_t>(r->maxSlots);
+        const size_t bytes = sizeof(int32_t) * static_cast<size_t>(p->nSlots);
+        if (bytes == 0) continue;
+        if (p->device == r->device)
+            MRT_HIP(hipMemcpyAsync(dst, p->dOwnPacked, bytes, hipMemcpyDeviceToDevice, st));
+        else
+            MRT_HIP(hipMemcpyPeerAsync(dst, r->device, p->dOwnPacked, p->device, bytes, st));
+    }
+    unpackGathered(r, r->dGathered, dBitmap, st);
+}
+
+// One frame of a device group into dBitmap (on the head's device; may be null) and, if given, the
+// host bitmap.  getSample() and stopRender() keep their meaning for the whole group: the sample
+// count advances once every shard has it, a stop reaches every shard (mrt_stop_render).
+void renderGroupFrame(mrt_renderer* r, int32_t* dBitmap, hipStream_t st, int32_t* hostBitmap) {
+    r->sample.store(0);
+    if (r->stopFlag.load()) return;
+    const int n = groupSize(r);
+    const int spp = std::max(1, r->cfg.samplesPixel);
+    const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
+    const uint64_t rays0 = r->totalRays.load();
+    std::vector<mrt_frame_stats> shardStats(static_cast<size_t>(n));
+    auto toHost = [&] {
+        if (hostBitmap == nullptr || dBitmap == nullptr) return;
+        MRT_HIP(hipMemcpyAsync(hostBitmap, dBitmap, npx * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        MRT_HIP(hipStreamSynchronize(st));
+    };
+    if (r->cfg.progressive == 0) {
+        forEachShard(r, [&](mrt_renderer* p, int i) {
+            renderFrameSingle(p, nullptr, p->dOwnPacked, p->stream);
+            shardStats[static_cast<size_t>(i)] = p->last;
+        });
+        assembleGroup(r, dBitmap, st);
+        toHost();
+        if (!r->stopFlag.load()) r->sample.store(r->cfg.samplesPixel);
+    } else {
+        for (int smp = 0; smp < spp && !r->stopFlag.load(); ++smp) {
+            forEachShard(r, [&](mrt_renderer* p, int i) {
+                renderProgressiveSample(p, nullptr, p->dOwnPacked, p->stream, smp, &shardStats[static_cast<size_t>(i)]);
+            });
+            assembleGroup(r, dBitmap, st);
+            toHost();
+            r->sample.store(smp + 1);  // Renderer.cpp:82-86
+        }
+        for (int i = 1; i < n; ++i) shardOf(r, i)->last = shardStats[static_cast<size_t>(i)];
+    }
+    mrt_frame_stats fs{};
+    for (const mrt_frame_stats& x : shardStats) addStats(fs, x);
+    r->last = fs;
+    r->totalRays.store(rays0 + fs.rays + fs.shadowRays);
+}
+
+void renderFrameDevice(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st,
+                       int32_t* hostBitmap = nullptr) {
+    if (r->peers.empty()) {
+        renderFrameSingle(r, dBitmap, dPacked, st, hostBitmap);
+        return;
+    }
+    if (dPacked != nullptr) throw std::runtime_error("a device group assembles its frame itself: no packed output");
+    renderGroupFrame(r, dBitmap, st, hostBitmap);
+}
+
+void stopAll(mrt_renderer* r) {
+    r->stopFlag.store(true);
+    for (auto& p : r->peers) p->stopFlag.store(true);
 }
 
 // An OBJ scene handed over as text (the Android front end reads the files through descriptors,
@@ -1007,8 +1102,11 @@ struct MemScene {
     std::map<std::string, std::string> textures;
 };
 
+mrt_renderer* createGroup(const mrt_config* cfg, const MemScene* mem);
+
 mrt_renderer* createRenderer(const mrt_config* cfg, const MemScene* mem = nullptr) {
     using namespace mrt;
+    if (cfg->deviceCount > 1) return createGroup(cfg, mem);
     auto r = std::make_unique<mrt_renderer>();
     r->keepHost = mem != nullptr;
     r->cfg = *cfg;
@@ -1073,6 +1171,58 @@ mrt_renderer* createRenderer(const mrt_config* cfg, const MemScene* mem = nullpt
     MRT_HIP(hipMemsetAsync(r->dBitmap, 0, sizeof(int32_t) * npx, r->stream));
     MRT_HIP(hipStreamSynchronize(r->stream));
     return r.release();
+}
+
+// A device group (mrt_config.devices): one renderer per shard, created concurrently (each parses
+// and uploads the scene on its own GPU), shard 0 the head.  The head enables peer access to the
+// other GPUs where the platform allows it (xGMI); hipMemcpyPeerAsync works either way.
+mrt_renderer* createGroup(const mrt_config* cfg, const MemScene* mem) {
+    const int n = cfg->deviceCount;
+    if (cfg->devices == nullptr) throw std::runtime_error("deviceCount > 1 needs the devices array");
+    if (cfg->rankCount > 1 || cfg->rankIndex != 0)
+        throw std::runtime_error("a device group shards the frame itself: leave rankIndex / rankCount at 0 / 1");
+    int visible = 0;
+    MRT_HIP(hipGetDeviceCount(&visible));
+    for (int i = 0; i < n; ++i)
+        if (cfg->devices[i] < 0 || cfg->devices[i] >= visible)
+            throw std::runtime_error("device group: ordinal " + std::to_string(cfg->devices[i]) + " not among the " +
+                                     std::to_string(visible) + " visible GPUs");
+    std::vector<std::unique_ptr<mrt_renderer>> shards(static_cast<size_t>(n));
+    std::vector<std::exception_ptr> err(static_cast<size_t>(n));
+    std::vector<std::thread> th;
+    for (int i = 0; i < n; ++i)
+        th.emplace_back([&, i] {
+            try {
+                mrt_config c = *cfg;
+                c.devices = nullptr;
+                c.deviceCount = 0;
+                c.device = cfg->devices[i];
+                c.rankIndex = i;
+                c.rankCount = n;
+                shards[static_cast<size_t>(i)].reset(createRenderer(&c, mem));
+                mrt_renderer* p = shards[static_cast<size_t>(i)].get();
+                p->dOwnPacked = p->frameMem.alloc<int32_t>(static_cast<size_t>(std::max(1, p->nSlots)));
+            } catch (...) {
+                err[static_cast<size_t>(i)] = std::current_exception();
+            }
+        });
+    for (std::thread& t : th) t.join();
+    for (const std::exception_ptr& e : err)
+        if (e) std::rethrow_exception(e);
+    std::unique_ptr<mrt_renderer> head = std::move(shards[0]);
+    MRT_HIP(hipSetDevice(head->device));
+    head->dGathered = head->frameMem.alloc<int32_t>(static_cast<size_t>(n) * static_cast<size_t>(std::max(1, head->maxSlots)));
+    for (int i = 1; i < n; ++i) {
+        const int d = cfg->devices[i];
+        int can = 0;
+        if (d != head->device && hipDeviceCanAccessPeer(&can, head->device, d) == hipSuccess && can) {
+            const hipError_t e = hipDeviceEnablePeerAccess(d, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) MRT_HIP(e);
+            (void)hipGetLastError();
+        }
+        head->peers.push_back(std::move(shards[static_cast<size_t>(i)]));
+    }
+    return head.release();
 }
 
 template <class F>
@@ -1179,6 +1329,7 @@ int64_t mrt_preview_arrays(const mrt_renderer* r, float* vertices, float* colors
 void mrt_destroy(mrt_renderer* r) {
     if (r != nullptr) {
         (void)hipStreamSynchronize(r->stream);
+        for (auto& p : r->peers) (void)hipStreamSynchronize(p->stream);
         delete r;
     }
 }
@@ -1213,29 +1364,12 @@ int mrt_render_frame_device(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked,
 int mrt_unpack_gathered(mrt_renderer* r, const int32_t* dGathered, int32_t* dBitmap, void* stream) {
     return guarded([&] {
         hipStream_t st = stream != nullptr ? static_cast<hipStream_t>(stream) : r->stream;
-        // one launch per kUnpackRanks shards (a launch per shard cost ~8 us each at N = 8)
-        for (int k0 = 0; k0 < r->rankCount; k0 += mrt::kUnpackRanks) {
-            mrt::UnpackArgs a{};
-            a.width = r->cfg.width;
-            a.first = k0;
-            a.stride = r->maxSlots;
-            const int ranks = std::min(mrt::kUnpackRanks, r->rankCount - k0);
-            int maxN = 0;
-            for (int j = 0; j < ranks; ++j) {
-                const auto k = static_cast<size_t>(k0 + j);
-                const auto& pre = r->prefixByRank[k];
-                const auto& un = r->unitsByRank[k];
-                a.maps[j] = r->mapByRank[k];
-                a.n[j] = un.empty() ? 0 : pre.back() + un.back().z * un.back().w;
-                maxN = std::max(maxN, a.n[j]);
-            }
-            mrt::launchUnpackRanks(a, ranks, maxN, dGathered, dBitmap, st);
-        }
+        unpackGathered(r, dGathered, dBitmap, st);
     });
 }
 
 int mrt_stop_render(mrt_renderer* r) {
-    r->stopFlag.store(true);
+    stopAll(r);
     return 0;
 }
 
@@ -1254,9 +1388,14 @@ int mrt_get_scene_info(const mrt_renderer* r, mrt_scene_info* info) {
     info->pixelSlots = r->nSlots;
     info->pixelSlotsMax = r->maxSlots;
     info->deviceBytes = static_cast<int64_t>(r->sceneMem.total + r->queueMem.total + r->frameMem.total);
-    info->deviceBytes += static_cast<int64_t>(r->tileMem.total);
     info->shadowStreamConcurrent = r->shadowConcurrent;
     info->shadowStreamsTried = r->shadowTries;
+    info->deviceCount = groupSize(r);
+    for (const auto& p : r->peers) {  // a device group: the whole frame's slots, every GPU's memory
+        info->pixelSlots += p->nSlots;
+        info->deviceBytes += static_cast<int64_t>(p->sceneMem.total + p->queueMem.total + p->frameMem.total);
+        info->shadowStreamConcurrent = std::min<int64_t>(info->shadowStreamConcurrent, p->shadowConcurrent);
+    }
     return 0;
 }
 
@@ -1271,13 +1410,15 @@ int mrt_set_camera(mrt_renderer* r, int32_t kind, const float* position, const f
                 throw std::runtime_error("mrt_set_camera: non-finite position / lookAt / up");
         const mrt::v3 p{position[0], position[1], position[2]}, l{lookAt[0], lookAt[1], lookAt[2]},
             u{up[0], up[1], up[2]};
+        mrt::GCamera cam;
         if (kind == 0) {
-            r->cam = mrt::makePerspective(p, l, u, a, b);
+            cam = mrt::makePerspective(p, l, u, a, b);
         } else if (kind == 1) {
-            r->cam = mrt::makeOrthographic(p, l, u, a, b);
+            cam = mrt::makeOrthographic(p, l, u, a, b);
         } else {
             throw std::runtime_error("camera kind: 0 perspective, 1 orthographic");
         }
+        for (int i = 0; i < groupSize(r); ++i) shardOf(r, i)->cam = cam;
     });
 }
 
@@ -1290,20 +1431,22 @@ int mrt_set_pixel_sampler(mrt_renderer* r, int32_t kind, float value) {
         gLastError = "pixel sampler: -1 by samplesPixel, 0 Constant, 1 StaticHaltonSeq";
         return -1;
     }
-    r->pixelSampler = kind;
-    r->pixelConst = value;
+    for (int i = 0; i < groupSize(r); ++i) {
+        shardOf(r, i)->pixelSampler = kind;
+        shardOf(r, i)->pixelConst = value;
+    }
     return 0;
 }
 
 int mrt_set_max_point(mrt_renderer* r, const float* maxPoint) {
     return guarded([&] {
         if (r == nullptr || maxPoint == nullptr) throw std::runtime_error("mrt_set_max_point: null argument");
-        r->maxPoint = mrt::v3{maxPoint[0], maxPoint[1], maxPoint[2]};
+        for (int i = 0; i < groupSize(r); ++i) shardOf(r, i)->maxPoint = mrt::v3{maxPoint[0], maxPoint[1], maxPoint[2]};
     });
 }
 
 int mrt_set_profiling(mrt_renderer* r, int32_t flags) {
-    r->profileFlags = flags;
+    for (int i = 0; i < groupSize(r); ++i) shardOf(r, i)->profileFlags = flags;
     return 0;
 }
 
@@ -1321,7 +1464,17 @@ int64_t mrt_wave_log(mrt_renderer* r, uint64_t* out) {
     return rc == 0 ? n : -1;
 }
 
+static int setTuningOne(mrt_renderer* r, int32_t key, int32_t value);
+
 int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
+    for (int i = 0; i < groupSize(r); ++i) {  // every shard of a device group alike
+        const int rc = setTuningOne(shardOf(r, i), key, value);
+        if (rc != 0) return rc;
+    }
+    return 0;
+}
+
+static int setTuningOne(mrt_renderer* r, int32_t key, int32_t value) {
     if (key == 1 && value >= 0 && value < mrt::kTraceVariants) {
         r->ds.variant = value;
         return 0;
@@ -1370,29 +1523,12 @@ int mrt_set_tuning(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.fuseShade = value;
         return 0;
     }
-    if (key == 19 && (value == 0 || value == 1)) {
-        r->ds.tiles = value;
-        if (value == 1) r->tileOverflowed = false;
-        return 0;
-    }
-    if (key == 20 && value >= 1 && value <= mrt::kTileSlots) {
-        r->tileMaxNew = value;
-        return 0;
-    }
-    if (key == 21 && value >= 0 && value <= 4096) {
-        r->tilePoolTarget = value;
-        return 0;
-    }
-    if (key == 22 && value >= 1 && value <= 64) {
-        r->tileRefill = value;
-        return 0;
-    }
-    if (key == 23 && value >= 1 && value <= 8) {
-        r->tileGrowth = value;
-        return 0;
-    }
     if (key == 27 && (value == 0 || value == 1)) {
         r->lastShadowRender = value;
+        return 0;
+    }
+    if (key == 28 && value >= 0 && value <= 65536) {
+        r->walkGridCap = value;
         return 0;
     }
     if (key == 6 && value >= 0 && value <= 100) {
@@ -1564,12 +1700,8 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 11: *value = r->shadeGridPerCU; return 0;
         case 16: *value = r->ds.packet; return 0;
         case 17: *value = r->ds.fuseShade; return 0;
-        case 19: *value = r->ds.tiles; return 0;
-        case 20: *value = r->tileMaxNew; return 0;
-        case 21: *value = r->tilePoolTarget; return 0;
-        case 22: *value = r->tileRefill; return 0;
-        case 23: *value = r->tileGrowth; return 0;
         case 27: *value = r->lastShadowRender; return 0;
+        case 28: *value = r->walkGridCap; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";
@@ -1581,16 +1713,30 @@ int mrt_get_frame_stats(const mrt_renderer* r, mrt_frame_stats* s) {
     return 0;
 }
 
+static void primaryHitsOne(mrt_renderer* r, int32_t* kind, int32_t* index, float* t);
+
 int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
     return guarded([&] {
-        using namespace mrt;
-        hipStream_t st = r->stream;
         const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
         for (size_t i = 0; i < npx; ++i) {
             kind[i] = -1;
             index[i] = -1;
             t[i] = 0.0F;
         }
+        for (int i = 0; i < groupSize(r); ++i) {  // a device group: every shard's pixels
+            mrt_renderer* p = shardOf(r, i);
+            MRT_HIP(hipSetDevice(p->device));
+            primaryHitsOne(p, kind, index, t);
+        }
+        MRT_HIP(hipSetDevice(r->device));
+    });
+}
+
+// the camera rays' first hits of this renderer's own pixels
+static void primaryHitsOne(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
+    {
+        using namespace mrt;
+        hipStream_t st = r->stream;
         const auto& units = r->unitsByRank[static_cast<size_t>(r->rankIndex)];
         const auto& prefix = r->prefixByRank[static_cast<size_t>(r->rankIndex)];
         mrt_renderer::Pipe& pp = r->pipe;
@@ -1649,7 +1795,7 @@ int mrt_primary_hits(mrt_renderer* r, int32_t* kind, int32_t* index, float* t) {
         (void)hipFree(dk);
         (void)hipFree(di);
         (void)hipFree(dt);
-    });
+    }
 }
 
 }  // extern "C"
@@ -1794,6 +1940,13 @@ void workThread(::MobileRT::Config& config) {
         const char* dev = std::getenv("MOBILERT_DEVICE");
         c.device = dev != nullptr ? std::atoi(dev) : -1;
         c.rankCount = 1;
+        // MOBILERT_DEVICES=0,1,...: the frame sharded over these GPUs (a device group)
+        const std::vector<int32_t> devices = mrt::parseDeviceList(std::getenv("MOBILERT_DEVICES"));
+        if (devices.size() > 1) {
+            c.devices = devices.data();
+            c.deviceCount = static_cast<int32_t>(devices.size());
+            c.device = -1;
+        }
         c.cull = 3;  // exact for every input
         c.progressive = 1;  // the UI polls config.bitmap while the frame renders
         const auto tc0 = std::chrono::steady_clock::now();
@@ -1845,5 +1998,5 @@ extern "C" void RayTrace(::MobileRT::Config& config, bool async) {
 
 extern "C" void stopRender() {
     std::lock_guard<std::mutex> lock(gRendererMutex);
-    if (gRenderer != nullptr) gRenderer->stopFlag.store(true);
+    if (gRenderer != nullptr) stopAll(gRenderer);
 }

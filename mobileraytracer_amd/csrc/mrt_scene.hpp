@@ -196,4 +196,7 @@ void fillHemisphereTrig(const std::vector<float>& shaderTable, std::vector<float
 constexpr uint32_t kSeedShaderTable = 0x4D525400u;   // Shader.cpp:23,37
 constexpr uint32_t kSeedSamplerTable = 0x4D525401u;  // StaticHaltonSeq.cpp:7-22
 
+// MOBILERT_DEVICES ("0,1,2,3") -> the device group's ordinals (mrt_config.devices); null -> {}
+std::vector<int32_t> parseDeviceList(const char* s);
+
 }  // namespace mrt

@@ -84,12 +84,12 @@ struct NoRays {
 #if MRT_PACKET_SEGMENTS
 // the level queue's packets over kWalkShards cursors (kFetchStride ints apart; each serving its
 // interleaved chunks, mrt_trace_ww.hpp), a workgroup starting on its XCD group's cursor (blockIdx %
-// 8) and trying MRT_WALK_SEGMENTS of them: the exhausted-queue polls spread over 8 addresses
+// 8) and trying walkSegments() of them: the exhausted-queue polls spread over 8 addresses
 struct PacketFetch {
     int* fetch;
     int count;
     int seg = static_cast<int>(blockIdx.x % kWalkShards);
-    int segsLeft = MRT_WALK_SEGMENTS;
+    int segsLeft = walkSegments();
     __device__ __forceinline__ int next() {
         const int packets = (count + 63) >> 6;
         while (segsLeft > 0) {

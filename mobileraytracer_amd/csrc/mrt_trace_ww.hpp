@@ -45,6 +45,12 @@ constexpr int kWalkShards = 8;        // work cursors per level (one per XCD gro
 #ifndef MRT_WALK_SEGMENTS
 #define MRT_WALK_SEGMENTS 2
 #endif
+// Cursors a workgroup tries: MRT_WALK_SEGMENTS when the grid covers every cursor's starting group
+// (>= kWalkShards workgroups, the persistent grids' normal case), else all of them, so that every
+// ray is walked whatever the grid size (a small shadow-grid percentage, a partition with few CUs).
+__device__ __forceinline__ int walkSegments() {
+    return gridDim.x >= static_cast<unsigned>(kWalkShards) ? MRT_WALK_SEGMENTS : kWalkShards;
+}
 constexpr int kWalkStack = kLdsStackMin;  // LDS stack entries per thread (deeper ones spill)
 constexpr int kWalkTop = kTopNodesMax;
 // The while-while walk's inner phase ends when fewer than this many lanes still look for a leaf
@@ -479,7 +485,7 @@ struct LevelQueue {
     int count;
     int* fetch;
     int seg = static_cast<int>(blockIdx.x % kWalkShards);  // wave-uniform cursor state
-    int segsLeft = MRT_WALK_SEGMENTS;
+    int segsLeft = walkSegments();
     int shift;  // the cursors' chunks: 2^shift rays
     __device__ __forceinline__ LevelQueue(const float4* o_, const float4* d_, float4* out_, int count_, int* fetch_)
         : rO(o_), rD(d_), out(out_), count(count_), fetch(fetch_), shift(segChunkShift(count_, kSegChunkLog)) {}

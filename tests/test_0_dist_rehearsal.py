@@ -1,6 +1,6 @@
 """Multi-rank rehearsal of bench.py's distributed path.
 
-bench.py under torch.distributed.run with 2 ranks on the one GPU of a test box: the gloo
+bench.py under torch.distributed.run, and `bench.py --gpus 2` spawning its own ranks, with 2 ranks on the one GPU of a test box: the gloo
 backend (MRT_BENCH_BACKEND=gloo: the gather goes through host memory; the measured multi-GPU path
 is RCCL with one GPU per rank), each rank renders its screen-tile shard into a packed buffer,
 rank 0 gathers and unpacks.  Rank 0's assembled bitmap must equal the single-GPU bench's and the
@@ -28,12 +28,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _bench(tmp, name, nproc):
+def _bench(tmp, name, nproc, launcher=True):
     out = os.path.join(tmp, name + ".npy")
     args = ["bench.py", "--gpus", str(nproc), "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
             "--width", str(W), "--height", str(H), "--spp", str(SPP), "--dump-bitmap", out]
     env = dict(os.environ, MRT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    if nproc > 1:
+    if nproc > 1 and launcher:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
     else:
@@ -60,3 +60,8 @@ def test_two_rank_bench_assembles_the_single_gpu_frame(tmp_path, oracle_mod):
     o.render(ref, threads=min(16, os.cpu_count() or 1))
     o.close()
     assert np.array_equal(two, ref), int((two != ref).sum())
+    # the driver's form: `python bench.py --gpus 2` with no launcher spawns its own 2 ranks
+    spawned, line_s = _bench(str(tmp_path), "spawned", 2, launcher=False)
+    js = json.loads(line_s)
+    assert js["n_gpus"] == 2 and "gloo gather" in js["config"]["parallelism"]
+    assert np.array_equal(spawned, one), int((spawned != one).sum())

@@ -485,11 +485,11 @@ def test_python_plugin_setters():
 
 
 def test_removed_tuning_keys_are_rejected():
-    """Binned emission (key 4), queue sorting (12-14) and graph replay (15) measured slower and
-    were removed from the product: their keys are unknown."""
+    """Binned emission (key 4), queue sorting (12-14), graph replay (15) and the tile kernel (19-23)
+    measured slower and were removed from the product: their keys are unknown."""
     import mobileraytracer_amd as m
     with m.Renderer(make_cfg(32, 32)) as r:
-        for key in (4, 12, 13, 14, 15):
+        for key in (4, 12, 13, 14, 15, 19, 20, 21, 22, 23):
             with pytest.raises(Exception):
                 r.set_tuning(key, 1)
 
@@ -531,17 +531,20 @@ def test_tail_donation_matches_oracle_and_is_invariant(oracle_mod):
 def test_walk_knobs_are_invariant_and_wave_log_is_consistent():
     """The shadow walk's grid size (tuning key 6), the walk's refill threshold (key 9), k_shade's
     lean or general instantiation (key 10) and its grid (key 11) change only scheduling: same
-    bitmap and ray counts.  In counting mode the wave log holds one entry per
+    bitmap and ray counts.  So do walk grids smaller than the 8 work cursors (key 28: 1, 3, 7
+    workgroups), where each workgroup must try every cursor.  In counting mode the wave log holds one entry per
     resident wave of every walk launch, and its rays add up to the frame's walked rays."""
     import mobileraytracer_amd as m
     cfg = make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5)
     outs = []
     with m.Renderer(cfg) as r:
-        for key, val in ((6, 0), (6, 40), (6, 100), (9, 1), (9, 64), (10, 0), (11, 3), (11, 14), (11, 28)):
+        for key, val in ((6, 0), (6, 1), (6, 40), (6, 100), (9, 1), (9, 64), (10, 0), (11, 3), (11, 14), (11, 28),
+                         (28, 1), (28, 3), (28, 7), (28, 9)):
             r.set_tuning(6, 0)
             r.set_tuning(9, 32)
             r.set_tuning(10, 1)
             r.set_tuning(11, -1)
+            r.set_tuning(28, 0)
             r.set_tuning(key, val)
             assert r.get_tuning(key) == val
             bm = np.zeros(cfg.width * cfg.height, np.int32)
@@ -550,6 +553,7 @@ def test_walk_knobs_are_invariant_and_wave_log_is_consistent():
             outs.append((bm, st["rays"], st["shadowRays"]))
         r.set_tuning(6, 0)
         r.set_tuning(9, 32)
+        r.set_tuning(28, 0)
         r.set_profiling(counting=True)
         bm = np.zeros(cfg.width * cfg.height, np.int32)
         r.render_frame(bm)

@@ -10,8 +10,8 @@ import mobileraytracer_amd as m
 from mobileraytracer_amd import scenes
 
 
-def run(ranks):
-    o, l, c = scenes.conference()
+def run(ranks, scene="conference"):
+    o, l, c = scenes.conference() if scene == "conference" else scenes.conference_flat()
     cfg = m.Config(width=1920, height=1080, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5,
                    objFilePath=o, mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=ranks)
     r = m.Renderer(cfg)
@@ -25,7 +25,7 @@ def run(ranks):
     torch.cuda.synchronize()
     f = r.frame_stats()
     p = list(f["walkPhases"])
-    out = {"ranks": ranks, "walkedRays": f["walkedRays"], "shadowRays": f["shadowRays"]}
+    out = {"scene": scene, "ranks": ranks, "walkedRays": f["walkedRays"], "shadowRays": f["shadowRays"]}
     for w, name in enumerate(("closest", "shadow")):
         for k, ph in enumerate(("inner", "leaf", "triangle")):
             it, ln = p[6 * w + 2 * k], p[6 * w + 2 * k + 1]
@@ -39,5 +39,7 @@ def run(ranks):
 
 
 if __name__ == "__main__":
-    for ranks in (1, 8):
-        print(json.dumps(run(ranks)), flush=True)
+    # usage: phase_occupancy.py [conference|flat] ...   (default: conference)
+    for scene in (sys.argv[1:] or ["conference"]):
+        for ranks in (1, 8):
+            print(json.dumps(run(ranks, scene)), flush=True)
