@@ -229,8 +229,11 @@ __device__ __forceinline__ auto makeWalkStack(int2* ldsStack, int2* gstack, int 
         return makeRefStack<kWalkThreads>(ldsStack, gstack, gdepth);
 }
 
+#ifndef MRT_WALK_WAVES
+#define MRT_WALK_WAVES 7  // waves per SIMD of the per-lane walks
+#endif
 template <bool kCount, int kVariant, int kCull>
-__global__ __launch_bounds__(kWalkThreads, 7) void k_trace(DScene s, Level lv, int* counters, int level,
+__global__ __launch_bounds__(kWalkThreads, MRT_WALK_WAVES) void k_trace(DScene s, Level lv, int* counters, int level,
                                                             int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(kWalkThreads, 8) void k_trace_packet(DScene s, Leve
 }
 
 template <bool kCount, int kVariant, int kCull>
-__global__ __launch_bounds__(kWalkThreads, 7) void k_shadow(DScene s, Level lv, int* counters, int level,
+__global__ __launch_bounds__(kWalkThreads, MRT_WALK_WAVES) void k_shadow(DScene s, Level lv, int* counters, int level,
                                                              int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);

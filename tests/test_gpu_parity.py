@@ -485,11 +485,12 @@ def test_python_plugin_setters():
 
 
 def test_removed_tuning_keys_are_rejected():
-    """Binned emission (key 4), queue sorting (12-14), graph replay (15) and the tile kernel (19-23)
-    measured slower and were removed from the product: their keys are unknown."""
+    """Binned emission (key 4), queue sorting (12-14), graph replay (15), the tile kernel (19-23), the
+    CU-masked shadow stream (29) and k_shade's shading-class binning (30) measured slower and were
+    removed from the product (DESIGN.md sections 2, 6): their keys are unknown."""
     import mobileraytracer_amd as m
     with m.Renderer(make_cfg(32, 32)) as r:
-        for key in (4, 12, 13, 14, 15, 19, 20, 21, 22, 23):
+        for key in (4, 12, 13, 14, 15, 19, 20, 21, 22, 23, 29, 30):
             with pytest.raises(Exception):
                 r.set_tuning(key, 1)
 

@@ -10,7 +10,8 @@ from mobileraytracer_amd import scenes
 
 
 def main():
-    o, l, c = scenes.conference()
+    # SCENE=flat: the flat-geometry stand-in
+    o, l, c = scenes.conference() if os.environ.get("SCENE", "conference") == "conference" else scenes.conference_flat()
     ranks = int(os.environ.get("RANKS", 1))
     variants = os.environ.get("VARIANTS", "6=100,6=50").split(",")
     rs = {}
