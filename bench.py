@@ -215,7 +215,7 @@ def kernel_source_stamp():
     return h.hexdigest()
 
 
-PMC_PROFILE = os.path.join("profiles", "r04_pmc_traffic.json")
+PMC_PROFILE = os.path.join("profiles", "r05_pmc_traffic.json")
 
 
 def workload_key(args, shard_of):
