@@ -279,9 +279,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     // the walk tree: the reference leaves regrouped by a full-sweep SAH (rebuildOverLeaves; the
     // reference tree itself with MOBILERT_WALK_TREE=0).  Rays with a non-finite 1/d and the
     // per-wave reference walk use the reference tree, appended after it in the same node array.
-    const char* walkTree = std::getenv("MOBILERT_WALK_TREE");
-    const bool regroup = walkTree == nullptr || std::atoi(walkTree) != 0;
-    const std::vector<HBVHNode> wn = regroup ? rebuildOverLeaves(tn, 2) : tn;
+    const std::vector<HBVHNode> wn = walkTreeOver(tn);
     r->nTri = static_cast<int64_t>(sc.triangles.size());
     r->nPlanes = static_cast<int64_t>(sc.planes.size());
     r->nSpheres = static_cast<int64_t>(sc.spheres.size());
@@ -1583,9 +1581,7 @@ int64_t mrt_walk_tree(const mrt_config* cfg, uint32_t* nodes, float* grid, int32
         }
         std::vector<int32_t> perm;
         const std::vector<HBVHNode> tn = buildBVH(&sc.triangles, &perm);
-        const char* walkTree = std::getenv("MOBILERT_WALK_TREE");
-        const bool regroup = walkTree == nullptr || std::atoi(walkTree) != 0;
-        const std::vector<HBVHNode> wn = regroup ? rebuildOverLeaves(tn, 2) : tn;
+        const std::vector<HBVHNode> wn = walkTreeOver(tn);
         GRoot r{};
         QGrid g{};
         std::vector<QNode4> qn;

@@ -11,6 +11,7 @@
 #include <deque>
 #include <functional>
 #include <fstream>
+#include <queue>
 #include <random>
 #include <sstream>
 #include <string>
@@ -1025,6 +1026,100 @@ struct Quantizer {
 };
 }  // namespace
 
+// The optimal collapse's dynamic programme (toQuantizedBVH4): forest[i * (W + 1) + j] = the least
+// summed wide-node area covering BVH2 node i's subtree with at most j trees, split[] its choices.
+// forest[1] (the root as a wide node) is the whole wide tree's cost.
+static void collapseForests(const std::vector<HBVHNode>& nodes, std::vector<double>* forestOut,
+                            std::vector<int8_t>* splitOut) {
+    auto inner = [&](int32_t i) { return nodes[static_cast<size_t>(i)].numPrimitives == 0; };
+    auto area = [&](int32_t i) {
+        const HAABB& b = nodes[static_cast<size_t>(i)].box;
+        const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,
+                     dz = static_cast<double>(b.mx.z) - b.mn.z;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    constexpr int W1 = kWalkWidth + 1;
+    std::vector<double>& forest = *forestOut;
+    std::vector<int8_t>& split = *splitOut;
+    {
+        forest.assign(nodes.size() * W1, 0.0);  // leaves: 0 (the same in every tree)
+        split.assign(nodes.size() * W1, 0);
+        std::vector<std::pair<int32_t, bool>> post{{0, false}};
+        while (!post.empty()) {
+            const auto [i, done] = post.back();
+            post.pop_back();
+            if (!inner(i)) continue;
+            const size_t ui = static_cast<size_t>(i);
+            const int32_t l = nodes[ui].indexOffset, r = l + 1;
+            if (!done) {
+                post.push_back({i, true});
+                post.push_back({l, false});
+                post.push_back({r, false});
+                continue;
+            }
+            const size_t ul = static_cast<size_t>(l) * W1, ur = static_cast<size_t>(r) * W1;
+            auto best = [&](int j, int* k) {  // at most j trees split between the two children
+                double c = std::numeric_limits<double>::infinity();
+                for (int a = 1; a < j; ++a) {
+                    const double v = forest[ul + static_cast<size_t>(a)] + forest[ur + static_cast<size_t>(j - a)];
+                    if (v < c) {
+                        c = v;
+                        *k = a;
+                    }
+                }
+                return c;
+            };
+            int kw = 1;
+            const double asWide = area(i) + best(kWalkWidth, &kw);  // node i as a wide node
+            split[ui * W1] = static_cast<int8_t>(kw);
+            forest[ui * W1 + 1] = asWide;
+            for (int j = 2; j < W1; ++j) {
+                int k = 1;
+                const double c = best(j, &k);
+                const bool self = asWide <= c;
+                forest[ui * W1 + static_cast<size_t>(j)] = self ? asWide : c;
+                split[ui * W1 + static_cast<size_t>(j)] = static_cast<int8_t>(self ? 0 : k);
+            }
+        }
+    }
+}
+
+// The optimal collapse's summed wide-node area and its depth in wide nodes (0 without an inner node)
+static double collapsedArea(const std::vector<HBVHNode>& nodes, int* depth) {
+    *depth = 0;
+    if (nodes.size() < 3 || nodes[0].numPrimitives > 0) return 0.0;  // no inner node (an empty scene: one empty root)
+    std::vector<double> forest;
+    std::vector<int8_t> split;
+    collapseForests(nodes, &forest, &split);
+    constexpr int W1 = kWalkWidth + 1;
+    auto inner = [&](int32_t i) { return nodes[static_cast<size_t>(i)].numPrimitives == 0; };
+    // the wide nodes as toQuantizedBVH4 forms them: node i's children are the trees of the best
+    // forests under its two BVH2 children; an inner tree root is a wide node one level down
+    std::function<void(int32_t, int, std::vector<int32_t>&)> trees = [&](int32_t i, int j, std::vector<int32_t>& out) {
+        const int k = inner(i) && j > 1 ? split[static_cast<size_t>(i) * W1 + static_cast<size_t>(j)] : 0;
+        if (k == 0) {
+            out.push_back(i);
+            return;
+        }
+        trees(nodes[static_cast<size_t>(i)].indexOffset, k, out);
+        trees(nodes[static_cast<size_t>(i)].indexOffset + 1, j - k, out);
+    };
+    std::vector<std::pair<int32_t, int>> st{{0, 1}};
+    while (!st.empty()) {
+        const auto [i, d] = st.back();
+        st.pop_back();
+        *depth = std::max(*depth, d);
+        const int32_t l = nodes[static_cast<size_t>(i)].indexOffset;
+        const int kw = split[static_cast<size_t>(i) * W1];
+        std::vector<int32_t> c;
+        trees(l, kw, c);
+        trees(l + 1, kWalkWidth - kw, c);
+        for (const int32_t k : c)
+            if (inner(k)) st.push_back({k, d + 1});
+    }
+    return forest[1];
+}
+
 bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
                      QGrid* grid, std::vector<QNode4>* out, std::vector<int32_t>* bvh2Of) {
     out->clear();
@@ -1066,47 +1161,7 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
     std::vector<double> forest;  // [i * W1 + j], j = 1..kWalkWidth
     std::vector<int8_t> split;   // [i * W1 + j]: trees taken from the left child (0: node i itself);
                                  // [i * W1]: the split of node i as a wide node
-    if (optimal) {
-        forest.assign(nodes.size() * W1, 0.0);  // leaves: 0 (the same in every tree)
-        split.assign(nodes.size() * W1, 0);
-        std::vector<std::pair<int32_t, bool>> post{{0, false}};
-        while (!post.empty()) {
-            const auto [i, done] = post.back();
-            post.pop_back();
-            if (!inner(i)) continue;
-            const size_t ui = static_cast<size_t>(i);
-            const int32_t l = nodes[ui].indexOffset, r = l + 1;
-            if (!done) {
-                post.push_back({i, true});
-                post.push_back({l, false});
-                post.push_back({r, false});
-                continue;
-            }
-            const size_t ul = static_cast<size_t>(l) * W1, ur = static_cast<size_t>(r) * W1;
-            auto best = [&](int j, int* k) {  // at most j trees split between the two children
-                double c = std::numeric_limits<double>::infinity();
-                for (int a = 1; a < j; ++a) {
-                    const double v = forest[ul + static_cast<size_t>(a)] + forest[ur + static_cast<size_t>(j - a)];
-                    if (v < c) {
-                        c = v;
-                        *k = a;
-                    }
-                }
-                return c;
-            };
-            int kw = 1;
-            const double asWide = area(i) + best(kWalkWidth, &kw);  // node i as a wide node
-            split[ui * W1] = static_cast<int8_t>(kw);
-            forest[ui * W1 + 1] = asWide;
-            for (int j = 2; j < W1; ++j) {
-                int k = 1;
-                const double c = best(j, &k);
-                const bool self = asWide <= c;
-                forest[ui * W1 + static_cast<size_t>(j)] = self ? asWide : c;
-                split[ui * W1 + static_cast<size_t>(j)] = static_cast<int8_t>(self ? 0 : k);
-            }
-        }
-    }
+    if (optimal) collapseForests(nodes, &forest, &split);
     // the trees of node i's best forest of at most j (BVH2 indices, left to right)
     std::function<void(int32_t, int, std::vector<int32_t>&)> trees = [&](int32_t i, int j, std::vector<int32_t>& out) {
         const int k = inner(i) && j > 1 ? split[static_cast<size_t>(i) * W1 + static_cast<size_t>(j)] : 0;
@@ -1434,6 +1489,217 @@ std::vector<HBVHNode> rebuildOverLeaves(const std::vector<HBVHNode>& ref, int we
         st.push_back({left, t.b, bestSplit});
     }
     return out;
+}
+
+// Insertion-based optimisation of a BVH2 over fixed leaves (Bittner, Hapala, Havran 2013).  In the
+// exact mode no inner node is culled, so a ray visits every inner node whose box it passes: for
+// rays spread over the scene the expected visits are the summed inner-node surface area over the
+// root's, the quantity the SAH sweep above approximates greedily and this pass lowers.  Each round
+// takes a batch of inner nodes (below), removes each (its sibling takes the parent's
+// place) and reinserts its two children, one at a time, as the sibling of the node where the summed
+// area grows least (a branch-and-bound search from the root); boxes stay exact unions, the leaves
+// are untouched.  Rounds stop after three in a row that lower the total by less than 0.001 %.
+#ifndef MRT_TREE_OPT_STOP
+#define MRT_TREE_OPT_STOP 0.99999
+#endif
+constexpr double kTreeOptStop = MRT_TREE_OPT_STOP;  // a round must lower the summed area below this fraction
+std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int rounds, bool bounded) {
+    if (in.size() < 8 || rounds <= 0) return in;
+    struct N {
+        HAABB box;
+        int32_t l = -1, r = -1, parent = -1;
+        int32_t first = 0, count = 0;  // leaf: primitive range
+        int32_t height = 0;            // longest path to a leaf below (leaves 0)
+    };
+    std::vector<N> t(in.size());
+    for (size_t i = 0; i < in.size(); ++i) {
+        t[i].box = in[i].box;
+        if (in[i].numPrimitives > 0) {
+            t[i].first = in[i].indexOffset;
+            t[i].count = in[i].numPrimitives;
+        } else {
+            t[i].l = in[i].indexOffset;
+            t[i].r = in[i].indexOffset + 1;
+            t[static_cast<size_t>(t[i].l)].parent = static_cast<int32_t>(i);
+            t[static_cast<size_t>(t[i].r)].parent = static_cast<int32_t>(i);
+        }
+    }
+    auto unite = [](const HAABB& a, const HAABB& b) { return HAABB{vmin(a.mn, b.mn), vmax(a.mx, b.mx)}; };
+    auto area = [](const HAABB& b) {
+        const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,
+                     dz = static_cast<double>(b.mx.z) - b.mn.z;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    };
+    int32_t root = 0;
+    auto refit = [&](int32_t i) {
+        for (; i >= 0; i = t[static_cast<size_t>(i)].parent) {
+            N& n = t[static_cast<size_t>(i)];
+            n.box = unite(t[static_cast<size_t>(n.l)].box, t[static_cast<size_t>(n.r)].box);
+            n.height = 1 + std::max(t[static_cast<size_t>(n.l)].height, t[static_cast<size_t>(n.r)].height);
+        }
+    };
+    {  // heights bottom-up (children have larger indices in the reference numbering)
+        for (size_t k = t.size(); k-- > 0;) {
+            N& n = t[k];
+            if (n.count == 0 && n.l >= 0)
+                n.height = 1 + std::max(t[static_cast<size_t>(n.l)].height, t[static_cast<size_t>(n.r)].height);
+        }
+    }
+    // The walk's traversal stack grows with the tree's depth (3 pushes per wide level at most; entries
+    // past the LDS part spill to global memory, and the packet walk's stack is bounded), so an
+    // insertion may not make the tree deeper than the sweep built it.
+    const int32_t maxHeight = bounded ? t[0].height : std::numeric_limits<int32_t>::max() / 4;
+    auto total = [&]() {
+        double a = 0.0;
+        for (const N& n : t)
+            if (n.count == 0 && n.l >= 0) a += area(n.box);
+        return a;
+    };
+    // the best sibling for subtree x: minimal area of the new parent plus the growth of every ancestor
+    // (fallback: the position x came from, which keeps the height)
+    auto bestSibling = [&](int32_t x, int32_t fallback) {
+        const HAABB bx = t[static_cast<size_t>(x)].box;
+        const double ax = area(bx);
+        const int32_t hx = t[static_cast<size_t>(x)].height;
+        struct Q {
+            double bound, induced;
+            int32_t node, depth;
+            bool operator<(const Q& o) const { return bound > o.bound; }
+        };
+        std::priority_queue<Q> pq;
+        pq.push(Q{ax, 0.0, root, 0});
+        double best = std::numeric_limits<double>::infinity();
+        int32_t bestNode = -1;
+        while (!pq.empty()) {
+            const Q q = pq.top();
+            pq.pop();
+            if (q.bound >= best) break;
+            const N& c = t[static_cast<size_t>(q.node)];
+            const double merged = area(unite(c.box, bx));
+            const double cost = q.induced + merged;
+            // the new parent sits at c's depth: x and c's subtree one level down
+            if (cost < best && q.depth + 1 + std::max(hx, c.height) <= maxHeight) {
+                best = cost;
+                bestNode = q.node;
+            }
+            if (c.count == 0 && c.l >= 0 && q.depth + 2 + hx <= maxHeight) {
+                const double ind = q.induced + merged - area(c.box);
+                const double bound = ind + ax;
+                if (bound < best) {
+                    pq.push(Q{bound, ind, c.l, q.depth + 1});
+                    pq.push(Q{bound, ind, c.r, q.depth + 1});
+                }
+            }
+        }
+        return bestNode >= 0 ? bestNode : fallback;
+    };
+    // x becomes the sibling of c under the (free) node p
+    auto insertAt = [&](int32_t x, int32_t c, int32_t p) {
+        const int32_t g = t[static_cast<size_t>(c)].parent;
+        N& np = t[static_cast<size_t>(p)];
+        np.l = c;
+        np.r = x;
+        np.count = 0;
+        np.parent = g;
+        np.height = 1 + std::max(t[static_cast<size_t>(c)].height, t[static_cast<size_t>(x)].height);
+        t[static_cast<size_t>(c)].parent = p;
+        t[static_cast<size_t>(x)].parent = p;
+        if (g < 0) {
+            root = p;
+        } else if (t[static_cast<size_t>(g)].l == c) {
+            t[static_cast<size_t>(g)].l = p;
+        } else {
+            t[static_cast<size_t>(g)].r = p;
+        }
+        refit(p);
+    };
+    double cur = total();
+    std::vector<int> stamp(t.size(), -100);  // the round a node was last taken out
+    int stale = 0;
+    for (int round = 0; round < rounds; ++round) {
+        // the batch: the 1 % of inner nodes below the root's children that fit their children worst
+        // (Bittner et al.'s m_min * m_sum * m_area: large, and much larger than its children), skipping
+        // the nodes moved in the last two rounds
+        std::vector<std::pair<double, int32_t>> cand;
+        for (size_t i = 0; i < t.size(); ++i) {
+            const N& n = t[i];
+            if (n.count != 0 || n.l < 0 || static_cast<int32_t>(i) == root || n.parent < 0 || n.parent == root) continue;
+            if (stamp[i] >= round - 2) continue;
+            const double a = area(n.box), al = area(t[static_cast<size_t>(n.l)].box), ar = area(t[static_cast<size_t>(n.r)].box);
+            const double m = (a / std::max(1e-30, std::min(al, ar))) * (a / std::max(1e-30, al + ar)) * a;
+            cand.push_back({m, static_cast<int32_t>(i)});
+        }
+        const size_t batch = std::max<size_t>(1, cand.size() / 100);
+        std::partial_sort(cand.begin(), cand.begin() + static_cast<std::ptrdiff_t>(std::min(batch, cand.size())), cand.end(),
+                          [](const auto& a, const auto& b) { return a.first > b.first; });
+        for (size_t k = 0; k < batch && k < cand.size(); ++k) {
+            const int32_t v = cand[k].second;
+            stamp[static_cast<size_t>(v)] = round;
+            N& nv = t[static_cast<size_t>(v)];
+            if (nv.count != 0 || nv.l < 0 || v == root || nv.parent < 0 || nv.parent == root) continue;
+            // remove v and its parent p: v's sibling takes p's place; v and p become free parents
+            const int32_t p = nv.parent;
+            const int32_t sib = t[static_cast<size_t>(p)].l == v ? t[static_cast<size_t>(p)].r : t[static_cast<size_t>(p)].l;
+            const int32_t g = t[static_cast<size_t>(p)].parent;
+            if (t[static_cast<size_t>(g)].l == p) t[static_cast<size_t>(g)].l = sib; else t[static_cast<size_t>(g)].r = sib;
+            t[static_cast<size_t>(sib)].parent = g;
+            refit(g);
+            const int32_t a = nv.l, b = nv.r;
+            // reinsert the larger child first
+            const bool aFirst = area(t[static_cast<size_t>(a)].box) >= area(t[static_cast<size_t>(b)].box);
+            const int32_t x1 = aFirst ? a : b, x2 = aFirst ? b : a;
+            t[static_cast<size_t>(x1)].parent = -1;
+            t[static_cast<size_t>(x2)].parent = -1;
+            nv.l = nv.r = -1;
+            insertAt(x1, bestSibling(x1, sib), v);
+            insertAt(x2, bestSibling(x2, x1), p);
+        }
+        const double next = total();
+        stale = next > cur * kTreeOptStop ? stale + 1 : 0;
+        cur = next;
+        if (stale >= 3) break;
+    }
+    // re-emit in the reference numbering: root 0, an inner node's children adjacent
+    std::vector<HBVHNode> out(1);
+    std::vector<std::pair<int32_t, int32_t>> st{{root, 0}};
+    while (!st.empty()) {
+        const auto [i, slot] = st.back();
+        st.pop_back();
+        const N& n = t[static_cast<size_t>(i)];
+        if (n.count > 0) {
+            out[static_cast<size_t>(slot)] = HBVHNode{n.box, n.first, n.count};
+            continue;
+        }
+        const int32_t left = static_cast<int32_t>(out.size());
+        out.resize(out.size() + 2);
+        out[static_cast<size_t>(slot)] = HBVHNode{n.box, left, 0};
+        st.push_back({n.r, left + 1});
+        st.push_back({n.l, left});
+    }
+    return out;
+}
+
+std::vector<HBVHNode> walkTreeOver(const std::vector<HBVHNode>& ref) {
+    const char* walkTree = std::getenv("MOBILERT_WALK_TREE");
+    if (walkTree != nullptr && std::atoi(walkTree) == 0) return ref;
+    const char* opt = std::getenv("MOBILERT_TREE_OPT");
+    const int rounds = opt != nullptr ? std::atoi(opt) : kTreeOptRounds;
+    std::vector<HBVHNode> sweep = rebuildOverLeaves(ref, 2);
+    if (rounds <= 0 || sweep.size() < 8) return sweep;
+    // The optimisation lowers the BVH2's summed area; the wide tree's, after the collapse, usually
+    // with it but not always, and an unconstrained one may deepen the tree (its walk then spills
+    // stack entries past the LDS part: the flat stand-in's 13 wide levels became 22, 3.5 % slower).
+    // Kept: the first of (free, height-bounded) whose wide tree has a smaller summed area and no
+    // more wide levels than the sweep's; else the sweep.
+    int dSweep = 0;
+    const double aSweep = collapsedArea(sweep, &dSweep);
+    for (const bool bounded : {false, true}) {
+        std::vector<HBVHNode> opt2 = optimizeOverLeaves(sweep, rounds, bounded);
+        int d = 0;
+        const double a = collapsedArea(opt2, &d);
+        if (a < aSweep && d <= dSweep) return opt2;
+    }
+    return sweep;
 }
 
 std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris) {

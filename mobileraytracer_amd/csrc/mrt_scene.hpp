@@ -157,6 +157,15 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
 // by a full-sweep SAH; its inner boxes are exact unions of the leaf boxes (reference numbering:
 // node 0 the root, an inner node's children at indexOffset and indexOffset + 1).
 std::vector<HBVHNode> rebuildOverLeaves(const std::vector<HBVHNode>& ref, int weight = 0);
+// The same tree with its summed inner-node area lowered by insertion-based optimisation (at most
+// `rounds` rounds; leaves and exact-union boxes kept, reference numbering; bounded: no insertion
+// makes the tree higher than it was)
+std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& tree, int rounds, bool bounded = true);
+// The walk tree over the reference tree's leaves: rebuildOverLeaves (weight 2), then
+// optimizeOverLeaves (MOBILERT_TREE_OPT rounds, default kTreeOptRounds) where it lowers the wide
+// tree's summed area without adding wide levels; the reference tree itself with MOBILERT_WALK_TREE=0
+constexpr int kTreeOptRounds = 100;
+std::vector<HBVHNode> walkTreeOver(const std::vector<HBVHNode>& ref);
 // The cull word (mrt_common.hpp) of every node of a triangle BVH built by buildBVH over tris
 // (already in BVH order): the normal-line cone and the conditioning bound K of its triangles.
 std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris);

@@ -16,8 +16,8 @@ def main():
     variants = os.environ.get("VARIANTS", "6=100,6=50").split(",")
     rs = {}
     for v in variants:
-        # W=0: MOBILERT_WALK_TREE, C=greedy: MOBILERT_COLLAPSE for this renderer's scene upload
-        env = {"W": "MOBILERT_WALK_TREE", "C": "MOBILERT_COLLAPSE"}
+        # W=0: MOBILERT_WALK_TREE, C=greedy: MOBILERT_COLLAPSE, O=rounds: MOBILERT_TREE_OPT for this renderer's scene upload
+        env = {"W": "MOBILERT_WALK_TREE", "C": "MOBILERT_COLLAPSE", "O": "MOBILERT_TREE_OPT"}
         for kv in filter(None, v.split("+")):
             k, val = kv.split("=")
             if k in env:
