@@ -1503,6 +1503,10 @@ std::vector<HBVHNode> rebuildOverLeaves(const std::vector<HBVHNode>& ref, int we
 #define MRT_TREE_OPT_STOP 0.99999
 #endif
 constexpr double kTreeOptStop = MRT_TREE_OPT_STOP;  // a round must lower the summed area below this fraction
+#ifndef MRT_TREE_OPT_BATCH
+#define MRT_TREE_OPT_BATCH 100
+#endif
+constexpr size_t kTreeOptBatchDiv = MRT_TREE_OPT_BATCH;  // a round moves 1 / this of the candidates
 std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int rounds, bool bounded) {
     if (in.size() < 8 || rounds <= 0) return in;
     struct N {
@@ -1629,7 +1633,7 @@ std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int ro
             const double m = (a / std::max(1e-30, std::min(al, ar))) * (a / std::max(1e-30, al + ar)) * a;
             cand.push_back({m, static_cast<int32_t>(i)});
         }
-        const size_t batch = std::max<size_t>(1, cand.size() / 100);
+        const size_t batch = std::max<size_t>(1, cand.size() / kTreeOptBatchDiv);
         std::partial_sort(cand.begin(), cand.begin() + static_cast<std::ptrdiff_t>(std::min(batch, cand.size())), cand.end(),
                           [](const auto& a, const auto& b) { return a.first > b.first; });
         for (size_t k = 0; k < batch && k < cand.size(); ++k) {
