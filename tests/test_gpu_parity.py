@@ -675,8 +675,9 @@ def test_shard_assembly_over_many_ranks():
 
 
 def test_c5_4k_8spp_shards_and_tiles(oracle_mod):
-    """C5 (3840x2160, 8 spp, PathTracer): the 2-, 4- and 8-shard assemblies equal the single-GPU
-    frame ("image identical across 1/2/4/8 GPUs"), and 32 whole reference tiles
+    """C5 (3840x2160, 8 spp, PathTracer): the 2-, 4- and 8-shard assemblies and an 8-shard device
+    group equal the single-GPU frame ("image identical across 1/2/4/8 GPUs"), and 32
+    whole reference tiles
     (240x135 px x 8 samples each, Renderer.cpp:125-135), stratified so that every tile row and
     every tile column of the 16 x 16 grid holds two of them, equal the oracle bit for bit."""
     kw = dict(width=3840, height=2160, shader=2, scene="conference", spp=8, max_depth=5)
@@ -687,6 +688,10 @@ def test_c5_4k_8spp_shards_and_tiles(oracle_mod):
     for world in (2, 4, 8):
         img, _, srays = _render_shards(kw, world)
         assert np.array_equal(img, single) and srays == rays, world
+    # the same 8-way split as a device group behind the C-ABI (mrt_config.devices; the ordinal
+    # repeated on a one-GPU box): one renderer per shard, each from a host thread of its own
+    group, grays, _ = gpu_render(make_cfg(**kw, devices=[0] * 8))
+    assert np.array_equal(group, single) and grays == rays
     # tile k covers column k % 16, row k / 16; rows r and columns (r * 5) % 16, (r * 5 + 8) % 16
     tiles = sorted({16 * r + (5 * r + 8 * h) % 16 for r in range(16) for h in range(2)})
     assert len(tiles) == 32
