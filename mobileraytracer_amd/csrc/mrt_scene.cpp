@@ -1515,17 +1515,31 @@ std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int ro
         int32_t first = 0, count = 0;  // leaf: primitive range
         int32_t height = 0;            // longest path to a leaf below (leaves 0)
     };
-    std::vector<N> t(in.size());
-    for (size_t i = 0; i < in.size(); ++i) {
-        t[i].box = in[i].box;
-        if (in[i].numPrimitives > 0) {
-            t[i].first = in[i].indexOffset;
-            t[i].count = in[i].numPrimitives;
-        } else {
-            t[i].l = in[i].indexOffset;
-            t[i].r = in[i].indexOffset + 1;
-            t[static_cast<size_t>(t[i].l)].parent = static_cast<int32_t>(i);
-            t[static_cast<size_t>(t[i].r)].parent = static_cast<int32_t>(i);
+    // the nodes reachable from the root (a build's array may hold unused zero slots), renumbered
+    // parents first
+    std::vector<N> t;
+    {
+        std::vector<std::pair<int32_t, int32_t>> st{{0, -1}};  // (input node, parent in t)
+        while (!st.empty()) {
+            const auto [i, parent] = st.back();
+            st.pop_back();
+            const int32_t k = static_cast<int32_t>(t.size());
+            t.emplace_back();
+            N& n = t.back();
+            const HBVHNode& h = in[static_cast<size_t>(i)];
+            n.box = h.box;
+            n.parent = parent;
+            if (parent >= 0) {
+                N& pn = t[static_cast<size_t>(parent)];
+                (pn.l < 0 ? pn.l : pn.r) = k;
+            }
+            if (h.numPrimitives > 0) {
+                n.first = h.indexOffset;
+                n.count = h.numPrimitives;
+            } else {
+                st.push_back({h.indexOffset + 1, k});
+                st.push_back({h.indexOffset, k});
+            }
         }
     }
     auto unite = [](const HAABB& a, const HAABB& b) { return HAABB{vmin(a.mn, b.mn), vmax(a.mx, b.mx)}; };
@@ -1542,7 +1556,7 @@ std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int ro
             n.height = 1 + std::max(t[static_cast<size_t>(n.l)].height, t[static_cast<size_t>(n.r)].height);
         }
     };
-    {  // heights bottom-up (children have larger indices in the reference numbering)
+    {  // heights bottom-up (children have larger indices: parents first above)
         for (size_t k = t.size(); k-- > 0;) {
             N& n = t[k];
             if (n.count == 0 && n.l >= 0)
