@@ -203,13 +203,14 @@ def strip_comments(src):
 
 
 def kernel_source_stamp():
-    """sha256 of the HIP sources the walk / shading kernels are built from, comments stripped: a
-    PMC profile is reported only while it was measured on this exact code."""
+    """sha256 of the sources the walk / shading kernels and the walk tree they read are built from
+    (the HIP kernels and the host scene build), comments stripped: a PMC profile is reported only
+    while it was measured on this exact code."""
     import hashlib
     h = hashlib.sha256()
     d = os.path.join(HERE, "mobileraytracer_amd", "csrc")
     for name in sorted(os.listdir(d)):
-        if name.endswith((".hip", ".hpp")):
+        if name.endswith((".hip", ".hpp", ".cpp")):
             with open(os.path.join(d, name), encoding="utf-8") as f:
                 h.update(name.encode() + b"\0" + strip_comments(f.read()).encode())
     return h.hexdigest()

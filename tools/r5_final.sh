@@ -8,7 +8,8 @@ export PYTHONUNBUFFERED=1
 python -c "from mobileraytracer_amd import _native as n; assert n.build_is_current(), 'stale libmobilert_amd.so'" || exit 2
 bash tools/pmc_run.sh ${N}_pmc > $OUT/pmc.log 2>&1 || { tail $OUT/pmc.log; exit 3; }
 tail -1 $OUT/pmc.log
-cp $R/gpurun_out/${N}_pmc/pmc_traffic.json $R/profiles/r05_pmc_traffic.json
+cp $R/gpurun_out/${N}_pmc/pmc_traffic.json $R/profiles/r05_pmc_traffic.json  # (this copy stays on the box:
+# back here, copy gpurun_out/${N}_pmc/pmc_traffic.json into profiles/ before committing)
 timeout -k 10 400 python bench.py > $OUT/bench.log 2>&1 || { tail $OUT/bench.log; exit 4; }
 tail -1 $OUT/bench.log > $OUT/bench.json; cut -c1-300 $OUT/bench.json
 timeout -k 10 200 python bench.py --shard-of 8 --no-cpu-baseline > $OUT/shard8.log 2>&1 || { tail $OUT/shard8.log; exit 5; }
