@@ -28,11 +28,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _bench(tmp, name, nproc, launcher=True):
+def _bench(tmp, name, nproc, launcher=True, extra_env=None, extra_args=()):
     out = os.path.join(tmp, name + ".npy")
     args = ["bench.py", "--gpus", str(nproc), "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
-            "--width", str(W), "--height", str(H), "--spp", str(SPP), "--dump-bitmap", out]
+            "--width", str(W), "--height", str(H), "--spp", str(SPP), "--dump-bitmap", out] + list(extra_args)
     env = dict(os.environ, MRT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    env.update(extra_env or {})
     if nproc > 1 and launcher:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
@@ -65,3 +66,12 @@ def test_two_rank_bench_assembles_the_single_gpu_frame(tmp_path, oracle_mod):
     js = json.loads(line_s)
     assert js["n_gpus"] == 2 and "gloo gather" in js["config"]["parallelism"]
     assert np.array_equal(spawned, one), int((spawned != one).sum())
+    # the RCCL path itself at world size 1 (MRT_BENCH_FORCE_DIST: process group, packed shard,
+    # gather, unpack) assembles the same frame
+    rccl = dict(MRT_BENCH_BACKEND="nccl", MRT_BENCH_FORCE_DIST="1", RANK="0", LOCAL_RANK="0", WORLD_SIZE="1",
+                MASTER_PORT=str(_free_port()))
+    img, line_r = _bench(str(tmp_path), "rccl", 1, launcher=False, extra_env=rccl,
+                         extra_args=("--steps", "3", "--warmup", "2"))
+    jr = json.loads(line_r)
+    assert "RCCL gather" in jr["config"]["parallelism"], jr["config"]["parallelism"]
+    assert np.array_equal(img, one), int((img != one).sum())
