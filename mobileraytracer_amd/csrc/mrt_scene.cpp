@@ -11,6 +11,8 @@
 #include <deque>
 #include <functional>
 #include <fstream>
+#include <memory>
+#include <mutex>
 #include <queue>
 #include <random>
 #include <sstream>
@@ -1697,27 +1699,184 @@ std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int ro
     return out;
 }
 
-std::vector<HBVHNode> walkTreeOver(const std::vector<HBVHNode>& ref) {
-    const char* walkTree = std::getenv("MOBILERT_WALK_TREE");
-    if (walkTree != nullptr && std::atoi(walkTree) == 0) return ref;
-    const char* opt = std::getenv("MOBILERT_TREE_OPT");
-    const int rounds = opt != nullptr ? std::atoi(opt) : kTreeOptRounds;
+// Rotations of a BVH2 over fixed leaves that lower the optimal 4-wide collapse's summed area
+// directly (the insertion pass above lowers the BVH2's): at each inner node n the four rotations
+// that swap one child with a grandchild under the other (Kopta et al. 2012), kept when the root's
+// collapse cost falls.  The collapse's forest table (collapseForests) of a node depends on its
+// subtree only, so a rotation recomputes the rotated child, n and n's ancestors.
+static std::vector<HBVHNode> rotateForWide(const std::vector<HBVHNode>& in, int sweeps) {
+    if (in.size() < 8 || sweeps <= 0) return in;
+    constexpr int W1 = kWalkWidth + 1;
+    struct R {
+        HAABB box;
+        int32_t l = -1, r = -1, parent = -1, first = 0, count = 0;
+        double F[W1] = {};
+    };
+    std::vector<R> t;
+    {
+        std::vector<std::pair<int32_t, int32_t>> st{{0, -1}};
+        while (!st.empty()) {
+            const auto [i, parent] = st.back();
+            st.pop_back();
+            const int32_t k = static_cast<int32_t>(t.size());
+            t.emplace_back();
+            R& n = t.back();
+            const HBVHNode& h = in[static_cast<size_t>(i)];
+            n.box = h.box;
+            n.parent = parent;
+            if (parent >= 0) {
+                R& pn = t[static_cast<size_t>(parent)];
+                (pn.l < 0 ? pn.l : pn.r) = k;
+            }
+            if (h.numPrimitives > 0) {
+                n.first = h.indexOffset;
+                n.count = h.numPrimitives;
+            } else {
+                st.push_back({h.indexOffset + 1, k});
+                st.push_back({h.indexOffset, k});
+            }
+        }
+    }
+    auto area = [](const HAABB& b) {
+        const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,
+                     dz = static_cast<double>(b.mx.z) - b.mn.z;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    auto inner = [&](int32_t i) { return t[static_cast<size_t>(i)].count == 0; };
+    auto dp = [&](int32_t i) {  // collapseForests' recurrence for node i from its children's rows
+        R& n = t[static_cast<size_t>(i)];
+        if (n.count > 0) return;
+        n.box = HAABB{vmin(t[static_cast<size_t>(n.l)].box.mn, t[static_cast<size_t>(n.r)].box.mn),
+                      vmax(t[static_cast<size_t>(n.l)].box.mx, t[static_cast<size_t>(n.r)].box.mx)};
+        const double* L = t[static_cast<size_t>(n.l)].F;
+        const double* Rr = t[static_cast<size_t>(n.r)].F;
+        auto best = [&](int j) {
+            double c = std::numeric_limits<double>::infinity();
+            for (int a = 1; a < j; ++a) c = std::min(c, L[a] + Rr[j - a]);
+            return c;
+        };
+        const double asWide = area(n.box) + best(kWalkWidth);
+        n.F[1] = asWide;
+        for (int j = 2; j < W1; ++j) n.F[j] = std::min(asWide, best(j));
+    };
+    for (size_t k = t.size(); k-- > 0;) dp(static_cast<int32_t>(k));  // children after parents
+    auto up = [&](int32_t i) {
+        for (; i >= 0; i = t[static_cast<size_t>(i)].parent) dp(i);
+    };
+    // swap subtree x (child of n) with y (child of n's other child m)
+    auto swapSub = [&](int32_t n, int32_t x, int32_t m, int32_t y) {
+        R& rn = t[static_cast<size_t>(n)];
+        R& rm = t[static_cast<size_t>(m)];
+        (rn.l == x ? rn.l : rn.r) = y;
+        (rm.l == y ? rm.l : rm.r) = x;
+        t[static_cast<size_t>(x)].parent = m;
+        t[static_cast<size_t>(y)].parent = n;
+        dp(m);
+        up(n);
+    };
+    double cur = t[0].F[1];
+    for (int sweep = 0; sweep < sweeps; ++sweep) {
+        int improved = 0;
+        for (int32_t n = 0; n < static_cast<int32_t>(t.size()); ++n) {
+            if (!inner(n)) continue;
+            for (int side = 0; side < 2; ++side) {
+                const int32_t x = side == 0 ? t[static_cast<size_t>(n)].l : t[static_cast<size_t>(n)].r;
+                const int32_t m = side == 0 ? t[static_cast<size_t>(n)].r : t[static_cast<size_t>(n)].l;
+                if (!inner(m)) continue;
+                bool done = false;
+                for (int g = 0; g < 2 && !done; ++g) {
+                    const int32_t y = g == 0 ? t[static_cast<size_t>(m)].l : t[static_cast<size_t>(m)].r;
+                    swapSub(n, x, m, y);
+                    if (t[0].F[1] < cur * (1.0 - 1e-12)) {
+                        cur = t[0].F[1];
+                        ++improved;
+                        done = true;
+                    } else {
+                        swapSub(n, y, m, x);  // undo
+                    }
+                }
+                if (done) break;
+            }
+        }
+        if (improved == 0) break;
+    }
+    std::vector<HBVHNode> out(1);
+    std::vector<std::pair<int32_t, int32_t>> st{{0, 0}};
+    while (!st.empty()) {
+        const auto [i, slot] = st.back();
+        st.pop_back();
+        const R& n = t[static_cast<size_t>(i)];
+        if (n.count > 0) {
+            out[static_cast<size_t>(slot)] = HBVHNode{n.box, n.first, n.count};
+            continue;
+        }
+        const int32_t left = static_cast<int32_t>(out.size());
+        out.resize(out.size() + 2);
+        out[static_cast<size_t>(slot)] = HBVHNode{n.box, left, 0};
+        st.push_back({n.r, left + 1});
+        st.push_back({n.l, left});
+    }
+    return out;
+}
+
+static std::vector<HBVHNode> walkTreeBuild(const std::vector<HBVHNode>& ref, int rounds, int rotSweeps) {
     std::vector<HBVHNode> sweep = rebuildOverLeaves(ref, 2);
     if (rounds <= 0 || sweep.size() < 8) return sweep;
     // The optimisation lowers the BVH2's summed area; the wide tree's, after the collapse, usually
     // with it but not always, and an unconstrained one may deepen the tree (its walk then spills
     // stack entries past the LDS part: the flat stand-in's 13 wide levels became 22, 3.5 % slower).
     // Kept: the first of (free, height-bounded) whose wide tree has a smaller summed area and no
-    // more wide levels than the sweep's; else the sweep.
+    // more wide levels than the sweep's, then rotated where that lowers the wide area further
+    // within the same depth; else the sweep.  (Rotations are not tried on trees the rule rejects:
+    // on the flat stand-in they made a rejected tree pass and its shadow walks test 9 % more
+    // triangles before an occluder, +1.6 % frame time, profiles/r05_tree_rotation_ab.txt.)
     int dSweep = 0;
     const double aSweep = collapsedArea(sweep, &dSweep);
     for (const bool bounded : {false, true}) {
         std::vector<HBVHNode> opt2 = optimizeOverLeaves(sweep, rounds, bounded);
         int d = 0;
         const double a = collapsedArea(opt2, &d);
-        if (a < aSweep && d <= dSweep) return opt2;
+        if (a < aSweep && d <= dSweep) {
+            std::vector<HBVHNode> rot = rotateForWide(opt2, rotSweeps);
+            int dr = 0;
+            const double ar = collapsedArea(rot, &dr);
+            return ar < a && dr <= dSweep ? rot : opt2;
+        }
     }
     return sweep;
+}
+
+std::vector<HBVHNode> walkTreeOver(const std::vector<HBVHNode>& ref) {
+    const char* walkTree = std::getenv("MOBILERT_WALK_TREE");
+    if (walkTree != nullptr && std::atoi(walkTree) == 0) return ref;
+    const char* opt = std::getenv("MOBILERT_TREE_OPT");
+    const int rounds = opt != nullptr ? std::atoi(opt) : kTreeOptRounds;
+    const char* rot = std::getenv("MOBILERT_TREE_ROT");
+    const int rotSweeps = rot != nullptr ? std::atoi(rot) : kTreeRotSweeps;
+    // Renderers of one scene in one process (a device group's shards, a front end re-creating its
+    // renderer, the test suite) share the tree: built once per (reference tree, settings), a few
+    // seconds for the conference stand-in.  The key is the whole reference tree's bytes.
+    std::string key(reinterpret_cast<const char*>(ref.data()), ref.size() * sizeof(HBVHNode));
+    key.append(reinterpret_cast<const char*>(&rounds), sizeof(rounds));
+    key.append(reinterpret_cast<const char*>(&rotSweeps), sizeof(rotSweeps));
+    static std::mutex mu;
+    static std::unordered_map<std::string, std::shared_ptr<const std::vector<HBVHNode>>> cache;
+    static std::deque<std::string> order;  // least recently built first: at most kTreeCacheScenes kept
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        const auto it = cache.find(key);
+        if (it != cache.end()) return *it->second;
+    }
+    auto tree = std::make_shared<const std::vector<HBVHNode>>(walkTreeBuild(ref, rounds, rotSweeps));
+    std::lock_guard<std::mutex> lock(mu);
+    if (cache.emplace(key, tree).second) {
+        order.push_back(key);
+        while (order.size() > kTreeCacheScenes) {
+            cache.erase(order.front());
+            order.pop_front();
+        }
+    }
+    return *tree;
 }
 
 std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris) {

@@ -163,8 +163,13 @@ std::vector<HBVHNode> rebuildOverLeaves(const std::vector<HBVHNode>& ref, int we
 std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& tree, int rounds, bool bounded = true);
 // The walk tree over the reference tree's leaves: rebuildOverLeaves (weight 2), then
 // optimizeOverLeaves (MOBILERT_TREE_OPT rounds, default kTreeOptRounds) where it lowers the wide
-// tree's summed area without adding wide levels; the reference tree itself with MOBILERT_WALK_TREE=0
+// tree's summed area without adding wide levels, then rotations that lower the wide area directly
+// (MOBILERT_TREE_ROT sweeps, default kTreeRotSweeps); the reference tree itself with
+// MOBILERT_WALK_TREE=0.  Built once per reference tree and settings in a process (the last
+// kTreeCacheScenes kept).
 constexpr int kTreeOptRounds = 100;
+constexpr int kTreeRotSweeps = 1;
+constexpr size_t kTreeCacheScenes = 4;
 std::vector<HBVHNode> walkTreeOver(const std::vector<HBVHNode>& ref);
 // The cull word (mrt_common.hpp) of every node of a triangle BVH built by buildBVH over tris
 // (already in BVH order): the normal-line cone and the conditioning bound K of its triangles.

@@ -132,6 +132,31 @@ def test_tree_optimisation_lowers_the_summed_area(case, monkeypatch):
         assert a1 <= a0 * 0.97, (a1, a0)
 
 
+@pytest.mark.parametrize("case", [dict(scene="conference"), dict(scene="conference_flat"), dict(scene="water"),
+                                  dict(scene="teapot")])
+def test_wide_rotations_lower_the_wide_area(case, monkeypatch):
+    """Rotations of the optimised tree kept where they lower the optimal collapse's summed area
+    (mrt_scene.cpp rotateForWide, MOBILERT_TREE_ROT sweeps): never a larger wide area than without
+    them, the conference stand-in's lower by >= 0.3 %, and the flat stand-in's tree (the sweep:
+    its optimised trees are deeper) untouched.  The process's tree cache keys on the settings."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, **case)
+    monkeypatch.setenv("MOBILERT_TREE_ROT", "0")
+    n0, g0, r0 = m.walk_tree(cfg)
+    monkeypatch.delenv("MOBILERT_TREE_ROT")
+    n1, g1, r1 = m.walk_tree(cfg)
+    width = int(r0[2])
+    a0, a1 = _wide_node_area(n0, g0, width), _wide_node_area(n1, g1, width)
+    assert a1 <= a0 * 1.0001, (a1, a0)
+    if case.get("scene") == "conference":
+        assert a1 <= a0 * 0.997, (a1, a0)
+    if case.get("scene") == "conference_flat":
+        assert np.array_equal(n0, n1)
+    # built once per reference tree and settings: the same arrays again, from the cache
+    n2, g2, r2 = m.walk_tree(cfg)
+    assert np.array_equal(n1, n2) and np.array_equal(g1, g2) and np.array_equal(r1, r2)
+
+
 @pytest.mark.parametrize("case", [dict(scene="conference"), dict(scene="water"), dict(sceneIndex=3)])
 def test_unused_slots_hold_inverted_boxes(case):
     """An unused child slot of the walk tree holds min 65535 / max 0 on every axis

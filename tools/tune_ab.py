@@ -17,7 +17,7 @@ def main():
     rs = {}
     for v in variants:
         # W=0: MOBILERT_WALK_TREE, C=greedy: MOBILERT_COLLAPSE, O=rounds: MOBILERT_TREE_OPT for this renderer's scene upload
-        env = {"W": "MOBILERT_WALK_TREE", "C": "MOBILERT_COLLAPSE", "O": "MOBILERT_TREE_OPT"}
+        env = {"W": "MOBILERT_WALK_TREE", "C": "MOBILERT_COLLAPSE", "O": "MOBILERT_TREE_OPT", "R": "MOBILERT_TREE_ROT"}
         for kv in filter(None, v.split("+")):
             k, val = kv.split("=")
             if k in env:
