@@ -454,6 +454,14 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
 #ifndef MRT_SEG_INTERLEAVE
 #define MRT_SEG_INTERLEAVE 1
 #endif
+// The cursors hand out the queue from its end (round 5): a level's queue is written in index order
+// by the shading before it, so its last entries are the most recently written and, at N = 1 (each
+// level's ray records ~400 MB, more than the 256 MB Infinity Cache), the ones still cached.  C4
+// 14.655 -> 14.575 ms, N = 8 shard unchanged (2.63 / 2.64 ms; its queues fit the cache), images
+// identical (profiles/r05_queue_order_ab.txt).
+#ifndef MRT_SEG_REVERSE
+#define MRT_SEG_REVERSE 1
+#endif
 #ifndef MRT_SEG_CHUNK_LOG
 #define MRT_SEG_CHUNK_LOG 12
 #endif
@@ -511,7 +519,11 @@ struct LevelQueue {
                 (void)segStart;
                 (void)segEnd;
                 const int idx = interleavedIndex(base + lanesBelowIn(pending), seg, shift);
+#if MRT_SEG_REVERSE
+                if (idx < count) got = count - 1 - idx;
+#else
                 if (idx < count) got = idx;
+#endif
 #else
                 const int idx = segStart + base + lanesBelowIn(pending);
                 if (idx < segEnd) got = idx;
