@@ -1,6 +1,7 @@
 """A/B of tuning settings on the C4 frame: one renderer per setting in one process, interleaved
 rounds, no per-launch events, images compared.  VARIANTS="6=100,6=75+3=1,W=0" (key=value pairs joined
-by '+', settings separated by ','; W sets MOBILERT_WALK_TREE for the upload); RANKS=N renders rank 0's shard of an N-GPU frame."""
+by '+', settings separated by ','; W / C / O / R set MOBILERT_WALK_TREE / MOBILERT_COLLAPSE / MOBILERT_TREE_OPT /
+MOBILERT_TREE_ROT for the upload, P Config.maxPathsPerPass); RANKS=N renders rank 0's shard of an N-GPU frame."""
 import os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -22,14 +23,17 @@ def main():
             k, val = kv.split("=")
             if k in env:
                 os.environ[env[k]] = val
+        # P=n: Config.maxPathsPerPass (the frame in passes of at most n paths)
+        paths = [int(kv.split("=")[1]) for kv in v.split("+") if kv.startswith("P=")]
         cfg = m.Config(width=1920, height=1080, shader=2, sceneIndex=-1, samplesPixel=4, maxDepth=5,
-                       objFilePath=o, mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=ranks)
+                       objFilePath=o, mtlFilePath=l, camFilePath=c, rankIndex=0, rankCount=ranks,
+                       maxPathsPerPass=paths[0] if paths else 0)
         r = m.Renderer(cfg)
         for kv in filter(None, v.split("+")):
             k, val = kv.split("=")
             if k in env:
                 os.environ.pop(env[k])
-            else:
+            elif k != "P":
                 r.set_tuning(int(k), int(val))
         rs[v] = r
     n = max(1920 * 1080, rs[variants[0]].scene_info()["pixelSlotsMax"])
