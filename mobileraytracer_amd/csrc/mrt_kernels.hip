@@ -229,8 +229,14 @@ __device__ __forceinline__ auto makeWalkStack(int2* ldsStack, int2* gstack, int 
         return makeRefStack<kWalkThreads>(ldsStack, gstack, gdepth);
 }
 
+// Waves per SIMD of the per-lane walks.  Round 5: 6, whose 80 VGPRs hold
+// the triangle loop's prefetch of the next triangle (MRT_TRI_PREFETCH, mrt_trace_ww.hpp); 7 waves
+// (72 VGPRs) without it measured 3 % slower, 6 waves without it the same as 7.
 #ifndef MRT_WALK_WAVES
-#define MRT_WALK_WAVES 7  // waves per SIMD of the per-lane walks
+#define MRT_WALK_WAVES 6
+#endif
+#ifndef MRT_SHADOW_WAVES
+#define MRT_SHADOW_WAVES MRT_WALK_WAVES
 #endif
 template <bool kCount, int kVariant, int kCull>
 __global__ __launch_bounds__(kWalkThreads, MRT_WALK_WAVES) void k_trace(DScene s, Level lv, int* counters, int level,
@@ -289,7 +295,7 @@ __global__ __launch_bounds__(kWalkThreads, 8) void k_trace_packet(DScene s, Leve
 }
 
 template <bool kCount, int kVariant, int kCull>
-__global__ __launch_bounds__(kWalkThreads, MRT_WALK_WAVES) void k_shadow(DScene s, Level lv, int* counters, int level,
+__global__ __launch_bounds__(kWalkThreads, MRT_SHADOW_WAVES) void k_shadow(DScene s, Level lv, int* counters, int level,
                                                              int2* gstack, int gdepth, unsigned long long* stats) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);

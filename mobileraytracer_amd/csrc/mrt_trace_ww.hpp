@@ -459,6 +459,15 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
 // level's ray records ~400 MB, more than the 256 MB Infinity Cache), the ones still cached.  C4
 // 14.655 -> 14.575 ms, N = 8 shard unchanged (2.63 / 2.64 ms; its queues fit the cache), images
 // identical (profiles/r05_queue_order_ab.txt).
+// The leaf loop's triangles software-pipelined (round 5): triangle k + 1's three loads go out
+// before triangle k's test, so a lane's tests wait on one round trip per leaf instead of one per
+// triangle.  It needs 9 more VGPRs across the test, which the walks' 6 waves per SIMD (80 VGPRs,
+// mrt_kernels.hip MRT_WALK_WAVES) hold: C4 14.53 -> 14.05 ms, N = 8 shard 2.61 -> 2.53 ms, the flat
+// stand-in 39.4 -> 37.7 ms, images identical (profiles/r05_tri_prefetch_ab.txt; at 7 waves it spilled
+// 36 B and lost).
+#ifndef MRT_TRI_PREFETCH
+#define MRT_TRI_PREFETCH 1
+#endif
 #ifndef MRT_SEG_REVERSE
 #define MRT_SEG_REVERSE 1
 #endif
@@ -870,6 +879,29 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
                 }
             }
             bool hit = false;
+#if MRT_TRI_PREFETCH
+            // software-pipelined: triangle k + 1's loads go out before triangle k's test
+            float4 ca = a0, cb = b0t, cc = c0;
+            for (int k = 0; k < nprim; ++k) {
+                if (kCount) phaseCount(&cnt->triIters, &cnt->triLanes);
+                const int j = first + k;
+                float4 na = ca, nb = cb, nc = cc;
+                if (k + 1 < nprim) {
+                    const uint32_t offn = static_cast<uint32_t>(j + 1) * 48u;
+                    na = bload3(triBuf, offn);
+                    nb = bload3(triBuf, offn + 16u);
+                    nc = bload3(triBuf, offn + 32u);
+                }
+                const float4 ta = ca, tb = cb, tc = cc;
+                ca = na;
+                cb = nb;
+                cc = nc;
+                const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
+                if (code == src) continue;
+                float t, u, v;
+                if (kCount) ++cnt->tris;
+                if (!triTest(ta, tb, tc, o, d, &t, &u, &v)) continue;
+#else
             for (int k = 0; k < nprim; ++k) {
                 if (kCount) phaseCount(&cnt->triIters, &cnt->triLanes);
                 const int j = first + k;
@@ -882,6 +914,7 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
                 if (!triTest(f ? a0 : bload3(triBuf, off), f ? b0t : bload3(triBuf, off + 16u),
                              f ? c0 : bload3(triBuf, off + 32u), o, d, &t, &u, &v))
                     continue;
+#endif
                 if (t < kEpsilon) continue;
                 if (kAny) {
                     if (!(t >= bt)) {
