@@ -18,6 +18,7 @@ namespace mrt {
 
 constexpr int kBlock = 256;         // threads per workgroup for every trace kernel
 constexpr int kLdsStackMin = 8;     // per-thread stack entries (8 bytes) in LDS; deeper ones spill
+static_assert((kLdsStackMin & (kLdsStackMin - 1)) == 0, "the LDS stack rings are indexed by a power-of-two mask");
 
 struct DScene {
     const float4* triGeom;     // 3 per triangle (BVH order): A, AB, AC  (xyz)
