@@ -468,6 +468,9 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
 #ifndef MRT_TRI_PREFETCH
 #define MRT_TRI_PREFETCH 1
 #endif
+#ifndef MRT_TRI_PREFETCH_ANY
+#define MRT_TRI_PREFETCH_ANY MRT_TRI_PREFETCH  // the any-hit (shadow) walk's
+#endif
 #ifndef MRT_SEG_REVERSE
 #define MRT_SEG_REVERSE 1
 #endif
@@ -879,42 +882,31 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
                 }
             }
             bool hit = false;
-#if MRT_TRI_PREFETCH
-            // software-pipelined: triangle k + 1's loads go out before triangle k's test
+            // software-pipelined (kPrefetch): triangle k + 1's loads go out before triangle k's test
+            constexpr bool kPrefetch = kAny ? MRT_TRI_PREFETCH_ANY != 0 : MRT_TRI_PREFETCH != 0;
             float4 ca = a0, cb = b0t, cc = c0;
             for (int k = 0; k < nprim; ++k) {
                 if (kCount) phaseCount(&cnt->triIters, &cnt->triLanes);
                 const int j = first + k;
-                float4 na = ca, nb = cb, nc = cc;
-                if (k + 1 < nprim) {
-                    const uint32_t offn = static_cast<uint32_t>(j + 1) * 48u;
-                    na = bload3(triBuf, offn);
-                    nb = bload3(triBuf, offn + 16u);
-                    nc = bload3(triBuf, offn + 32u);
+                float4 ta = ca, tb = cb, tc = cc;
+                if constexpr (kPrefetch) {
+                    if (k + 1 < nprim) {
+                        const uint32_t offn = static_cast<uint32_t>(j + 1) * 48u;
+                        ca = bload3(triBuf, offn);
+                        cb = bload3(triBuf, offn + 16u);
+                        cc = bload3(triBuf, offn + 32u);
+                    }
+                } else if (k > 0) {
+                    const uint32_t off = static_cast<uint32_t>(j) * 48u;
+                    ta = bload3(triBuf, off);
+                    tb = bload3(triBuf, off + 16u);
+                    tc = bload3(triBuf, off + 32u);
                 }
-                const float4 ta = ca, tb = cb, tc = cc;
-                ca = na;
-                cb = nb;
-                cc = nc;
                 const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
                 if (code == src) continue;
                 float t, u, v;
                 if (kCount) ++cnt->tris;
                 if (!triTest(ta, tb, tc, o, d, &t, &u, &v)) continue;
-#else
-            for (int k = 0; k < nprim; ++k) {
-                if (kCount) phaseCount(&cnt->triIters, &cnt->triLanes);
-                const int j = first + k;
-                const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(j));
-                if (code == src) continue;
-                const uint32_t off = static_cast<uint32_t>(j) * 48u;
-                float t, u, v;
-                if (kCount) ++cnt->tris;
-                const bool f = k == 0;
-                if (!triTest(f ? a0 : bload3(triBuf, off), f ? b0t : bload3(triBuf, off + 16u),
-                             f ? c0 : bload3(triBuf, off + 32u), o, d, &t, &u, &v))
-                    continue;
-#endif
                 if (t < kEpsilon) continue;
                 if (kAny) {
                     if (!(t >= bt)) {
