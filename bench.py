@@ -248,10 +248,11 @@ def pmc_traffic(workload):
 def kernel_roofline(r, step):
     """Per-kernel algorithmic bytes and serialised launch durations (outside the timed region).
 
-    Kernels as the timed frames run them: level 1 is ONE launch, k_trace_packet_shade (camera rays
-    generated, packet-walked and shaded); k_trace is the per-lane closest-hit walk of levels 2 ..
-    maxDepth (level maxDepth + 1 is not walked); k_shade shades levels 2 .. maxDepth; k_shadow walks
-    the shadow rays of every level.  Bytes per level come from one counting frame (which runs level
+    Kernels as the timed frames run them: level 1's camera rays are packet-walked by k_trace_packet
+    (or, with tuning key 17, generated, walked and shaded in one launch, k_trace_packet_shade);
+    k_trace is the per-lane closest-hit walk of levels 2 .. maxDepth (level maxDepth + 1 is not
+    walked); k_shade shades levels 1 (2 when fused) .. maxDepth; k_shadow walks the shadow rays of
+    every level.  Bytes per level come from one counting frame (which runs level
     1 as separate launches: the same walk, counted), durations from two frames with the shadow
     stream serialised and HIP events around every launch on the stream it runs on."""
     r.set_profiling(counting=True)
@@ -262,12 +263,14 @@ def kernel_roofline(r, step):
     keys = ("traceMs", "shadowMs", "shadeMs", "fusedMs", "traceLaunches", "shadowLaunches", "shadeLaunches",
             "fusedLaunches")
     t = dict.fromkeys(keys, 0)
+    t["level1TraceMs"] = 0.0  # level 1's walk: the packet kernel where it is not fused with its shading
     frames = 2
     for _ in range(frames):
         step()
         f = r.frame_stats()
         for k in keys:
             t[k] += f[k]
+        t["level1TraceMs"] += f["levelTraceMs"][0]
     r.set_profiling()
     r.set_tuning(3, 1)
     md = r.config.maxDepth
@@ -276,7 +279,9 @@ def kernel_roofline(r, step):
     nodes, tris, leaves = c["levelNodeRecords"], c["levelTriTests"], c["levelLeafRecords"]
     shaded = c["levelShadedVertices"]
     fused = t["fusedLaunches"] > 0
-    walk_levels = range(1 if fused else 0, md)  # k_trace: depths 2 (1 unfused) .. maxDepth
+    packet = not fused and r.get_tuning(16) != 0  # level 1 by the packet walk in its own launch
+    # k_trace: depths 2 .. maxDepth (depth 1: the packet walk, fused or not), 1 .. without packets
+    walk_levels = range(1 if (fused or packet) else 0, md)
     # k_trace: per ray 32 (ray read: origin, direction) + 16 (hit write) + 32 per node record + 36 per
     # triangle test; `fetched`: the bytes the load instructions request - 16 per child
     # record of the quantized 4-wide tree, 48 per walk-tree leaf record (exact box + certified-cull
@@ -327,11 +332,20 @@ def kernel_roofline(r, step):
                "shadow_tris": c["shadowTriTests"] / max(1, n_sh),
                "shadow_leaves": c["shadowLeafRecords"] / max(1, n_sh), "shaded_vertices": c["shadedVertices"]}
     lv = lambda rng: [l + 1 for l in rng]  # noqa: E731
-    out = {"k_trace": entry(trace_b, t["traceMs"], t["traceLaunches"], trace_f, lv(walk_levels)),
+    # level 1 unfused: its packet walk (k_trace_packet) reads the camera rays k_raygen wrote and writes
+    # the hits; its time is the first level's trace time, its launches one per frame
+    packet_ms = t["level1TraceMs"] if packet else 0.0
+    packet_launches = frames if packet else 0
+    out = {"k_trace": entry(trace_b, t["traceMs"] - packet_ms, t["traceLaunches"] - packet_launches, trace_f,
+                            lv(walk_levels)),
            "k_shadow": entry(shadow_b, t["shadowMs"], t["shadowLaunches"], shadow_f),
            "k_shade": entry(shade_b, t["shadeMs"], t["shadeLaunches"] - t["fusedLaunches"], None, lv(shade_levels))}
     if fused:
         out["k_trace_packet_shade"] = entry(fused_b, t["fusedMs"], t["fusedLaunches"], fused_f, [1])
+    elif packet:
+        packet_b = 48.0 * rays[0] + 32.0 * nodes[0] + 36.0 * tris[0]
+        packet_f = 48.0 * rays[0] + 16.0 * nodes[0] + 48.0 * leaves[0] + 36.0 * tris[0]
+        out["k_trace_packet"] = entry(packet_b, packet_ms, packet_launches, packet_f, [1])
     return out, per_ray
 
 

@@ -489,7 +489,10 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.refill = 32;  // kWalkRefill
     d.leanShade = 1;
     d.packet = r->stackNeed <= kPacketStack ? 1 : 0;  // the packet walk's uniform stack must hold the tree's need
-    d.fuseShade = 1;
+    // level 1's shading in its own launch (tuning key 17 = 0): since round 5's walks at 6 waves per
+    // SIMD the separate launches are faster (C4 14.07 -> 13.81 ms, N = 8 shard 2.55 -> 2.51 ms,
+    // profiles/r05_fused_level1_ab.txt)
+    d.fuseShade = 0;
     d.matsFinite = 1;
     for (const HMaterial& m : sc.materials) {
         for (const v3 c : {m.Kd, m.Ks, m.Kt})

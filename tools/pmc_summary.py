@@ -13,9 +13,11 @@ import csv, glob, json, os, re, sys
 from collections import defaultdict
 
 # the kernels of the timed frames in the default (exact, cull mode 3) configuration, as bench.py's
-# roofline names them: level 1 fused (k_trace_packet_shade), the per-lane closest-hit walk of the
-# deeper levels, the shadow walk and the lean PathTracer shading kernel
+# roofline names them: level 1's packet walk (k_trace_packet; k_trace_packet_shade where level 1 is
+# fused, tuning key 17), the per-lane closest-hit walk of the deeper levels, the shadow walk and the
+# lean PathTracer shading kernel
 PRODUCT = {"k_trace": (r"k_trace<false, 1, 3>",), "k_trace_packet_shade": (r"k_trace_packet_shade<2, 3>",),
+           "k_trace_packet": (r"k_trace_packet<false, 3>",),
            "k_shadow": (r"k_shadow<false, 1, 3>",), "k_shade": (r"k_shade<2, false>",)}
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import kernel_source_stamp, workload_key  # noqa: E402
