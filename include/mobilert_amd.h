@@ -109,7 +109,9 @@ typedef struct mrt_frame_stats {
     uint64_t shadowTriTests;
     double traceMs;         /* profiling: summed duration of closest-hit trace launches */
     double shadowMs;        /* profiling: summed duration of any-hit trace launches */
-    double frameMs;         /* profiling: whole frame on the render stream */
+    double frameMs;         /* whole frame on the render stream, host wall time; a device group: the
+                               group's wall time (the per-kernel ms fields and launch counts are
+                               summed over its shards) */
     int64_t traceLaunches;
     int64_t shadowLaunches;
     double shadeMs;         /* profiling: summed duration of the shading launches */
@@ -140,6 +142,9 @@ typedef struct mrt_frame_stats {
                                       the leaf phase and the triangle loop: {iters, lanes} x 3 x 2; then per
                                       walk, summed over inner iterations, the wave's lanes without a ray
                                       and with a finished one: {idle, done} x 2 */
+    uint64_t packetWaveRecords[3]; /* counting pass only, the level-1 packet walk (scalar loads, each record
+                                      fetched once for the wave's 64 rays): per wave, inner nodes visited
+                                      (128 B each), leaf records loaded (48 B), triangle records loaded (48 B) */
 } mrt_frame_stats;
 
 /* A named byte buffer (a map_Kd texture file handed over by the Android front end). */
@@ -216,9 +221,10 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  * key 16 = camera rays by the wave-coherent packet walk in cull modes 0 and 3 (1, default) or the
  *          per-lane walk (0); refused (-1) when the walk tree needs a deeper traversal stack than
  *          the packet walk's LDS stack (kPacketStack),
- * key 17 = level 1 fused: camera rays generated, packet-walked and shaded in one launch (1, default,
- *          where it applies: BVH, packet walk, Whitted / PathTracer, untextured, lean shading, no
- *          counting) or the separate raygen / walk / shade launches (0),
+ * key 17 = level 1 fused: camera rays generated, packet-walked and shaded in one launch (1, where it
+ *          applies: BVH, packet walk, Whitted / PathTracer, untextured, lean shading, no counting) or
+ *          the separate raygen / walk / shade launches (0, default since round 5: faster with the
+ *          6-wave walks),
  * key 27 = the last shadow walk of a pass on the render stream with the closest-hit spill stacks
  *          (1, default) or on the shadow stream (0),
  * key 28 = at most this many workgroups per walk launch (0, default: the occupancy grid; 1-65536):

@@ -6,7 +6,9 @@
 // with MobileRT::Config from app/MobileRT/Config.hpp:12-83.  This header re-declares the same
 // struct (same members, same order, same types) so a front end built against the reference
 // header links against libmobilert_amd.so unchanged.  GPU-only knobs come from environment
-// variables (MOBILERT_MAX_DEPTH, MOBILERT_DEVICE), see INTEGRATION.md.
+// variables, see INTEGRATION.md: MOBILERT_MAX_DEPTH (RayDepthMax), MOBILERT_DEVICE (the one GPU to
+// render on) and MOBILERT_DEVICES ("0,1,..": a device group - the frame's screen-tile shards spread
+// over these GPUs from one process, as renderFrame spreads it over its workers, Renderer.cpp:62-82).
 #ifndef MOBILERT_AMD_HPP
 #define MOBILERT_AMD_HPP
 

@@ -147,12 +147,20 @@ public:
         c.device = -1;
         // MOBILERT_DEVICES=0,1,...: the frame sharded over these GPUs (mrt_config.devices; the
         // reference's renderFrame spreads a frame over its workers, Renderer.cpp:62-82)
+        // (the same rules and message as the library's own parser, mrt::parseDeviceList: every item a
+        // whole non-negative decimal ordinal)
         std::vector<std::int32_t> devices;
-        if (const char* dl = std::getenv("MOBILERT_DEVICES")) {
+        const char* dl = std::getenv("MOBILERT_DEVICES");
+        if (dl != nullptr && *dl != '\0') {
             std::string item;
             for (const char* q = dl;; ++q) {
+                if (*q == '\0' && item.empty() && q != dl) break;  // a trailing comma ends the list
                 if (*q == ',' || *q == '\0') {
-                    if (!item.empty()) devices.push_back(static_cast<std::int32_t>(std::stoi(item)));
+                    char* end = nullptr;
+                    const long v = std::strtol(item.c_str(), &end, 10);
+                    if (item.empty() || end != item.c_str() + item.size() || v < 0 || v > 0x7fffffffL)
+                        throw std::runtime_error("MOBILERT_DEVICES: bad ordinal '" + item + "'");
+                    devices.push_back(static_cast<std::int32_t>(v));
                     item.clear();
                     if (*q == '\0') break;
                 } else {

@@ -169,7 +169,8 @@ class Renderer:
         out["levelShadowRays"] = list(s.levelShadowRays)
         out["levelTraceMs"] = list(s.levelTraceMs)
         out["levelShadowMs"] = list(s.levelShadowMs)
-        for k in ("levelNodeRecords", "levelTriTests", "levelLeafRecords", "levelShadedVertices", "walkPhases"):
+        for k in ("levelNodeRecords", "levelTriTests", "levelLeafRecords", "levelShadedVertices", "walkPhases",
+                  "packetWaveRecords"):
             out[k] = list(getattr(s, k))
         return out
 

@@ -77,6 +77,7 @@ class MrtFrameStats(ctypes.Structure):
         ("levelShadedVertices", ctypes.c_uint64 * 16),
         ("shadowOccluded", ctypes.c_uint64),
         ("walkPhases", ctypes.c_uint64 * 16),
+        ("packetWaveRecords", ctypes.c_uint64 * 3),
     ]
 
 

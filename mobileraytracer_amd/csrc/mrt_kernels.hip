@@ -290,6 +290,14 @@ __global__ __launch_bounds__(kWalkThreads, 8) void k_trace_packet(DScene s, Leve
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris, kStatLeaves);
         reduceCounts<kCount>(cnt, stats, kStatLevelNodes + level - 1, kStatLevelTris + level - 1, kStatLevelLeaves + level - 1);
+        // the packet's own per-wave records (its per-lane fallback walks count only per lane, above)
+        const uint32_t w[3] = {cnt.innerIters, cnt.leafIters, cnt.triIters};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            unsigned long long x = w[k];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+            if (laneId() == 0 && x != 0) atomicAdd(stats + kStatPacket + k, x);
+        }
         waveLog(cnt, stats, 0, level, t0);
     }
 }
@@ -1102,23 +1110,33 @@ void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream
 // spill stacks were sized for.
 template <typename K>
 int persistentGrid(K kernel, int slot, int maxThreads) {
-    // (atomics: the shards of a device group launch from host threads of their own; every thread
-    // computes the same values)
-    static std::atomic<int> occ[24] = {};
-    static std::atomic<int> cusCache{0};
+    // Cached per device ordinal (a device group's shards launch from host threads of their own, each
+    // with its own device current, and the GPUs of a group may differ in CU count): every thread
+    // that fills an entry computes the same value for that device, so relaxed atomics suffice.
+    constexpr int kDevices = 64;
+    static std::atomic<int> occ[kDevices][24] = {};
+    static std::atomic<int> cusCache[kDevices] = {};
     const int cap = std::max(1, maxThreads / kWalkThreads);
-    int cus = cusCache.load(std::memory_order_relaxed);
-    if (cus == 0) {
-        hipDeviceProp_t prop;
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return cap;
-        cus = prop.multiProcessorCount;
-        cusCache.store(cus, std::memory_order_relaxed);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return cap;
+    hipDeviceProp_t prop;
+    if (dev < 0 || dev >= kDevices) {  // (beyond the cache: asked every time)
+        int o = 0;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, kWalkThreads, 0) != hipSuccess || o <= 0)
+            return cap;
+        return std::min(cap, o * prop.multiProcessorCount);
     }
-    int o = occ[slot].load(std::memory_order_relaxed);
+    int cus = cusCache[dev].load(std::memory_order_relaxed);
+    if (cus == 0) {
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return cap;
+        cus = prop.multiProcessorCount;
+        cusCache[dev].store(cus, std::memory_order_relaxed);
+    }
+    int o = occ[dev][slot].load(std::memory_order_relaxed);
     if (o == 0) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kernel, kWalkThreads, 0) != hipSuccess) o = 0;
-        occ[slot].store(o, std::memory_order_relaxed);
+        occ[dev][slot].store(o, std::memory_order_relaxed);
     }
     return o > 0 ? std::min(cap, o * cus) : cap;
 }

@@ -55,7 +55,10 @@ constexpr int kStatLevelShaded = kStatLevelLeaves + kMaxLevels;  // counting pas
 constexpr int kStatOccluded = kStatLevelShaded + kMaxLevels;  // counting pass: occluded shadow rays
 constexpr int kStatPhases = kStatOccluded + 1;  // counting pass: 2 walks x {inner, leaf, triangle} x {iterations, lanes},
                                                 // then 2 walks x inner {idle, done} lanes
-constexpr int kNumStats = kStatPhases + 16;
+// counting pass, the level-1 packet walk, per wave (scalar loads: each record fetched once for the
+// wave's rays): inner nodes visited, leaf records loaded, triangle records loaded
+constexpr int kStatPacket = kStatPhases + 16;
+constexpr int kNumStats = kStatPacket + 3;
 // counting builds: per walk launch (closest / any-hit x level) and wave {start, end (100 MHz
 // ticks), rays fetched, child records fetched}, after the statistics (mrt_wave_log)
 constexpr int kWaveLogWaves = 8192;

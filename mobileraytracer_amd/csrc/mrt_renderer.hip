@@ -5,6 +5,8 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -92,15 +94,100 @@ std::vector<int32_t> mrt::parseDeviceList(const char* s) {
     std::string item;
     std::istringstream in(s);
     while (std::getline(in, item, ',')) {
-        size_t used = 0;
-        const int v = std::stoi(item, &used);
-        if (used != item.size() || v < 0) throw std::runtime_error(std::string("MOBILERT_DEVICES: bad ordinal '") + item + "'");
-        out.push_back(v);
+        char* end = nullptr;
+        const long v = std::strtol(item.c_str(), &end, 10);
+        if (item.empty() || end != item.c_str() + item.size() || v < 0 || v > 0x7fffffffL)
+            throw std::runtime_error(std::string("MOBILERT_DEVICES: bad ordinal '") + item + "'");
+        out.push_back(static_cast<int32_t>(v));
     }
     return out;
 }
 
 namespace {
+
+// The shard workers of a device group: one long-lived host thread per shard 1..n-1, bound to its
+// shard's GPU once (hipSetDevice is per thread), woken per frame (or per sample in progressive
+// mode) to run that frame's work for its shard; shard 0 runs in the calling thread.  Replaces a
+// std::thread per shard and frame (creation, join and hipSetDevice on every frame).
+class ShardPool {
+public:
+    explicit ShardPool(const std::vector<int>& devices) : n_(static_cast<int>(devices.size())), err_(devices.size()) {
+        for (int i = 1; i < n_; ++i) th_.emplace_back([this, i, d = devices[static_cast<size_t>(i)]] { loop(i, d); });
+    }
+    ~ShardPool() {
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            quit_ = true;
+        }
+        wake_.notify_all();
+        for (std::thread& t : th_) t.join();
+    }
+    ShardPool(const ShardPool&) = delete;
+    ShardPool& operator=(const ShardPool&) = delete;
+
+    // job(i) for every shard i: 1..n-1 on the workers, 0 in the calling thread; returns when all
+    // are done, then rethrows the first failure (in shard order)
+    void run(const std::function<void(int)>& job) {
+        std::lock_guard<std::mutex> serial(runMu_);  // one frame of the group at a time
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            job_ = &job;
+            for (std::exception_ptr& e : err_) e = nullptr;
+            pending_ = n_ - 1;
+            ++gen_;
+        }
+        wake_.notify_all();
+        try {
+            job(0);
+        } catch (...) {
+            err_[0] = std::current_exception();
+        }
+        {
+            std::unique_lock<std::mutex> lock(mu_);
+            done_.wait(lock, [this] { return pending_ == 0; });
+            job_ = nullptr;
+        }
+        for (const std::exception_ptr& e : err_)
+            if (e) std::rethrow_exception(e);
+    }
+
+private:
+    void loop(int i, int device) {
+        const hipError_t bound = hipSetDevice(device);
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* job = nullptr;
+            {
+                std::unique_lock<std::mutex> lock(mu_);
+                wake_.wait(lock, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                job = job_;
+            }
+            try {
+                if (bound != hipSuccess)
+                    throw std::runtime_error(std::string("shard worker: hipSetDevice: ") + hipGetErrorString(bound));
+                (*job)(i);
+            } catch (...) {
+                err_[static_cast<size_t>(i)] = std::current_exception();
+            }
+            {
+                std::lock_guard<std::mutex> lock(mu_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+
+    const int n_;
+    std::mutex runMu_, mu_;
+    std::condition_variable wake_, done_;
+    std::vector<std::thread> th_;
+    std::vector<std::exception_ptr> err_;
+    const std::function<void(int)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool quit_ = false;
+};
 
 }  // namespace
 
@@ -191,6 +278,7 @@ struct mrt_renderer {
     std::vector<std::unique_ptr<mrt_renderer>> peers;
     int32_t* dOwnPacked = nullptr;
     int32_t* dGathered = nullptr;
+    std::unique_ptr<ShardPool> shardPool;  // the head's shard workers (declared after peers: stopped first)
 
     ~mrt_renderer() {
         if (hostStats != nullptr) (void)hipHostFree(hostStats);
@@ -817,6 +905,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     fs->shadowTriTests += hs[kStatTrisShadow];
     fs->shadowOccluded += hs[kStatOccluded];
     for (int k = 0; k < 16; ++k) fs->walkPhases[k] += hs[kStatPhases + k];
+    for (int k = 0; k < 3; ++k) fs->packetWaveRecords[k] += hs[kStatPacket + k];
     fs->leafRecords += hs[kStatLeaves];
     fs->shadowLeafRecords += hs[kStatLeavesShadow];
     for (int l = 0; l < kMaxLevels && l < 16; ++l) {
@@ -873,6 +962,7 @@ void addStats(mrt_frame_stats& a, const mrt_frame_stats& b) {
     a.leafRecords += b.leafRecords;
     a.shadowOccluded += b.shadowOccluded;
     for (int k = 0; k < 16; ++k) a.walkPhases[k] += b.walkPhases[k];
+    for (int k = 0; k < 3; ++k) a.packetWaveRecords[k] += b.packetWaveRecords[k];
     a.shadowLeafRecords += b.shadowLeafRecords;
     a.fusedMs += b.fusedMs;
     a.fusedLaunches += b.fusedLaunches;
@@ -994,32 +1084,12 @@ void unpackGathered(const mrt_renderer* r, const int32_t* dGathered, int32_t* dB
 mrt_renderer* shardOf(mrt_renderer* r, int i) { return i == 0 ? r : r->peers[static_cast<size_t>(i - 1)].get(); }
 int groupSize(const mrt_renderer* r) { return 1 + static_cast<int>(r->peers.size()); }
 
-// f(shard, i) for every shard of the group, shard i from a host thread with its device current
-// (shard 0 in the calling thread); the first failure is rethrown after all have finished
+// f(shard, i) for every shard of the group, shard i on the head's shard worker i (bound to its
+// device; shard 0 in the calling thread); the first failure is rethrown after all have finished
 template <class F>
 void forEachShard(mrt_renderer* r, F&& f) {
-    const int n = groupSize(r);
-    std::vector<std::exception_ptr> err(static_cast<size_t>(n));
-    std::vector<std::thread> th;
-    for (int i = 1; i < n; ++i)
-        th.emplace_back([&, i] {
-            try {
-                mrt_renderer* p = shardOf(r, i);
-                MRT_HIP(hipSetDevice(p->device));
-                f(p, i);
-            } catch (...) {
-                err[static_cast<size_t>(i)] = std::current_exception();
-            }
-        });
-    try {
-        MRT_HIP(hipSetDevice(r->device));
-        f(r, 0);
-    } catch (...) {
-        err[0] = std::current_exception();
-    }
-    for (std::thread& t : th) t.join();
-    for (const std::exception_ptr& e : err)
-        if (e) std::rethrow_exception(e);
+    MRT_HIP(hipSetDevice(r->device));
+    r->shardPool->run([&](int i) { f(shardOf(r, i), i); });
 }
 
 // The shards' packed pixels into the head's gather buffer (peer copies over xGMI; a shard on the
@@ -1046,6 +1116,7 @@ void assembleGroup(mrt_renderer* r, int32_t* dBitmap, hipStream_t st) {
 void renderGroupFrame(mrt_renderer* r, int32_t* dBitmap, hipStream_t st, int32_t* hostBitmap) {
     r->sample.store(0);
     if (r->stopFlag.load()) return;
+    const auto t0 = std::chrono::steady_clock::now();
     const int n = groupSize(r);
     const int spp = std::max(1, r->cfg.samplesPixel);
     const size_t npx = static_cast<size_t>(r->cfg.width) * static_cast<size_t>(r->cfg.height);
@@ -1077,6 +1148,10 @@ void renderGroupFrame(mrt_renderer* r, int32_t* dBitmap, hipStream_t st, int32_t
     }
     mrt_frame_stats fs{};
     for (const mrt_frame_stats& x : shardStats) addStats(fs, x);
+    // the group's frame time is its wall time (the shards run at the same time), not the shards' sum:
+    // until every shard has finished and the assembly is queued; the per-kernel durations stay summed
+    // over the shards (mrt_frame_stats)
+    fs.frameMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     r->last = fs;
     r->totalRays.store(rays0 + fs.rays + fs.shadowRays);
 }
@@ -1223,6 +1298,7 @@ mrt_renderer* createGroup(const mrt_config* cfg, const MemScene* mem) {
         }
         head->peers.push_back(std::move(shards[static_cast<size_t>(i)]));
     }
+    head->shardPool = std::make_unique<ShardPool>(std::vector<int>(cfg->devices, cfg->devices + n));
     return head.release();
 }
 

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <future>
 #include <fstream>
 #include <memory>
 #include <mutex>
@@ -1566,8 +1567,9 @@ std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int ro
         }
     }
     // The walk's traversal stack grows with the tree's depth (3 pushes per wide level at most; entries
-    // past the LDS part spill to global memory, and the packet walk's stack is bounded), so an
-    // insertion may not make the tree deeper than the sweep built it.
+    // past the LDS part spill to global memory, and the packet walk's stack is bounded), so a
+    // bounded optimisation searches only positions that keep the tree within the sweep's height (the
+    // fallbacks below usually do too; walkTreeBuild rejects any result whose wide tree is deeper).
     const int32_t maxHeight = bounded ? t[0].height : std::numeric_limits<int32_t>::max() / 4;
     auto total = [&]() {
         double a = 0.0;
@@ -1576,7 +1578,8 @@ std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int ro
         return a;
     };
     // the best sibling for subtree x: minimal area of the new parent plus the growth of every ancestor
-    // (fallback: the position x came from, which keeps the height)
+    // within the height bound (fallback, when the bounded search finds none: a position that keeps
+    // the height, chosen by the caller below)
     auto bestSibling = [&](int32_t x, int32_t fallback) {
         const HAABB bx = t[static_cast<size_t>(x)].box;
         const double ax = area(bx);
@@ -1671,8 +1674,16 @@ std::vector<HBVHNode> optimizeOverLeaves(const std::vector<HBVHNode>& in, int ro
             t[static_cast<size_t>(x1)].parent = -1;
             t[static_cast<size_t>(x2)].parent = -1;
             nv.l = nv.r = -1;
+            // Fallbacks that keep every height at most what it was before v was taken out: sib now
+            // stands where p stood, so x1 beside sib sits one level higher than under v.  If x1 went
+            // there, x2 beside x1 rebuilds the old shape (sib beside the pair x1, x2); if x1 went
+            // elsewhere, x2 beside sib is one level higher than under v - unless x1 went into sib's
+            // subtree, whose new height the search checked at sib's depth, not one below.  So the
+            // fallbacks usually keep the bound; the guarantee is walkTreeBuild's check of the wide
+            // tree's depth, which rejects an optimised tree deeper than the sweep's.
             insertAt(x1, bestSibling(x1, sib), v);
-            insertAt(x2, bestSibling(x2, x1), p);
+            const bool pairAtP = t[static_cast<size_t>(v)].l == sib && t[static_cast<size_t>(v)].r == x1;
+            insertAt(x2, bestSibling(x2, pairAtP ? x1 : sib), p);
         }
         const double next = total();
         stale = next > cur * kTreeOptStop ? stale + 1 : 0;
@@ -1855,28 +1866,44 @@ std::vector<HBVHNode> walkTreeOver(const std::vector<HBVHNode>& ref) {
     const int rotSweeps = rot != nullptr ? std::atoi(rot) : kTreeRotSweeps;
     // Renderers of one scene in one process (a device group's shards, a front end re-creating its
     // renderer, the test suite) share the tree: built once per (reference tree, settings), a few
-    // seconds for the conference stand-in.  The key is the whole reference tree's bytes.
+    // seconds for the conference stand-in.  The key is the whole reference tree's bytes.  A build
+    // in flight is shared too: the shards of a device group are created concurrently, and the
+    // first to miss builds while the others wait on its future.
+    using Tree = std::shared_ptr<const std::vector<HBVHNode>>;
     std::string key(reinterpret_cast<const char*>(ref.data()), ref.size() * sizeof(HBVHNode));
     key.append(reinterpret_cast<const char*>(&rounds), sizeof(rounds));
     key.append(reinterpret_cast<const char*>(&rotSweeps), sizeof(rotSweeps));
     static std::mutex mu;
-    static std::unordered_map<std::string, std::shared_ptr<const std::vector<HBVHNode>>> cache;
+    static std::unordered_map<std::string, std::shared_future<Tree>> cache;
     static std::deque<std::string> order;  // least recently built first: at most kTreeCacheScenes kept
+    std::promise<Tree> mine;
+    std::shared_future<Tree> pending;
     {
         std::lock_guard<std::mutex> lock(mu);
         const auto it = cache.find(key);
-        if (it != cache.end()) return *it->second;
-    }
-    auto tree = std::make_shared<const std::vector<HBVHNode>>(walkTreeBuild(ref, rounds, rotSweeps));
-    std::lock_guard<std::mutex> lock(mu);
-    if (cache.emplace(key, tree).second) {
-        order.push_back(key);
-        while (order.size() > kTreeCacheScenes) {
-            cache.erase(order.front());
-            order.pop_front();
+        if (it != cache.end()) {
+            pending = it->second;
+        } else {
+            cache.emplace(key, mine.get_future().share());
+            order.push_back(key);
+            while (order.size() > kTreeCacheScenes) {  // (a waiter holds its own copy of the future)
+                cache.erase(order.front());
+                order.pop_front();
+            }
         }
     }
-    return *tree;
+    if (pending.valid()) return *pending.get();  // built, or being built by another thread
+    try {
+        Tree tree = std::make_shared<const std::vector<HBVHNode>>(walkTreeBuild(ref, rounds, rotSweeps));
+        mine.set_value(tree);
+        return *tree;
+    } catch (...) {
+        mine.set_exception(std::current_exception());  // the waiters see the failure too ...
+        std::lock_guard<std::mutex> lock(mu);          // ... and a later call builds again
+        cache.erase(key);
+        order.erase(std::remove(order.begin(), order.end(), key), order.end());
+        throw;
+    }
 }
 
 std::vector<uint32_t> triangleConeWords(const std::vector<HBVHNode>& nodes, const std::vector<HTriangle>& tris) {

@@ -183,6 +183,7 @@ __device__ __forceinline__ void tracePacketF(const DScene& s, const float4* __re
         while (ref != kRefDone) {
             if (ref >= 0) {  // ---- inner node: four children, entered on any lane's hit ----
                 // the node's float grid indices (DScene::triQNodesF): one scalar round trip
+                if (kCount && lane == 0) ++cnt->innerIters;  // per wave: 128 B through the scalar cache
                 float4 nf[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) nf[j] = sload4f(qnf + 32 * ref + 4 * j);
@@ -258,6 +259,10 @@ __device__ __forceinline__ void tracePacketF(const DScene& s, const float4* __re
             const int lastTri = r.count - 1;
             const float4 b0 = sload4f(lb + 12 * first), b1 = sload4f(lb + 12 * first + 4), b2 = sload4f(lb + 12 * first + 8);
             PacketTri tri0 = loadPacketTri(tg, first), tri1 = loadPacketTri(tg, min(first + 1, lastTri));
+            if (kCount && lane == 0) {  // per wave: the 48-B leaf record and two 48-B triangle records
+                ++cnt->leafIters;
+                cnt->triIters += 2u;
+            }
             pinSgprs(b0);
             pinSgprs(b1);
             pinSgprs(b2);
@@ -274,6 +279,7 @@ __device__ __forceinline__ void tracePacketF(const DScene& s, const float4* __re
             if (__ballot(test) != 0) {
                 for (int k = 0; k < nprim; k += 2) {
                     if (k > 0) {
+                        if (kCount && lane == 0) cnt->triIters += 2u;
                         tri0 = loadPacketTri(tg, first + k);
                         tri1 = loadPacketTri(tg, min(first + k + 1, lastTri));
                         tri0.pin();

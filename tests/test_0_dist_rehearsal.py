@@ -75,3 +75,20 @@ def test_two_rank_bench_assembles_the_single_gpu_frame(tmp_path, oracle_mod):
     jr = json.loads(line_r)
     assert "RCCL gather" in jr["config"]["parallelism"], jr["config"]["parallelism"]
     assert np.array_equal(img, one), int((img != one).sum())
+
+
+def test_group_bench_assembles_the_single_gpu_frame(tmp_path):
+    """`bench.py --gpus 4 --path group`: the front ends' multi-GPU path (one process, one Renderer
+    over a device group, MOBILERT_DEVICES) with the ordinal repeated on the one-GPU box; the
+    assembled bitmap equals the single-GPU bench's frame."""
+    import json
+    import torch
+    assert not torch.cuda.is_initialized(), "must run before this process touches the GPU"
+    one, _ = _bench(str(tmp_path), "one_g", 1)
+    grp, line = _bench(str(tmp_path), "group", 4, launcher=False, extra_env={"MOBILERT_DEVICES": "0,0,0,0"},
+                       extra_args=("--path", "group", "--steps", "2", "--warmup", "1"))
+    j = json.loads(line)
+    assert j["n_gpus"] == 4 and j["config"]["parallelism"].startswith("device group x4"), j["config"]
+    assert j["config"]["devices"] == [0, 0, 0, 0]
+    assert j["value"] > 0 and j["roofline"]["kernels"]["k_trace"]["avg_launch_ms"] > 0
+    assert np.array_equal(grp, one), int((grp != one).sum())

@@ -51,3 +51,25 @@ def test_cli_refuses_before_touching_a_gpu():
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=REPO, env=dict(env, WORLD_SIZE="3"),
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2 and "WORLD_SIZE=3" in p.stderr, p.stderr[-2000:]
+
+
+def test_group_path_runs_in_one_process():
+    from bench import group_devices
+    # --path group: one process for the whole device group, never spawned
+    assert launch_plan(4, {}, 4, "group") == ("run", None)
+    assert launch_plan(4, {"MOBILERT_DEVICES": "0,0,0,0"}, 1, "group") == ("run", None)  # one-GPU rehearsal
+    assert group_devices(3, {}) == [0, 1, 2]
+    assert group_devices(4, {"MOBILERT_DEVICES": "0,0,0,0"}) == [0, 0, 0, 0]
+
+
+def test_group_path_refuses_bad_device_lists():
+    act, msg = launch_plan(4, {}, 2, "group")
+    assert act == "error" and "2 visible" in msg
+    act, msg = launch_plan(4, {"MOBILERT_DEVICES": "0,0"}, 1, "group")
+    assert act == "error" and "lists 2" in msg
+    act, msg = launch_plan(2, {"MOBILERT_DEVICES": "0,1x"}, 8, "group")
+    assert act == "error" and "bad ordinal '1x'" in msg
+    act, msg = launch_plan(2, {"MOBILERT_DEVICES": "0,-1"}, 8, "group")
+    assert act == "error" and "bad ordinal" in msg
+    act, msg = launch_plan(2, {"WORLD_SIZE": "2"}, 8, "group")
+    assert act == "error" and "without a launcher" in msg

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 5: the GPU test suite (optionally a -k selection), then the bench line.
-# usage: tools/r5_check.sh NAME [pytest -k expression]
+# The GPU test suite (optionally a -k selection), then the bench line.
+# usage: tools/check.sh NAME [pytest -k expression]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; R=$(pwd)
-OUT=$R/gpurun_out/${1:-r5}; mkdir -p $OUT
+OUT=$R/gpurun_out/${1:-check}; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 python -c "from mobileraytracer_amd import _native as n; assert n.build_is_current(), 'stale libmobilert_amd.so'" || exit 2
 if [ "${SKIP_TESTS:-0}" != "1" ]; then

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Flat-geometry stand-in rehearsal (verdict r4 item 7): PMC passes keyed to the flat workload, the
+# Flat-geometry stand-in rehearsal: PMC passes keyed to the flat workload, the
 # phase occupancy of both stand-ins, and the flat bench line.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; R=$(pwd)
-N=${1:-r5flat}; OUT=$R/gpurun_out/$N; mkdir -p $OUT
+N=${1:-flat}; OUT=$R/gpurun_out/$N; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 python -c "from mobileraytracer_amd import _native as n; assert n.build_is_current(), 'stale libmobilert_amd.so'" || exit 2
 timeout -k 10 200 python bench.py --scene flat --no-cpu-baseline > $OUT/flat.log 2>&1 || { tail $OUT/flat.log; exit 3; }
