@@ -308,7 +308,7 @@ def issue_fractions(ctr):
     return out or None
 
 
-def kernel_roofline(r, step):
+def kernel_roofline(r, step, overlap=1):
     """Per-kernel algorithmic bytes and serialised launch durations (outside the timed region).
 
     Kernels as the timed frames run them: level 1's camera rays are packet-walked by k_trace_packet
@@ -341,8 +341,10 @@ def kernel_roofline(r, step):
 
     t = timed_frames(0)
     # the same launches in product frames (the shadow walk beside the next level's walk and shading):
-    # each launch's time on its own stream, stretched by what shares the GPU with it
-    t_ov = timed_frames(1)
+    # each launch's time on its own stream, stretched by what shares the GPU with it.  (With
+    # --overlap 0 the product frames are the serialised ones: no second pass, so a rocprofv3 summary of
+    # such a run holds only serialised launches and recomputes avg_launch_ms.)
+    t_ov = timed_frames(1) if overlap else t
     r.set_tuning(3, 1)
     md = r.config.maxDepth
     rays = c["levelRays"]          # index l - 1: rays of depth l
@@ -524,7 +526,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    kernels, per_ray = kernel_roofline(r, step)
+    kernels, per_ray = kernel_roofline(r, step, args.overlap)
     r.set_tuning(3, args.overlap)
 
     if dist_on:
@@ -668,6 +670,13 @@ def main():
             # bounces)
             "measured_ceilings_gbs": {"divergent_64B_records_32MiB": 6648.4, "wave_coherent_64B_records_32MiB": 27859.6},
             "durations": "serialised frames (shadow stream off), HIP events on the render stream",
+            # the same kernel in the product frames (shadow walks beside it): slower per launch
+            "frac_overlapped": dom.get("frac_overlapped"),
+            "avg_launch_ms_overlapped": dom.get("avg_launch_ms_overlapped"),
+            # the rocprofv3 summaries these durations agree with (tools/final.sh): a run whose frames are
+            # all serialised (--overlap 0) for avg_launch_ms, the default run for the overlapped figure
+            "rocprof_summaries": {"serialised": "profiles/r06_kernel_stats_serial.csv",
+                                  "product_frames": "profiles/r06_kernel_stats.csv"},
             "kernels": kernels,
         },
         "cpu_baseline": None,
