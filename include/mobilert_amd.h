@@ -229,9 +229,10 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  *          (1, default) or on the shadow stream (0),
  * key 28 = at most this many workgroups per walk launch (0, default: the occupancy grid; 1-65536):
  *          a test knob, every grid size walks every ray.
- * (Keys 4, 12-15, 18, 19-25, 29, 30 - binned emission, queue sorting, graph replay, the tile kernel,
- * a shadow-occluder probe, the deeper levels' walk and shading in one launch, a CU-masked shadow
- * stream, k_shade's vertices binned by shading class - measured slower and were removed.) */
+ * (Keys 4, 12-15, 18, 19-25, 29, 30, 32 - binned emission, queue sorting, graph replay, the tile
+ * kernel, a shadow-occluder probe, the deeper levels' walk and shading in one launch, a CU-masked
+ * shadow stream, k_shade's vertices binned by shading class, the shadow walks yielding to the next
+ * level's shading - measured slower and were removed.) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /

@@ -305,12 +305,6 @@ __global__ __launch_bounds__(kWalkThreads, 8) void k_trace_packet(DScene s, Leve
 template <bool kCount, int kVariant, int kCull>
 __global__ __launch_bounds__(kWalkThreads, MRT_SHADOW_WAVES) void k_shadow(DScene s, Level lv, int* counters, int level,
                                                              int2* gstack, int gdepth, unsigned long long* stats) {
-    // level: the depth in its low 8 bits; above them the level whose shading this walk yields to
-    // (0: none; tuning key 32): once that k_shade has started, the waves take no more rays, finish
-    // the ones they hold and exit, and a later launch of the same level takes the rest from the
-    // same cursors (every ray is walked exactly once, by whichever launch claimed it)
-    const int yieldAt = level >> 8;
-    level &= 255;
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
     const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -321,8 +315,7 @@ __global__ __launch_bounds__(kWalkThreads, MRT_SHADOW_WAVES) void k_shadow(DScen
         __shared__ QNode4 ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest,
-                                             yieldAt > 0 ? counters + kCntShading : nullptr, yieldAt);
+        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest);
     }
     while (kVariant == 0) {
         int base = 0;
@@ -683,9 +676,6 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
     }
     const float4* const mats = kFull ? s.mats : tab;
     const float4* const lights = kFull ? s.lights : tab + 4 * s.nMats;
-    // this level's shading has started: a shadow walk beside it that yields (tuning key 32) stops
-    // taking rays (agent scope: the walk reads it on other XCDs while this kernel runs)
-    if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(counters + kCntShading, level, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int count = min(counters[cntRays(level)], lv.cap);
     // {rays of level+1, shadow rays of level}: one 64-bit allocation per block and iteration
     auto* pair = reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1));
@@ -1197,10 +1187,10 @@ void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st, int gridPct) {
     if (s.accel != kAccBVH) {
-        hipLaunchKernelGGL((k_trace_other<true>), dim3(1024), dim3(256), 0, st, s, lv, counters, level & 255);
+        hipLaunchKernelGGL((k_trace_other<true>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }
-    MRT_LAUNCH_WALK(k_shadow, 5);  // (level: k_shadow decodes the yield level above its low 8 bits)
+    MRT_LAUNCH_WALK(k_shadow, 5);
 }
 
 bool canFuseLevel1(int shader, const DScene& s, const ShadeArgs& a) {

@@ -22,9 +22,6 @@ constexpr int kTopNodesMax = 64 * 4 / kWalkWidth;  // walk-tree nodes numbered b
 // adjacent ints so k_shade allocates both with one 64-bit atomic per block.
 constexpr int kCntPairs = 0;                          // 2 * (kMaxLevels + 1) ints
 constexpr int kCntOverflow = 64;
-// the level whose k_shade has started (written by its first block; the shadow walks' cooperative
-// yield reads it, tuning key 32); on its own 128-byte line
-constexpr int kCntShading = 96;
 constexpr int kPacketStack = 128;  // the packet walk's wave-uniform stack entries (mrt_trace_packet.hpp)
 constexpr int kMaxFetchShards = 8;                    // work cursors per level (one per XCD group)
 constexpr int kFetchStride = 32;                      // ints between cursors (a 128-byte line each)

@@ -257,7 +257,6 @@ struct mrt_renderer {
     bool fusedL1 = false;                // the last pass ran level 1 as k_trace_packet_shade
     int lastShadowRender = 1;            // tuning key 27: the last shadow walk on the render stream
     int walkGridCap = 0;                 // tuning key 28: at most this many workgroups per walk launch (0: none)
-    int shadowYield = 0;                 // tuning key 32: a shadow walk yields to the next level's shading
     unsigned long long* hostStats = nullptr;  // pinned: the per-pass statistics read back by DMA
 
     // host copies for the GL preview of the Android front end (mrt_preview_arrays; kept only for
@@ -814,15 +813,6 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // is skipped, or follows it on the same stream), so it may overlap the previous level's
         // shadow walk, still running on the shadow stream.
         const bool lastOnRender = r->lastShadowRender != 0 && sb != st && nLevels >= 2;
-        // Cooperative yield (tuning key 32; not in profiling frames, whose events pair one shadow launch
-        // per level): the shadow walk of level l stops taking rays once level l + 1's shading has
-        // started (k_shade's first block publishes its level), so that shading runs on the whole GPU;
-        // after that shading a continuation launch of level l, on the shadow stream, walks the rest from
-        // the same cursors.  The last walk on the shadow stream does not yield.
-        const int lastSb = lastOnRender ? nLevels - 2 : nLevels - 1;
-        const bool yieldOn = r->shadowYield != 0 && sb != st && !timing && !counting && r->ds.accel == kAccBVH &&
-                             r->ds.variant == 1;
-        int pendingCont = 0;  // the level whose yielded walk awaits its continuation
         if (sb != st) {
             const hipEvent_t start = syncEvent(pp, sync++);
             MRT_HIP(hipEventRecord(start, st));
@@ -857,28 +847,17 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 MRT_HIP(hipEventRecord(shaded, st));
                 MRT_HIP(hipStreamWaitEvent(sb, shaded, 0));
             }
-            if (pendingCont > 0) {  // (on the shadow stream, after this level's shading: the wait above)
-                launchShadow(r->ds, pp.levels[pendingCont], pp.counters, pendingCont, pp.gstackShadow, r->gdepth,
-                             pp.stats, counting, walkThreads, sb, shadowPct);
-                shadowDone[pendingCont] = syncEvent(pp, sync++);
-                MRT_HIP(hipEventRecord(shadowDone[pendingCont], sb));
-                pendingCont = 0;
-            }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ss));
             // the last level (depth > RayDepthMax) shades nothing: no shadow rays
-            const bool yields = yieldOn && !onRender && l < lastSb;
             if (l < nLevels) {
                 // the last shadow walk runs alone: a large shard gives it the full grid (C4 N = 1:
                 // 13.34 -> 13.29 ms); a small one keeps the narrow grid (N = 8: 2.53 vs 2.55 ms)
                 const bool lastAlone = l + 1 == nLevels && r->shadowGridPct == 0 && pathsPerLane >= 8.0;
-                launchShadow(r->ds, pp.levels[l], pp.counters, yields ? l | ((l + 1) << 8) : l,
-                             onRender ? pp.gstack : pp.gstackShadow, r->gdepth, pp.stats, counting, walkThreads, ss,
-                             lastAlone ? 100 : shadowPct);
+                launchShadow(r->ds, pp.levels[l], pp.counters, l, onRender ? pp.gstack : pp.gstackShadow, r->gdepth,
+                             pp.stats, counting, walkThreads, ss, lastAlone ? 100 : shadowPct);
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), ss));
-            if (yields && l < nLevels) {
-                pendingCont = l;  // shadowDone[l] after its continuation
-            } else if (sb != st && !onRender) {
+            if (sb != st && !onRender) {
                 shadowDone[l] = syncEvent(pp, sync++);
                 MRT_HIP(hipEventRecord(shadowDone[l], sb));
             }
@@ -1633,10 +1612,6 @@ static int setTuningOne(mrt_renderer* r, int32_t key, int32_t value) {
         r->shadowGridPct = value;
         return 0;
     }
-    if (key == 32 && (value == 0 || value == 1)) {
-        r->shadowYield = value;
-        return 0;
-    }
     gLastError = "unknown tuning key/value";
     return -1;
 }
@@ -1802,7 +1777,6 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 17: *value = r->ds.fuseShade; return 0;
         case 27: *value = r->lastShadowRender; return 0;
         case 28: *value = r->walkGridCap; return 0;
-        case 32: *value = r->shadowYield; return 0;
         default: break;
     }
     gLastError = "unknown tuning key";

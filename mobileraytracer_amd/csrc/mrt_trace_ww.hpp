@@ -507,13 +507,8 @@ struct LevelQueue {
     int seg = static_cast<int>(blockIdx.x % kWalkShards);  // wave-uniform cursor state
     int segsLeft = walkSegments();
     int shift;  // the cursors' chunks: 2^shift rays
-    // cooperative yield (k_shadow, tuning key 32): no more rays once *yieldFlag >= yieldAt
-    const int* yieldFlag = nullptr;
-    int yieldAt = 0;
-    __device__ __forceinline__ LevelQueue(const float4* o_, const float4* d_, float4* out_, int count_, int* fetch_,
-                                          const int* yieldFlag_ = nullptr, int yieldAt_ = 0)
-        : rO(o_), rD(d_), out(out_), count(count_), fetch(fetch_), shift(segChunkShift(count_, kSegChunkLog)),
-          yieldFlag(yieldFlag_), yieldAt(yieldAt_) {}
+    __device__ __forceinline__ LevelQueue(const float4* o_, const float4* d_, float4* out_, int count_, int* fetch_)
+        : rO(o_), rD(d_), out(out_), count(count_), fetch(fetch_), shift(segChunkShift(count_, kSegChunkLog)) {}
     __device__ __forceinline__ float4 o(int i) const { return rO[i]; }
     __device__ __forceinline__ float4 d(int i) const { return rD[i]; }
     __device__ __forceinline__ void hit(int i, float4 h) const { out[i] = h; }
@@ -522,9 +517,6 @@ struct LevelQueue {
     __device__ __forceinline__ int take(uint64_t pending) {
         const int lane = static_cast<int>(threadIdx.x & 63u);
         int got = -1;
-        if (yieldFlag != nullptr && segsLeft > 0 &&
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(yieldFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= yieldAt)
-            segsLeft = 0;  // the queue counts as drained for this launch: tail donation, then exit
         while (pending != 0 && segsLeft > 0) {
             const int n = __popcll(pending);
             const int leader = __ffsll(static_cast<unsigned long long>(pending)) - 1;
@@ -955,9 +947,8 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
 template <bool kAny, bool kCount, int kCull, class Stack>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
                                                 const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                Stack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest,
-                                                const int* yieldFlag = nullptr, int yieldAt = 0) {
-    LevelQueue q(rOs, rDs, out, count, fetch, yieldFlag, yieldAt);
+                                                Stack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest) {
+    LevelQueue q(rOs, rDs, out, count, fetch);
     traceWhileWhileQ<kAny, kCount, kCull>(s, q, st, cnt, ldsTop, tailBest);
 }
 

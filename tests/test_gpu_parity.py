@@ -330,35 +330,6 @@ def test_shadow_stream_overlap_is_invariant():
             assert np.array_equal(bm, outs[0][0]) and rays == outs[0][1] and shadows == outs[0][2]
 
 
-def test_shadow_yield_is_invariant():
-    """The shadow walks' cooperative yield (tuning key 32: a walk stops taking rays once the next
-    level's shading has started, and a continuation launch walks the rest from the same cursors)
-    changes nothing: bitmaps and ray counts equal the non-yielding frames, with the last shadow
-    walk on either stream (key 27), a narrow shadow grid (key 6), and on the C4 frame itself, whose
-    shadow walks run beside the next level's shading."""
-    import mobileraytracer_amd as m
-    cases = ((make_cfg(1920, 1080, shader=2, scene="conference", spp=4, max_depth=5), ()),
-             (make_cfg(480, 272, shader=2, scene="conference", spp=4, max_depth=5), ((27, 0),)),
-             (make_cfg(480, 272, shader=2, scene="conference", spp=2, max_depth=6), ((6, 30),)),
-             (make_cfg(256, 256, shader=1, scene="water", max_depth=5), ()),
-             (make_cfg(128, 128, shader=2, scene="water", spp=2, max_depth=4, spl=3), ()))
-    for cfg, extra in cases:
-        outs = []
-        with m.Renderer(cfg) as r:
-            for k, v in extra:
-                r.set_tuning(k, v)
-            for y in (0, 1, 0, 1):
-                r.set_tuning(32, y)
-                assert r.get_tuning(32) == y
-                bm = np.zeros(cfg.width * cfg.height, np.int32)
-                r.render_frame(bm)
-                st = r.frame_stats()
-                outs.append((bm, st["rays"], st["shadowRays"], list(st["levelRays"]), list(st["levelShadowRays"])))
-        for other in outs[1:]:
-            assert np.array_equal(outs[0][0], other[0]), (cfg.width, cfg.height, extra)
-            assert outs[0][1:] == other[1:], (cfg.width, cfg.height, extra)
-
-
 def test_shadow_order_is_invariant():
     """The shadow walk's child order (key 5: near or far first) only changes which occluder is
     found first: every pixel, ray count and shadow-ray count is the same, for Whitted (3-child
