@@ -474,6 +474,21 @@ __device__ __forceinline__ void stageTop(const DScene& s, QNode4* ldsTop) {
 #ifndef MRT_SEG_REVERSE
 #define MRT_SEG_REVERSE 1
 #endif
+// The leaf phase's triangles spread over the wave (round 6, MRT_TRI_SPREAD = 1, default): the leaf
+// phase wave-uniform, each lane testing its leaf's first triangle itself (loaded with the leaf box)
+// and the leaves' further triangles spread over all 64 lanes, one (owner, triangle) pair per lane and
+// round, results merged by each owner in its own triangle order - the per-lane loop's results bit
+// for bit.  Spill-free at 80 VGPRs (no prefetch; qa, qb recomputed per inner phase).  Flat stand-in
+// 37.7 -> 36.5 ms, its N = 8 shard 7.36 -> 7.02 ms, the Conference stand-in within +-0.5 % (13.91 /
+// 13.97 ms, N = 8 2.52 / 2.51 ms); closest-hit triangle-loop lane use 0.35 -> 0.54
+// (profiles/r06_tri_spread_ab.txt).  0: the per-lane loop with the prefetch above.  (Round 5's form,
+// which spilled 44-68 B at 72 VGPRs, lost everywhere.)
+#ifndef MRT_TRI_SPREAD
+#define MRT_TRI_SPREAD 1
+#endif
+#ifndef MRT_TRI_SPREAD_ANY
+#define MRT_TRI_SPREAD_ANY MRT_TRI_SPREAD  // the any-hit (shadow) walk's
+#endif
 #ifndef MRT_SEG_CHUNK_LOG
 #define MRT_SEG_CHUNK_LOG 12
 #endif
@@ -556,6 +571,9 @@ struct LevelQueue {
 template <bool kAny, bool kCount, int kCull, class Stack, class Queue>
 __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stack& st, TravCount* cnt,
                                                  const QNode4* ldsTop, int* tailBest) {
+    // MRT_TRI_SPREAD for this walk: 0 the per-lane triangle loop, 1 the spread tests
+    constexpr int kSpread = kAny ? MRT_TRI_SPREAD_ANY : MRT_TRI_SPREAD;
+    __shared__ uint8_t spreadOwners[kSpread != 0 ? 192 * 4 : 1];  // per wave: the owner lane of each spread test
     constexpr int kHelper = -2;  // rayIdx of a lane walking a subtree given by another lane
     const bool donate = s.tailDonate != 0;
     const int top = min(kWalkTop, s.triTop);
@@ -823,6 +841,11 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
         // (counting builds: the wave's lanes without a ray and with a finished one, per inner iteration)
         const uint32_t idleLanes = kCount ? static_cast<uint32_t>(__popcll(__ballot(rayIdx == -1))) : 0u;
         const uint32_t doneLanes = kCount ? static_cast<uint32_t>(__popcll(__ballot(rayIdx != -1 && over2(ref, leaf)))) : 0u;
+        // the spread leaf phase: qa, qb recomputed per inner phase from o and 1/d (the same operations,
+        // the same bits), so that they hold no registers through the spread tests
+        const v3 qaL = kSpread == 0 ? qa : v3{s.qgrid.step[0] * inv.x, s.qgrid.step[1] * inv.y, s.qgrid.step[2] * inv.z};
+        const v3 qbL = kSpread == 0 ? qb : v3{(s.qgrid.origin[0] - o.x) * inv.x, (s.qgrid.origin[1] - o.y) * inv.y,
+                                              (s.qgrid.origin[2] - o.z) * inv.z};
         while (static_cast<unsigned>(ref) < static_cast<unsigned>(kRefDone)) {
             if (kCount) {
                 phaseCount(&cnt->innerIters, &cnt->innerLanes);
@@ -835,8 +858,8 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
             const bool finite = __ballot(!finiteInv(inv)) == 0;
             const int order = kAny ? s.anyOrder : 0;
             ref = refTree ? innerStep<kInner>(nodeBuf, ref, o, d, inv, curLim, st, cnt, kCount, finite, order)
-                          : order == 0 ? innerStepQ<kInner, 0>(qBuf, ldsTop, top, ref, qa, qb, curLim, st, cnt, kCount)
-                                       : innerStepQ<kInner, 1>(qBuf, ldsTop, top, ref, qa, qb, curLim, st, cnt, kCount);
+                          : order == 0 ? innerStepQ<kInner, 0>(qBuf, ldsTop, top, ref, qaL, qbL, curLim, st, cnt, kCount)
+                                       : innerStepQ<kInner, 1>(qBuf, ldsTop, top, ref, qaL, qbL, curLim, st, cnt, kCount);
             if (ref < 0 && leaf >= 0) {  // postpone this leaf, keep walking
                 leaf = ref;
                 ref = popCulled(st, curLim, cull);
@@ -847,6 +870,147 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
                 break;
         }
         // ---- leaves ----
+        if constexpr (kSpread != 0) {
+        // Wave-uniform: every lane takes part in the spread rounds, holding a leaf or not.
+        constexpr uint32_t kNoHitBits = 0x7F800001u;  // a signalling NaN: no arithmetic result has these bits
+        while (__ballot(leaf < 0) != 0) {
+            const bool holding = leaf < 0;
+            int first = 0, nprim = 0;
+            float4 a0 = make_float4(0.0F, 0.0F, 0.0F, 0.0F), b0t = a0, c0 = a0;
+            if (holding) {
+                if (kCount) phaseCount(&cnt->leafIters, &cnt->leafLanes);
+                first = leafFirst(leaf);
+                nprim = leafCount(leaf);
+                const uint32_t off0 = static_cast<uint32_t>(first) * 48u;
+                a0 = bload3(triBuf, off0);
+                b0t = bload3(triBuf, off0 + 16u);
+                c0 = bload3(triBuf, off0 + 32u);
+                if (!refTree) {
+                    const uint32_t lo = static_cast<uint32_t>(first) * 48u;
+                    const float4 b0 = bload4(leafBuf, lo);
+                    if (kCount) ++cnt->leaves;
+                    if (kCull == kCullExact) {
+                        const float4 b1 = bload4(leafBuf, lo + 16u);
+                        const float4 b2 = bload4(leafBuf, lo + 32u);
+                        float te, ex, ey, ez;
+                        if (!slabFiniteAxes(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv, &te, &ex, &ey, &ez)) {
+                            nprim = 0;
+                        } else {
+                            const float lim = fminf(bt, shT);
+                            if (te > lim && leafKey(b1, b2, te, ex, ey, ez, d, inv) > lim) nprim = 0;
+                        }
+                    } else {
+                        const int2 b1 = bload2i(leafBuf, lo + 16u);
+                        float te;
+                        const bool in =
+                            slabFinite(b0.x, b0.y, b0.z, b0.w, __int_as_float(b1.x), __int_as_float(b1.y), o, inv, &te);
+                        if (!in || (cull && te > cullLimit<kCull>(fminf(bt, shT)))) nprim = 0;
+                    }
+                }
+            }
+            // this lane's first triangle, tested here
+            bool hit = false;
+            if (nprim > 0) {
+                if (kCount) phaseCount(&cnt->triIters, &cnt->triLanes);
+                const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(first));
+                float t, u, v;
+                if (code != src) {
+                    if (kCount) ++cnt->tris;
+                    if (triTest(a0, b0t, c0, o, d, &t, &u, &v) && !(t < kEpsilon)) {
+                        if (kAny) {
+                            hit = !(t >= bt);
+                        } else if (betterThan(t, code, bt, bcode)) {
+                            bt = t;
+                            bcode = code;
+                        }
+                    }
+                }
+            }
+            // the others: slice k = the lanes with a (k+1)-th triangle left (an occluded any-hit lane
+            // has none), laid out slice after slice, 64 tests per round
+            const uint64_t m1 = __ballot(nprim > 1 && !hit);
+            if (m1 != 0) {
+                const uint64_t m2 = __ballot(nprim > 2 && !hit), m3 = __ballot(nprim > 3 && !hit);
+                const int c1 = __popcll(m1), c12 = c1 + __popcll(m2), total = c12 + __popcll(m3);
+                // the owner of every test, by its place in the layout (this wave's LDS table): lane
+                // byte-writes, then reads by the same wave (LDS operations of a wave complete in order)
+                uint8_t* const owners = spreadOwners + 192 * (threadIdx.x >> 6);
+                if (nprim > 1 && !hit) owners[lanesBelowIn(m1)] = static_cast<uint8_t>(lane);
+                if (nprim > 2 && !hit) owners[c1 + lanesBelowIn(m2)] = static_cast<uint8_t>(lane);
+                if (nprim > 3 && !hit) owners[c12 + lanesBelowIn(m3)] = static_cast<uint8_t>(lane);
+                __builtin_amdgcn_wave_barrier();
+                bool hit2 = false;
+                for (int base = 0; base < total; base += 64) {
+                    // tester: test g's slice and owner lane
+                    const int g = base + lane;
+                    const int tk = g < c1 ? 1 : g < c12 ? 2 : 3;
+                    const int own = g < total ? static_cast<int>(owners[g]) : lane;
+                    const int srcLane = own << 2;  // ds_bpermute byte address
+                    const v3 to{__int_as_float(__builtin_amdgcn_ds_bpermute(srcLane, __float_as_int(o.x))),
+                                __int_as_float(__builtin_amdgcn_ds_bpermute(srcLane, __float_as_int(o.y))),
+                                __int_as_float(__builtin_amdgcn_ds_bpermute(srcLane, __float_as_int(o.z)))};
+                    const v3 td{__int_as_float(__builtin_amdgcn_ds_bpermute(srcLane, __float_as_int(d.x))),
+                                __int_as_float(__builtin_amdgcn_ds_bpermute(srcLane, __float_as_int(d.y))),
+                                __int_as_float(__builtin_amdgcn_ds_bpermute(srcLane, __float_as_int(d.z)))};
+                    const uint32_t tsrc = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(srcLane, static_cast<int>(src)));
+                    const int tj = leafFirst(__builtin_amdgcn_ds_bpermute(srcLane, leaf)) + tk;
+                    uint32_t tt = kNoHitBits;
+                    if (g < total) {
+                        if (kCount) phaseCount(&cnt->triIters, &cnt->triLanes);
+                        const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(tj));
+                        if (code != tsrc) {
+                            if (kCount) ++cnt->tris;
+                            const uint32_t off = static_cast<uint32_t>(tj) * 48u;
+                            const float4 ta = bload3(triBuf, off), tb = bload3(triBuf, off + 16u), tc = bload3(triBuf, off + 32u);
+                            float t, u, v;
+                            if (triTest(ta, tb, tc, to, td, &t, &u, &v) && !(t < kEpsilon)) tt = __float_as_uint(t);
+                        }
+                    }
+                    // owners: the results of their tests in this round, in triangle order
+#pragma unroll
+                    for (int k = 1; k <= 3; ++k) {
+                        const uint64_t mk = k == 1 ? m1 : k == 2 ? m2 : m3;  // (uniform)
+                        const int idx = (k == 1 ? 0 : k == 2 ? c1 : c12) + lanesBelowIn(mk);
+                        const bool mine = ((mk >> lane) & 1ull) != 0 && idx >= base && idx < base + 64;
+                        const uint32_t rt = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((idx - base) << 2, static_cast<int>(tt)));
+                        if (mine && rt != kNoHitBits) {
+                            const float t = __uint_as_float(rt);
+                            const uint32_t code = encodePrim(kTriangle, static_cast<uint32_t>(leafFirst(leaf) + k));
+                            if (kAny) {
+                                hit2 = hit2 || !(t >= bt);
+                            } else if (betterThan(t, code, bt, bcode)) {
+                                bt = t;
+                                bcode = code;
+                            }
+                        }
+                    }
+                }
+                hit = hit || hit2;
+                __builtin_amdgcn_wave_barrier();  // (the table is rewritten by the next leaf iteration)
+            }
+            if (holding) {
+                if (kAny && hit) {
+                    if (kCount) cnt->occluded += (rayIdx >= 0 && pend == 0) ? 1u : 0u;  // (else counted at the merge)
+                    if (rayIdx >= 0 && pend == 0) {
+                        q.occ(rayIdx, 1.0F);
+                        rayIdx = -1;
+                    } else {  // a helper, or an owner waiting for helpers: the merge writes it
+                        occ = true;
+                    }
+                    st.sp = 0;
+                    ref = kRefDone;
+                    leaf = 0;
+                } else {
+                    leaf = 0;
+                    if (ref < 0) {  // the next node is a leaf too: test it now
+                        leaf = ref;
+                        ref = popCulled(st, cullLimit<kInner>(fminf(bt, shT)), cull);
+                    }
+                }
+            }
+            if (__popcll(__ballot(leaf < 0)) < leafExit) break;
+        }
+        } else {
         while (leaf < 0) {
             if (kCount) phaseCount(&cnt->leafIters, &cnt->leafLanes);
             const int first = leafFirst(leaf);
@@ -939,6 +1103,7 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
             // back to the inner phase once fewer than kLeafExit lanes hold a leaf: the others keep
             // theirs (tested first when the leaf phase resumes, so each lane's order is unchanged)
             if (__popcll(__ballot(leaf < 0)) < leafExit) break;
+        }
         }
     }
 }
