@@ -223,8 +223,9 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  *          the packet walk's LDS stack (kPacketStack),
  * key 17 = level 1 fused: camera rays generated, packet-walked and shaded in one launch (1, where it
  *          applies: BVH, packet walk, Whitted / PathTracer, untextured, lean shading, no counting) or
- *          the separate raygen / walk / shade launches (0, default since round 5: faster with the
- *          6-wave walks),
+ *          the separate raygen / walk / shade launches (0); -1 (default since round 6): fused below
+ *          16 paths per resident walk lane (a shard of C4 at N >= 2), separate above (DESIGN.md
+ *          section 7),
  * key 27 = the last shadow walk of a pass on the render stream with the closest-hit spill stacks
  *          (1, default) or on the shadow stream (0),
  * key 28 = at most this many workgroups per walk launch (0, default: the occupancy grid; 1-65536):

@@ -68,7 +68,7 @@ struct DScene {
     int32_t refill;            // idle lanes before a walk wave fetches new rays (tuning key 9, default 32)
     int32_t leanShade;         // k_shade's lean instantiation where it applies (tuning key 10)
     int32_t packet;            // level-1 rays take the wave-coherent walk (tuning key 16; modes 0 / 3)
-    int32_t fuseShade;         // level 1: the packet walk shades its own hits (tuning key 17, default 0)
+    int32_t fuseShade;         // level 1: the packet walk shades its own hits (set per pass: tuning key 17)
     // textures (map_Kd): scenes with a textured material only (`textured` != 0)
     const float4* triTex;      // 2 per triangle: (tA.xy, tB.xy), (tC.xy, -, -)
     const int4* texInfo;       // per texture: width, height, channels, first byte in texels

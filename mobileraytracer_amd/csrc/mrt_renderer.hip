@@ -251,6 +251,7 @@ struct mrt_renderer {
     int overlap = 1;                     // tuning key 3: shadow rays on their own stream
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
     int shadowGridPct = 0;               // tuning key 6: shadow walk grid, percent of its occupancy grid (0 auto)
+    int fuseL1Mode = -1;                 // tuning key 17: level 1 fused (1), in separate launches (0), -1 auto
     int refill = 0;                      // tuning key 9: walk refill threshold (0 auto: by paths per lane)
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
@@ -577,9 +578,7 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     d.refill = 32;  // kWalkRefill
     d.leanShade = 1;
     d.packet = r->stackNeed <= kPacketStack ? 1 : 0;  // the packet walk's uniform stack must hold the tree's need
-    // level 1's shading in its own launch (tuning key 17 = 0): since round 5's walks at 6 waves per
-    // SIMD the separate launches are faster (C4 14.07 -> 13.81 ms, N = 8 shard 2.55 -> 2.51 ms,
-    // profiles/r05_fused_level1_ab.txt)
+    // level 1 fused or not: chosen per pass by paths per walk lane (tuning key 17, renderPass)
     d.fuseShade = 0;
     d.matsFinite = 1;
     for (const HMaterial& m : sc.materials) {
@@ -772,17 +771,21 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         ra.sppTotal = r->cfg.samplesPixel;
         setPixelSampler(r, &ra);
         ra.sampleBase = sampleBase;
-        // level 1 fused (ray generation, packet walk and shading in one launch) where it applies
-        // (with per-launch events too: the serialised roofline frames time the kernel the timed frames run)
-        const bool fuseL1 = nLevels >= 1 && !(skipLast && nLevels == 1) && !(skipLastShade && nLevels == 1) &&
-                            canFuseLevel1(shader, r->ds, sa);
-        r->fusedL1 = fuseL1;
-        if (!fuseL1) launchRaygen(ra, pp.levels[1], pp.counters, st);
         // With few paths per resident walk lane (a small shard: C4 at N >= 4) the levels are short
         // and tail-bound, and a full-width shadow walk starves the next level's shading of CUs;
         // a narrower shadow grid leaves them room (C4 shard at N = 8: 2.92 -> 2.83 ms; at N = 1 the
         // full grid is 2.6 % faster).  Results do not depend on the grid.
         const double pathsPerLane = static_cast<double>(ra.nPaths) / std::max(1, r->traceThreads);
+        // Level 1 fused (ray generation, packet walk and shading in one launch, tuning key 17) where
+        // it applies; by default below 16 paths per walk lane: C4 at N = 2 (10.5 paths per lane)
+        // 7.59 -> 7.44 ms, at N = 4 / 8 the same, at N = 1 (21) separate launches are faster, 13.94
+        // vs 14.09 ms (profiles/r06_fused_level1_ab.txt).  (With per-launch events too: the
+        // serialised roofline frames time the kernel the timed frames run.)
+        r->ds.fuseShade = r->fuseL1Mode >= 0 ? r->fuseL1Mode : (pathsPerLane < 16.0 ? 1 : 0);
+        const bool fuseL1 = nLevels >= 1 && !(skipLast && nLevels == 1) && !(skipLastShade && nLevels == 1) &&
+                            canFuseLevel1(shader, r->ds, sa);
+        r->fusedL1 = fuseL1;
+        if (!fuseL1) launchRaygen(ra, pp.levels[1], pp.counters, st);
         // the walk launches' thread cap (tuning key 28 narrows it; the spill stacks hold traceThreads)
         const int walkThreads = r->walkGridCap > 0 ? std::min(r->traceThreads, r->walkGridCap * kBlock)
                                                    : r->traceThreads;
@@ -1596,8 +1599,8 @@ static int setTuningOne(mrt_renderer* r, int32_t key, int32_t value) {
         r->ds.packet = value;
         return 0;
     }
-    if (key == 17 && (value == 0 || value == 1)) {
-        r->ds.fuseShade = value;
+    if (key == 17 && value >= -1 && value <= 1) {
+        r->fuseL1Mode = value;
         return 0;
     }
     if (key == 27 && (value == 0 || value == 1)) {
@@ -1774,7 +1777,7 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 10: *value = r->ds.leanShade; return 0;
         case 11: *value = r->shadeGridPerCU; return 0;
         case 16: *value = r->ds.packet; return 0;
-        case 17: *value = r->ds.fuseShade; return 0;
+        case 17: *value = r->fuseL1Mode; return 0;
         case 27: *value = r->lastShadowRender; return 0;
         case 28: *value = r->walkGridCap; return 0;
         default: break;

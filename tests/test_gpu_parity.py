@@ -404,7 +404,7 @@ def test_fused_level1_shading_is_invariant():
     for cfg in cases:
         outs = []
         with m.Renderer(cfg) as r:
-            assert r.get_tuning(17) == 0  # separate launches by default since round 5
+            assert r.get_tuning(17) == -1  # auto (by paths per walk lane) since round 6
             for fuse, cull in ((1, 3), (0, 3), (1, 0), (0, 0)):
                 r.set_tuning(17, fuse)
                 r.set_tuning(2, cull)
