@@ -224,7 +224,7 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  * key 17 = level 1 fused: camera rays generated, packet-walked and shaded in one launch (1, where it
  *          applies: BVH, packet walk, Whitted / PathTracer, untextured, lean shading, no counting) or
  *          the separate raygen / walk / shade launches (0); -1 (default since round 6): fused below
- *          16 paths per resident walk lane (a shard of C4 at N >= 2), separate above (DESIGN.md
+ *          12 paths per resident walk lane (a shard of C4 at N >= 2), separate above (DESIGN.md
  *          section 7),
  * key 27 = the last shadow walk of a pass on the render stream with the closest-hit spill stacks
  *          (1, default) or on the shadow stream (0),

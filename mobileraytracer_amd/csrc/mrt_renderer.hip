@@ -777,11 +777,12 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // full grid is 2.6 % faster).  Results do not depend on the grid.
         const double pathsPerLane = static_cast<double>(ra.nPaths) / std::max(1, r->traceThreads);
         // Level 1 fused (ray generation, packet walk and shading in one launch, tuning key 17) where
-        // it applies; by default below 16 paths per walk lane: C4 at N = 2 (10.5 paths per lane)
-        // 7.59 -> 7.44 ms, at N = 4 / 8 the same, at N = 1 (21) separate launches are faster, 13.94
-        // vs 14.09 ms (profiles/r06_fused_level1_ab.txt).  (With per-launch events too: the
-        // serialised roofline frames time the kernel the timed frames run.)
-        r->ds.fuseShade = r->fuseL1Mode >= 0 ? r->fuseL1Mode : (pathsPerLane < 16.0 ? 1 : 0);
+        // it applies; by default below 12 paths per resident walk lane (traceThreads: the packet
+        // walk's 8 workgroups per CU): C4 at N = 2 (7.9 paths per lane) 7.59 -> 7.44 ms, at N = 4 / 8
+        // the same, at N = 1 (15.8) separate launches are faster, 13.94 vs 14.09 ms
+        // (profiles/r06_fused_level1_ab.txt).  (With per-launch events too: the serialised roofline
+        // frames time the kernel the timed frames run.)
+        r->ds.fuseShade = r->fuseL1Mode >= 0 ? r->fuseL1Mode : (pathsPerLane < 12.0 ? 1 : 0);
         const bool fuseL1 = nLevels >= 1 && !(skipLast && nLevels == 1) && !(skipLastShade && nLevels == 1) &&
                             canFuseLevel1(shader, r->ds, sa);
         r->fusedL1 = fuseL1;
