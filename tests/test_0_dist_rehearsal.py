@@ -92,3 +92,25 @@ def test_group_bench_assembles_the_single_gpu_frame(tmp_path):
     assert j["config"]["devices"] == [0, 0, 0, 0]
     assert j["value"] > 0 and j["roofline"]["kernels"]["k_trace"]["avg_launch_ms"] > 0
     assert np.array_equal(grp, one), int((grp != one).sum())
+
+
+def test_distinct_gpus_rccl_and_group_bench(tmp_path):
+    """Where the box has several GPUs: bench.py's RCCL rank path (one GPU per rank, `--gpus 2`
+    spawning its ranks) and its device-group path over distinct ordinals (peer copies) assemble the
+    single-GPU frame.  Skipped on one-GPU boxes, where the rehearsals above stand in for them."""
+    import json
+    import torch
+    n = torch.cuda.device_count()  # (counting devices does not initialise them)
+    if n < 2:
+        pytest.skip("one visible GPU: distinct-device paths need two")
+    assert not torch.cuda.is_initialized(), "must run before this process touches the GPU"
+    one, _ = _bench(str(tmp_path), "one_d", 1)
+    rccl, line = _bench(str(tmp_path), "rccl2", 2, launcher=False, extra_env={"MRT_BENCH_BACKEND": "nccl"})
+    assert "RCCL gather" in json.loads(line)["config"]["parallelism"]
+    assert np.array_equal(rccl, one), int((rccl != one).sum())
+    k = min(8, n)
+    grp, line = _bench(str(tmp_path), "group_d", k, launcher=False, extra_env={"MOBILERT_DEVICES": ""},
+                       extra_args=("--path", "group"))
+    j = json.loads(line)
+    assert j["config"]["devices"] == list(range(k)) and j["n_gpus"] == k
+    assert np.array_equal(grp, one), int((grp != one).sum())

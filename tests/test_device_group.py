@@ -6,8 +6,10 @@ The reference's Renderer::renderFrame spreads one frame over all its workers
 shard i of the screen-tile partition renders on devices[i] from a host thread of its own, and the
 head (devices[0]) gathers the packed shards (peer copies) and unpacks the frame.  On the one-GPU
 test box the ordinals repeat (0,0,0,0): the shards then share the GPU, which exercises every step
-of the group path except the xGMI transfer itself.  The bitmap, getSample() and
-getTotalCastedRays() must equal the single-GPU renderer's bit for bit.
+of the group path except the xGMI transfer itself.  On a box with several GPUs the same checks
+also run with distinct ordinals (0,1 and every visible GPU up to 8): the peer-access setup and the
+hipMemcpyPeerAsync assembly.  The bitmap, getSample() and getTotalCastedRays() must equal the
+single-GPU renderer's bit for bit.
 """
 import os
 import subprocess
@@ -30,6 +32,16 @@ CASES = (
 )
 
 
+def _device_lists():
+    """Repeated ordinals always; distinct ones where the box has several GPUs."""
+    import torch
+    n = torch.cuda.device_count()  # (counting devices does not initialise them)
+    lists = [[0, 0], [0, 0, 0, 0]]
+    if n >= 2:
+        lists += [[0, 1], list(range(min(8, n)))]
+    return lists
+
+
 def _render(cfg, frames=1):
     import mobileraytracer_amd as m
     with m.Renderer(cfg) as r:
@@ -47,7 +59,7 @@ def _render(cfg, frames=1):
 def test_device_group_equals_single_gpu(idx, progressive):
     kw = dict(CASES[idx])
     single, _ = _render(make_cfg(**kw, progressive=progressive), frames=2)
-    for devices in ([0, 0], [0, 0, 0, 0]):
+    for devices in _device_lists():
         group, info = _render(make_cfg(**kw, progressive=progressive, devices=devices), frames=2)
         assert info["deviceCount"] == len(devices)
         for a, b in zip(single, group):
@@ -97,7 +109,9 @@ def test_raytrace_and_facade_with_mobilert_devices(tmp_path):
     every bitmap, getSample() and getTotalCastedRays() equal the single-GPU run's."""
     from mobileraytracer_amd import scenes
     runs = {}
-    for name, devs in (("single", None), ("group", "0,0,0")):
+    import torch
+    groups = [("group", "0,0,0")] + ([("group_distinct", "0,1")] if torch.cuda.device_count() >= 2 else [])
+    for name, devs in [("single", None)] + groups:
         env = dict(os.environ)
         env.pop("MOBILERT_MAX_DEPTH", None)
         env.pop("MOBILERT_DEVICES", None)
@@ -114,10 +128,12 @@ def test_raytrace_and_facade_with_mobilert_devices(tmp_path):
                            env=env)
         assert q.returncode == 0, q.stdout + q.stderr
         runs[name] = (d1, d2, [l for l in p.stdout.splitlines() if l.startswith("Casted rays")])
-    (s1, s2, srays), (g1, g2, grays) = runs["single"], runs["group"]
-    assert srays == grays and srays
-    for d, e in ((s1, g1), (s2, g2)):
-        names = sorted(f for f in os.listdir(d) if f != "async_stop.bin")  # async_stop: a partial frame
-        assert names and names == sorted(f for f in os.listdir(e) if f != "async_stop.bin")
-        for f in names:
-            assert open(d / f, "rb").read() == open(e / f, "rb").read(), f
+    s1, s2, srays = runs["single"]
+    for name, _ in groups:
+        g1, g2, grays = runs[name]
+        assert srays == grays and srays
+        for d, e in ((s1, g1), (s2, g2)):
+            names = sorted(f for f in os.listdir(d) if f != "async_stop.bin")  # async_stop: a partial frame
+            assert names and names == sorted(f for f in os.listdir(e) if f != "async_stop.bin")
+            for f in names:
+                assert open(d / f, "rb").read() == open(e / f, "rb").read(), (name, f)
