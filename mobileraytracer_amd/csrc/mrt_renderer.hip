@@ -61,6 +61,20 @@ struct DeviceMem {
     ~DeviceMem() { release(); }
 };
 
+// The wide collapse's node costs (toQuantizedBVH4's nodeCost).  Default (round 6): a sample of the
+// frame's own rays (mrt::frameRayNodeCosts: the camera's rays, their bounces and shadow rays), so
+// that the collapse minimises the wide-node visits of the rays this frame walks rather than of
+// uniformly random lines: node records per shadow ray 60.6 -> 53.0, per closest-hit ray 93.0 ->
+// 91.4; C4 13.94-13.97 -> 13.68-13.70 ms, N = 8 shard 2.53 -> 2.47 ms, the flat stand-in unchanged
+// (profiles/r06_ray_collapse_ab.txt).  MOBILERT_COLLAPSE=area: surface areas (an empty vector);
+// =greedy: round 1's greedy collapse.  Any cost gives an exact walk.
+std::vector<double> walkCollapseCosts(const std::vector<mrt::HBVHNode>& wn, const mrt::HScene& sc, const mrt::GCamera& cam,
+                                      int width, int height, int maxDepth) {
+    const char* ce = std::getenv("MOBILERT_COLLAPSE");
+    if (ce != nullptr && (std::string(ce) == "area" || std::string(ce) == "greedy")) return {};
+    return mrt::frameRayNodeCosts(wn, sc, cam, width, height, maxDepth);
+}
+
 int bvhDepth(const std::vector<mrt::HBVHNode>& nodes) {
     if (nodes.empty()) return 0;
     int best = 0;
@@ -390,7 +404,9 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     // the walk tree, numbered (top breadth-first), then quantized; the reference tree in its own
     // GNode array
     std::vector<QNode4> qn;
-    d.qEnabled = toQuantizedBVH4(wn, sc.triangles.size(), &d.triRoot, kTopNodesMax, &d.triTop, &d.qgrid, &qn) ? 1 : 0;
+    const std::vector<double> rayCost = walkCollapseCosts(wn, sc, r->cam, r->cfg.width, r->cfg.height, r->maxDepth);
+    d.qEnabled = toQuantizedBVH4(wn, sc.triangles.size(), &d.triRoot, kTopNodesMax, &d.triTop, &d.qgrid, &qn, nullptr,
+                                 rayCost.empty() ? nullptr : &rayCost) ? 1 : 0;
     if (d.qEnabled == 0 || qn.empty()) qn.resize(1);  // (a leaf or empty root: no inner node)
     d.triQNodes = r->sceneMem.upload(qn, st);
     {
@@ -1654,13 +1670,19 @@ int64_t mrt_walk_tree(const mrt_config* cfg, uint32_t* nodes, float* grid, int32
     int64_t n = -1;
     const int rc = guarded([&] {
         HScene sc;
+        // the camera too: the collapse weighs nodes by the frame's rays, as the renderer does
+        const float ratio = cfg->height > 0 ? static_cast<float>(cfg->width) / static_cast<float>(cfg->height) : 1.0F;
+        GCamera cam{};
+        bool haveCam = true;
         if (cfg->sceneIndex >= 0 && cfg->sceneIndex <= 3) {
             sc = builtinScene(cfg->sceneIndex);
+            cam = builtinCamera(cfg->sceneIndex, ratio);
         } else {
             std::string err;
             if (!loadObjScene(cfg->objFilePath ? cfg->objFilePath : "", cfg->mtlFilePath ? cfg->mtlFilePath : "", &sc,
                               &err))
                 throw std::runtime_error(err);
+            haveCam = loadCameraFile(cfg->camFilePath ? cfg->camFilePath : "", ratio, &cam, &err);
         }
         std::vector<int32_t> perm;
         const std::vector<HBVHNode> tn = buildBVH(&sc.triangles, &perm);
@@ -1669,7 +1691,11 @@ int64_t mrt_walk_tree(const mrt_config* cfg, uint32_t* nodes, float* grid, int32
         QGrid g{};
         std::vector<QNode4> qn;
         int top = 0;
-        if (!toQuantizedBVH4(wn, sc.triangles.size(), &r, kTopNodesMax, &top, &g, &qn))
+        const int maxDepth = cfg->maxDepth > 0 ? cfg->maxDepth : kRayDepthMaxDefault;
+        const std::vector<double> cost =
+            haveCam ? walkCollapseCosts(wn, sc, cam, cfg->width, cfg->height, maxDepth) : std::vector<double>{};
+        if (!toQuantizedBVH4(wn, sc.triangles.size(), &r, kTopNodesMax, &top, &g, &qn, nullptr,
+                             cost.empty() ? nullptr : &cost))
             throw std::runtime_error("walk tree not quantizable (non-finite boxes)");
         n = static_cast<int64_t>(qn.size());
         if (nodes != nullptr) std::memcpy(nodes, qn.data(), qn.size() * sizeof(QNode4));

@@ -1033,9 +1033,10 @@ struct Quantizer {
 // summed wide-node area covering BVH2 node i's subtree with at most j trees, split[] its choices.
 // forest[1] (the root as a wide node) is the whole wide tree's cost.
 static void collapseForests(const std::vector<HBVHNode>& nodes, std::vector<double>* forestOut,
-                            std::vector<int8_t>* splitOut) {
+                            std::vector<int8_t>* splitOut, const std::vector<double>* nodeCost = nullptr) {
     auto inner = [&](int32_t i) { return nodes[static_cast<size_t>(i)].numPrimitives == 0; };
     auto area = [&](int32_t i) {
+        if (nodeCost != nullptr) return (*nodeCost)[static_cast<size_t>(i)];
         const HAABB& b = nodes[static_cast<size_t>(i)].box;
         const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,
                      dz = static_cast<double>(b.mx.z) - b.mn.z;
@@ -1124,7 +1125,8 @@ static double collapsedArea(const std::vector<HBVHNode>& nodes, int* depth) {
 }
 
 bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
-                     QGrid* grid, std::vector<QNode4>* out, std::vector<int32_t>* bvh2Of) {
+                     QGrid* grid, std::vector<QNode4>* out, std::vector<int32_t>* bvh2Of,
+                     const std::vector<double>* nodeCost) {
     out->clear();
     if (bvh2Of != nullptr) bvh2Of->clear();
     if (topPlaced != nullptr) *topPlaced = 0;
@@ -1164,7 +1166,7 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
     std::vector<double> forest;  // [i * W1 + j], j = 1..kWalkWidth
     std::vector<int8_t> split;   // [i * W1 + j]: trees taken from the left child (0: node i itself);
                                  // [i * W1]: the split of node i as a wide node
-    if (optimal) collapseForests(nodes, &forest, &split);
+    if (optimal) collapseForests(nodes, &forest, &split, nodeCost);
     // the trees of node i's best forest of at most j (BVH2 indices, left to right)
     std::function<void(int32_t, int, std::vector<int32_t>&)> trees = [&](int32_t i, int j, std::vector<int32_t>& out) {
         const int k = inner(i) && j > 1 ? split[static_cast<size_t>(i) * W1 + static_cast<size_t>(j)] : 0;
@@ -1828,6 +1830,184 @@ static std::vector<HBVHNode> rotateForWide(const std::vector<HBVHNode>& in, int 
         st.push_back({n.l, left});
     }
     return out;
+}
+
+std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
+                                      int width, int height, int maxDepth) {
+    std::vector<double> cost(nodes.size(), 0.0);
+    if (nodes.empty() || sc.triangles.empty() || width <= 0 || height <= 0) return cost;
+    struct Ray {
+        v3 o, d;
+        float w;
+    };
+    auto inner = [&](size_t i) { return nodes[i].numPrimitives == 0 && nodes.size() > 1; };
+    // the slab entry of a box (t >= 0), or +inf when the half-line misses it
+    auto entry = [](const HAABB& b, v3 o, v3 inv) {
+        float t0 = 0.0F, t1 = std::numeric_limits<float>::infinity();
+        for (int a = 0; a < 3; ++a) {
+            const float lo = (comp(b.mn, a) - comp(o, a)) * comp(inv, a), hi = (comp(b.mx, a) - comp(o, a)) * comp(inv, a);
+            t0 = std::max(t0, std::min(lo, hi));
+            t1 = std::min(t1, std::max(lo, hi));
+        }
+        return t0 <= t1 ? t0 : std::numeric_limits<float>::infinity();
+    };
+    auto triHit = [](const HTriangle& t, v3 o, v3 d, float* tOut) {  // Moller-Trumbore, float
+        const v3 p = cross(d, t.AC);
+        const float det = dot(t.AB, p);
+        if (std::fabs(det) < 1e-9F) return false;
+        const float inv = 1.0F / det;
+        const v3 s = o - t.A;
+        const float u = inv * dot(s, p);
+        if (u < 0.0F || u > 1.0F) return false;
+        const v3 q = cross(s, t.AB);
+        const float v = inv * dot(d, q);
+        if (v < 0.0F || u + v > 1.0F) return false;
+        *tOut = inv * dot(t.AC, q);
+        return *tOut > 1e-4F;
+    };
+    // closest hit: triangle index (BVH order), or -2 for a light, -1 for none
+    auto closest = [&](v3 o, v3 d, float* tBest) {
+        const v3 inv{1.0F / d.x, 1.0F / d.y, 1.0F / d.z};
+        int best = -1;
+        float bt = std::numeric_limits<float>::infinity();
+        std::vector<int32_t> st{0};
+        while (!st.empty()) {
+            const size_t i = static_cast<size_t>(st.back());
+            st.pop_back();
+            if (!(entry(nodes[i].box, o, inv) < bt)) continue;
+            if (inner(i)) {
+                st.push_back(nodes[i].indexOffset + 1);
+                st.push_back(nodes[i].indexOffset);
+                continue;
+            }
+            for (int32_t k = 0; k < nodes[i].numPrimitives; ++k) {
+                float t;
+                const int32_t j = nodes[i].indexOffset + k;
+                if (triHit(sc.triangles[static_cast<size_t>(j)], o, d, &t) && t < bt) {
+                    bt = t;
+                    best = j;
+                }
+            }
+        }
+        for (const HLight& l : sc.lights) {
+            float t;
+            if (l.kind == kAreaLight && triHit(l.tri, o, d, &t) && t < bt) {
+                bt = t;
+                best = -2;
+            }
+        }
+        *tBest = bt;
+        return best;
+    };
+    std::vector<const HLight*> areaLights;
+    for (const HLight& l : sc.lights)
+        if (l.kind == kAreaLight) areaLights.push_back(&l);
+    // the sample: the frame's walked rays (camera rays of a 192 x 108 pixel grid, each path's
+    // bounces and shadow rays); camera rays weigh 0.6 (the packet walk's cost per ray against the
+    // per-lane walks', profiles/r06_bench.json), the others 1
+    std::vector<Ray> rays;
+    std::mt19937 rng(0x4D525406u);
+    std::uniform_real_distribution<float> U(0.0F, 1.0F);
+    // (camera weight 0.25 / 1, shadow weight 0.5 / 2, grids of 96 x 54 and 384 x 216 pixels and an
+    // area floor of 0.1 % / 10 % measured within 0.5 % of these: profiles/r06_ray_collapse_ab.txt)
+    constexpr float camW = 0.6F, shadowW = 1.0F, floorW = 0.01F;
+    constexpr int gx = 192, gy = 108;
+    struct Path {
+        v3 o, d;
+        int depth;
+    };
+    for (int py = 0; py < gy; ++py)
+        for (int px = 0; px < gx; ++px) {
+            const float u = (static_cast<float>(px) + U(rng)) / static_cast<float>(gx);
+            const float v = (static_cast<float>(py) + U(rng)) / static_cast<float>(gy);
+            v3 o, d;
+            if (cam.kind == 1) {
+                o = (cam.position + cam.right * ((u - 0.5F) * cam.hFov)) + cam.up * ((0.5F - v) * cam.vFov);
+                d = cam.direction;
+            } else {
+                const v3 dest = ((cam.position + cam.direction) + cam.right * fastArcTan(cam.hFov * (u - 0.5F))) +
+                                cam.up * fastArcTan(cam.vFov * (0.5F - v));
+                o = cam.position;
+                d = normalize(dest - cam.position);
+            }
+            std::vector<Path> work{{o, d, 1}};
+            while (!work.empty()) {
+                const Path p = work.back();
+                work.pop_back();
+                rays.push_back(Ray{p.o, p.d, p.depth == 1 ? camW : 1.0F});
+                float t;
+                const int hit = closest(p.o, p.d, &t);
+                if (hit < 0) continue;  // a miss, or a light (emissive: no children)
+                const HTriangle& tri = sc.triangles[static_cast<size_t>(hit)];
+                const HMaterial m = tri.mat >= 0 && tri.mat < static_cast<int32_t>(sc.materials.size())
+                                        ? sc.materials[static_cast<size_t>(tri.mat)] : HMaterial{};
+                if (m.Le.x > 0.0F || m.Le.y > 0.0F || m.Le.z > 0.0F) continue;
+                v3 n = normalize(cross(tri.AB, tri.AC));
+                if (dot(n, p.d) > 0.0F) n = -n;
+                const v3 P = p.o + p.d * t + n * 1e-3F;
+                const bool diffuse = m.Kd.x > 0.0F || m.Kd.y > 0.0F || m.Kd.z > 0.0F;
+                if (diffuse && !areaLights.empty()) {  // a shadow ray to a random point of a random light
+                    const HLight& l = *areaLights[static_cast<size_t>(U(rng) * 0.99999F * static_cast<float>(areaLights.size()))];
+                    float r1 = U(rng), r2 = U(rng);
+                    if (r1 + r2 >= 1.0F) {
+                        r1 = 1.0F - r1;
+                        r2 = 1.0F - r2;
+                    }
+                    const v3 q = (l.tri.A + l.tri.AB * r1) + l.tri.AC * r2;
+                    rays.push_back(Ray{P, normalize(q - P), shadowW});
+                }
+                if (p.depth >= maxDepth) continue;  // the depth-capped level is not walked
+                if (diffuse && (p.depth <= 1 || U(rng) > 0.5F)) {  // cosine bounce (PathTracer.cpp:89-91)
+                    const float phi = 6.2831853F * U(rng), r2 = U(rng);
+                    const v3 a = std::fabs(n.x) > 0.1F ? v3{0.0F, 1.0F, 0.0F} : v3{1.0F, 0.0F, 0.0F};
+                    const v3 tu = normalize(cross(a, n)), tv = cross(n, tu);
+                    const float ct = std::sqrt(r2);
+                    work.push_back(Path{P, normalize((tu * (std::cos(phi) * ct) + tv * (std::sin(phi) * ct)) + n * std::sqrt(1.0F - r2)),
+                                        p.depth + 1});
+                }
+                if (m.Ks.x > 0.0F || m.Ks.y > 0.0F || m.Ks.z > 0.0F) work.push_back(Path{P, reflect(p.d, n), p.depth + 1});
+            }
+        }
+    // every node whose box each sample ray's half-line passes (the exact walk culls no inner node)
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::vector<double>> part(hw, std::vector<double>(nodes.size(), 0.0));
+    std::vector<std::thread> pool;
+    for (unsigned w = 0; w < hw; ++w)
+        pool.emplace_back([&, w] {
+            std::vector<int32_t> st;
+            std::vector<double>& c = part[w];
+            for (size_t k = w; k < rays.size(); k += hw) {
+                const Ray& r = rays[k];
+                const v3 inv{1.0F / r.d.x, 1.0F / r.d.y, 1.0F / r.d.z};
+                st.assign(1, 0);
+                while (!st.empty()) {
+                    const size_t i = static_cast<size_t>(st.back());
+                    st.pop_back();
+                    if (!(entry(nodes[i].box, r.o, inv) < std::numeric_limits<float>::infinity())) continue;
+                    c[i] += r.w;
+                    if (inner(i)) {
+                        st.push_back(nodes[i].indexOffset);
+                        st.push_back(nodes[i].indexOffset + 1);
+                    }
+                }
+            }
+        });
+    for (std::thread& t : pool) t.join();
+    double total = 0.0;
+    for (const Ray& r : rays) total += r.w;
+    auto area = [&](size_t i) {
+        const HAABB& b = nodes[i].box;
+        const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,
+                     dz = static_cast<double>(b.mx.z) - b.mn.z;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    const double rootArea = std::max(1e-30, area(0));
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        double s = 0.0;
+        for (unsigned w = 0; w < hw; ++w) s += part[w][i];
+        cost[i] = s + floorW * total * area(i) / rootArea;
+    }
+    return cost;
 }
 
 static std::vector<HBVHNode> walkTreeBuild(const std::vector<HBVHNode>& ref, int rounds, int rotSweeps) {

@@ -151,8 +151,18 @@ void toDeviceBVH(const std::vector<HBVHNode>& nodes, size_t numPrims, std::vecto
 // of largest area replaced by its own children while fewer than four), quantized like
 // Quantizer (mrt_scene.cpp) and numbered as toDeviceBVH numbers (the first topCount breadth-first).  Fills
 // root (box of nodes[0], reference into out); false when a box or the grid is not finite.
+// nodeCost: the collapse's cost of each BVH2 node as a wide node (null: its surface area).
 bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot* root, int topCount, int* topPlaced,
-                     QGrid* grid, std::vector<QNode4>* out, std::vector<int32_t>* bvh2Of = nullptr);
+                     QGrid* grid, std::vector<QNode4>* out, std::vector<int32_t>* bvh2Of = nullptr,
+                     const std::vector<double>* nodeCost = nullptr);
+// The frame's own ray distribution as collapse costs (MOBILERT_COLLAPSE=rays, an A/B setting): a
+// sample of the frame's walked rays - camera rays over a pixel grid, then per hit a shadow ray to a
+// random point of a random light and the PathTracer's children (cosine bounce, mirror reflection)
+// up to maxDepth, traced on the host - and cost[i] = the weighted number of sample rays whose
+// half-line passes node i's box (the exact walk visits every wide node it passes), plus 1 % of the
+// node's share of the root's area as a floor.  Any cost gives an exact walk: only the collapse changes.
+std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
+                                      int width, int height, int maxDepth);
 // A tree over the same leaves (primitive ranges and boxes) as the reference tree `ref`, grouped
 // by a full-sweep SAH; its inner boxes are exact unions of the leaf boxes (reference numbering:
 // node 0 the root, an inner node's children at indexOffset and indexOffset + 1).

@@ -101,6 +101,7 @@ def test_optimal_collapse_beats_greedy(case, monkeypatch):
     the trees it considers, so its sum is never larger (up to the quantization's outward step)."""
     import mobileraytracer_amd as m
     cfg = make_cfg(64, 64, **case)
+    monkeypatch.setenv("MOBILERT_COLLAPSE", "area")  # (the default weighs nodes by the frame's rays)
     nodes, grid, root = m.walk_tree(cfg)
     monkeypatch.setenv("MOBILERT_COLLAPSE", "greedy")
     gnodes, ggrid, groot = m.walk_tree(cfg)
@@ -120,6 +121,7 @@ def test_tree_optimisation_lowers_the_summed_area(case, monkeypatch):
     beyond the quantization's outward step, and the conference stand-in's falls by >= 3 %."""
     import mobileraytracer_amd as m
     cfg = make_cfg(64, 64, **case)
+    monkeypatch.setenv("MOBILERT_COLLAPSE", "area")
     monkeypatch.setenv("MOBILERT_TREE_OPT", "0")
     n0, g0, r0 = m.walk_tree(cfg)
     monkeypatch.setenv("MOBILERT_TREE_OPT", "100")
@@ -141,6 +143,7 @@ def test_wide_rotations_lower_the_wide_area(case, monkeypatch):
     its optimised trees are deeper) untouched.  The process's tree cache keys on the settings."""
     import mobileraytracer_amd as m
     cfg = make_cfg(64, 64, **case)
+    monkeypatch.setenv("MOBILERT_COLLAPSE", "area")
     monkeypatch.setenv("MOBILERT_TREE_ROT", "0")
     n0, g0, r0 = m.walk_tree(cfg)
     monkeypatch.delenv("MOBILERT_TREE_ROT")
@@ -183,3 +186,30 @@ def test_unused_slots_hold_inverted_boxes(case):
     near = np.where(qa > 0, lo, hi)  # the rotated word: near = min plane for qa > 0, else max
     far = np.where(qa > 0, hi, lo)
     assert np.all(near > far)
+
+
+@pytest.mark.parametrize("collapse", ["area", "greedy"])
+@pytest.mark.parametrize("case", [dict(scene="conference"), dict(scene="water"), dict(sceneIndex=3)])
+def test_ray_weighted_collapse_keeps_the_leaves(case, collapse, monkeypatch):
+    """The default collapse weighs each BVH2 node by a sample of the frame's own rays
+    (mrt_scene.cpp frameRayNodeCosts): the same reference leaves, each once, in a tree of no more
+    wide nodes than the greedy collapse's, and (for a scene the camera sees) a different tree from
+    the area collapse's - a collapse choice only, which the exactness argument does not depend on."""
+    import mobileraytracer_amd as m
+    cfg = make_cfg(64, 64, **case)
+    nodes, grid, root = m.walk_tree(cfg)
+    monkeypatch.setenv("MOBILERT_COLLAPSE", collapse)
+    onodes, ogrid, oroot = m.walk_tree(cfg)
+    assert int(root[1]) == int(oroot[1]) and np.array_equal(grid, ogrid)
+    width = int(root[2])
+
+    def leaves(n, r):
+        refs = n[:, 3 * width:].view(np.int32)
+        out = [int(x) for x in refs.ravel() if int(x) < 0 and int(x) != EMPTY]
+        return sorted(out) if int(r[0]) >= 0 else [int(r[0])]
+
+    assert leaves(nodes, root) == leaves(onodes, oroot)
+    if collapse == "greedy":
+        assert len(nodes) <= len(onodes)
+    if collapse == "area" and case.get("scene") == "conference":
+        assert not np.array_equal(nodes, onodes)
