@@ -1832,25 +1832,26 @@ static std::vector<HBVHNode> rotateForWide(const std::vector<HBVHNode>& in, int 
     return out;
 }
 
-std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
-                                      int width, int height, int maxDepth) {
-    std::vector<double> cost(nodes.size(), 0.0);
-    if (nodes.empty() || sc.triangles.empty() || width <= 0 || height <= 0) return cost;
-    struct Ray {
-        v3 o, d;
-        float w;
-    };
+namespace {
+// the slab entry of a box (t >= 0), or +inf when the half-line misses it
+float halfLineEntry(const HAABB& b, v3 o, v3 inv) {
+    float t0 = 0.0F, t1 = std::numeric_limits<float>::infinity();
+    for (int a = 0; a < 3; ++a) {
+        const float lo = (comp(b.mn, a) - comp(o, a)) * comp(inv, a), hi = (comp(b.mx, a) - comp(o, a)) * comp(inv, a);
+        t0 = std::max(t0, std::min(lo, hi));
+        t1 = std::min(t1, std::max(lo, hi));
+    }
+    return t0 <= t1 ? t0 : std::numeric_limits<float>::infinity();
+}
+}  // namespace
+
+std::vector<SampleRay> sampleFrameRays(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
+                                       int maxDepth) {
+    using Ray = SampleRay;
+    std::vector<Ray> rays;
+    if (nodes.empty() || sc.triangles.empty()) return rays;
     auto inner = [&](size_t i) { return nodes[i].numPrimitives == 0 && nodes.size() > 1; };
-    // the slab entry of a box (t >= 0), or +inf when the half-line misses it
-    auto entry = [](const HAABB& b, v3 o, v3 inv) {
-        float t0 = 0.0F, t1 = std::numeric_limits<float>::infinity();
-        for (int a = 0; a < 3; ++a) {
-            const float lo = (comp(b.mn, a) - comp(o, a)) * comp(inv, a), hi = (comp(b.mx, a) - comp(o, a)) * comp(inv, a);
-            t0 = std::max(t0, std::min(lo, hi));
-            t1 = std::min(t1, std::max(lo, hi));
-        }
-        return t0 <= t1 ? t0 : std::numeric_limits<float>::infinity();
-    };
+    const auto entry = halfLineEntry;
     auto triHit = [](const HTriangle& t, v3 o, v3 d, float* tOut) {  // Moller-Trumbore, float
         const v3 p = cross(d, t.AC);
         const float det = dot(t.AB, p);
@@ -1905,12 +1906,11 @@ std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const 
     // the sample: the frame's walked rays (camera rays of a 192 x 108 pixel grid, each path's
     // bounces and shadow rays); camera rays weigh 0.6 (the packet walk's cost per ray against the
     // per-lane walks', profiles/r06_bench.json), the others 1
-    std::vector<Ray> rays;
     std::mt19937 rng(0x4D525406u);
     std::uniform_real_distribution<float> U(0.0F, 1.0F);
     // (camera weight 0.25 / 1, shadow weight 0.5 / 2, grids of 96 x 54 and 384 x 216 pixels and an
     // area floor of 0.1 % / 10 % measured within 0.5 % of these: profiles/r06_ray_collapse_ab.txt)
-    constexpr float camW = 0.6F, shadowW = 1.0F, floorW = 0.01F;
+    constexpr float camW = 0.6F, shadowW = 1.0F;
     constexpr int gx = 192, gy = 108;
     struct Path {
         v3 o, d;
@@ -1968,6 +1968,16 @@ std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const 
                 if (m.Ks.x > 0.0F || m.Ks.y > 0.0F || m.Ks.z > 0.0F) work.push_back(Path{P, reflect(p.d, n), p.depth + 1});
             }
         }
+    return rays;
+}
+
+std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
+                                      int width, int height, int maxDepth) {
+    std::vector<double> cost(nodes.size(), 0.0);
+    if (nodes.empty() || sc.triangles.empty() || width <= 0 || height <= 0) return cost;
+    const std::vector<SampleRay> rays = sampleFrameRays(nodes, sc, cam, maxDepth);
+    auto inner = [&](size_t i) { return nodes[i].numPrimitives == 0 && nodes.size() > 1; };
+    constexpr float floorW = 0.01F;
     // every node whose box each sample ray's half-line passes (the exact walk culls no inner node)
     const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::vector<double>> part(hw, std::vector<double>(nodes.size(), 0.0));
@@ -1977,13 +1987,13 @@ std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const 
             std::vector<int32_t> st;
             std::vector<double>& c = part[w];
             for (size_t k = w; k < rays.size(); k += hw) {
-                const Ray& r = rays[k];
+                const SampleRay& r = rays[k];
                 const v3 inv{1.0F / r.d.x, 1.0F / r.d.y, 1.0F / r.d.z};
                 st.assign(1, 0);
                 while (!st.empty()) {
                     const size_t i = static_cast<size_t>(st.back());
                     st.pop_back();
-                    if (!(entry(nodes[i].box, r.o, inv) < std::numeric_limits<float>::infinity())) continue;
+                    if (!(halfLineEntry(nodes[i].box, r.o, inv) < std::numeric_limits<float>::infinity())) continue;
                     c[i] += r.w;
                     if (inner(i)) {
                         st.push_back(nodes[i].indexOffset);
@@ -1994,7 +2004,7 @@ std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const 
         });
     for (std::thread& t : pool) t.join();
     double total = 0.0;
-    for (const Ray& r : rays) total += r.w;
+    for (const SampleRay& r : rays) total += r.w;
     auto area = [&](size_t i) {
         const HAABB& b = nodes[i].box;
         const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,

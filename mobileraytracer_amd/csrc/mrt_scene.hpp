@@ -163,6 +163,13 @@ bool toQuantizedBVH4(const std::vector<HBVHNode>& nodes, size_t numPrims, GRoot*
 // node's share of the root's area as a floor.  Any cost gives an exact walk: only the collapse changes.
 std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
                                       int width, int height, int maxDepth);
+// frameRayNodeCosts' sample: the rays (origin, direction, weight) traced on the host over `nodes`
+struct SampleRay {
+    v3 o, d;
+    float w;
+};
+std::vector<SampleRay> sampleFrameRays(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
+                                       int maxDepth);
 // A tree over the same leaves (primitive ranges and boxes) as the reference tree `ref`, grouped
 // by a full-sweep SAH; its inner boxes are exact unions of the leaf boxes (reference numbering:
 // node 0 the root, an inner node's children at indexOffset and indexOffset + 1).
