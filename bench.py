@@ -370,12 +370,16 @@ def kernel_roofline(r, step, overlap=1):
     # written (vertex or result record); per shaded hit 48 (normals, material id) + 64 (material) + 64
     # (light) + 32 (the vertex's six draws, one compact block); per shadow ray 48 written; per child ray
     # 36 written (not for the depth-capped level's children, whose payloads are never written)
-    def shade_bytes(l, read_rays=True):
+    # (read_rays False: the fused level-1 kernel, whose rays and hits stay in registers; regen: level 1's
+    # k_shade regenerating its camera rays (tuning key 33 = 2): it reads the hit only, 16 + 16 per ray)
+    def shade_bytes(l, read_rays=True, regen=False):
         child = 36.0 * rays[l + 1] if l + 1 < md else 0.0
-        return (68.0 if read_rays else 16.0) * rays[l] + 208.0 * shaded[l] + 48.0 * shadows[l] + child
+        per_ray = 32.0 if regen else 68.0 if read_rays else 16.0
+        return per_ray * rays[l] + 208.0 * shaded[l] + 48.0 * shadows[l] + child
 
     shade_levels = range(1 if fused else 0, md)
-    shade_b = sum(shade_bytes(l) for l in shade_levels)
+    gen = r.get_tuning(33) if packet else 0  # 1: the packet walk generates and stores the camera rays; 2: k_shade regenerates them
+    shade_b = sum(shade_bytes(l, regen=(l == 0 and gen == 2)) for l in shade_levels)
     # the fused level-1 launch: the packet walk's gathers (no ray record read: the rays are generated
     # in the kernel; no hit record written: it is shaded in the same wave) + level 1's shading
     fused_b = 32.0 * nodes[0] + 36.0 * tris[0] + shade_bytes(0, read_rays=False)
@@ -430,12 +434,16 @@ def kernel_roofline(r, step, overlap=1):
         # lane: priced by what it moves - per lane the ray read (32 B), the hit write (16 B) and the
         # winner's triangle re-read for u, v (48 B); per wave the records it loads (counting frame,
         # packetWaveRecords).  SURVEY 8(d)'s per-lane price is kept beside it as `lane_basis_*`.
+        # (tuning key 33: 1 the walk generates the rays and stores their 36-B records instead of reading
+        # 32 B; 2 it stores nothing, k_shade regenerates them)
         wn, wl, wt = c["packetWaveRecords"]
-        packet_b = 96.0 * rays[0] + 128.0 * wn + 48.0 * wl + 48.0 * wt
+        ray_b = 32.0 if gen == 0 else 36.0 if gen == 1 else 0.0
+        packet_b = (64.0 + ray_b) * rays[0] + 128.0 * wn + 48.0 * wl + 48.0 * wt
         lane_b = 48.0 * rays[0] + 32.0 * nodes[0] + 36.0 * tris[0]
         e = entry(packet_b, packet_ms, packet_launches, None, [1], packet_ms_ov)
-        e["frac_basis"] = ("bytes the kernel moves: per lane 96 B (ray, hit, winner's triangle), per wave 128 B per node "
-                           "visit + 48 B per leaf record + 48 B per triangle record (scalar loads, once per wave)")
+        e["frac_basis"] = ("bytes the kernel moves: per lane 64 B (hit, winner's triangle) + the camera ray's record "
+                           f"({ray_b:.0f} B: tuning key 33 = {gen}), per wave 128 B per node visit + 48 B per leaf "
+                           "record + 48 B per triangle record (scalar loads, once per wave)")
         lpf = max(1.0, packet_launches / frames)  # packet launches per frame (the counting frame is one frame)
         e["wave_records_per_launch"] = {"node_visits": wn / lpf, "leaf_records": wl / lpf, "triangle_records": wt / lpf}
         e["lane_basis_bytes_per_launch"] = lane_b / lpf

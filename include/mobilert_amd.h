@@ -229,7 +229,12 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  * key 27 = the last shadow walk of a pass on the render stream with the closest-hit spill stacks
  *          (1, default) or on the shadow stream (0),
  * key 28 = at most this many workgroups per walk launch (0, default: the occupancy grid; 1-65536):
- *          a test knob, every grid size walks every ray.
+ *          a test knob, every grid size walks every ray,
+ * key 33 = where level 1 is not fused (key 17), the packet walk generates the camera rays itself and
+ *          stores the records the shading reads (1), or k_shade regenerates them too (2, Whitted /
+ *          PathTracer; default), or the walk reads those of a k_raygen launch (0),
+ * key 34 = level 1's resolve folded into the per-pixel accumulation, one launch (1, default), or the
+ *          resolve and k_accumulate launched separately (0).
  * (Keys 4, 12-15, 18, 19-25, 29, 30, 32 - binned emission, queue sorting, graph replay, the tile
  * kernel, a shadow-occluder probe, the deeper levels' walk and shading in one launch, a CU-masked
  * shadow stream, k_shade's vertices binned by shading class, the shadow walks yielding to the next

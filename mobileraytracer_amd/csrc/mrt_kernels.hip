@@ -275,18 +275,43 @@ __global__ __launch_bounds__(kWalkThreads, MRT_WALK_WAVES) void k_trace(DScene s
     }
 }
 
+// Camera rays generated where they are walked (round 6, tuning key 33): cameraRay (k_raygen's
+// function) per lane at the start of each packet, and the records k_shade reads stored from there,
+// so that k_raygen's launch and the walk's reads of its records are gone.
+struct PacketRaysStore {
+    const RaygenArgs* a;
+    Level lv;
+    __device__ __forceinline__ void operator()(int i, float4* o4, float4* d4) const {
+        cameraRay(*a, i, o4, d4);
+        if (a->storeRays != 0) {  // (else k_shade regenerates them)
+            lv.rO[i] = *o4;
+            lv.rD[i] = *d4;
+            lv.tree[i] = 1u;
+        }
+    }
+};
+
 // Level-1 (camera) rays in cull modes 0 and 3: the wave-coherent walk (mrt_trace_packet.hpp).
-template <bool kCount, int kCull>
-__global__ __launch_bounds__(kWalkThreads, 8) void k_trace_packet(DScene s, Level lv, int* counters, int level,
-                                                                   int2* gstack, int gdepth, unsigned long long* stats) {
+// kGen: the walk generates the camera rays (PacketRaysStore) instead of reading k_raygen's.
+// (7 waves per SIMD with kGen: at 8 its 64 VGPRs spilled 12 B; the packet walk measured the same
+// at 6, 7 and 8, section 3.1 of DESIGN.md)
+template <bool kCount, int kCull, bool kGen>
+__global__ __launch_bounds__(kWalkThreads, kGen ? 7 : 8) void k_trace_packet(DScene s, Level lv, int* counters, int level,
+                                                                   int2* gstack, int gdepth, unsigned long long* stats,
+                                                                   RaygenArgs ra) {
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];  // per-lane fallback walks only
     __shared__ int waveStacks[kWalkThreads / 64][kPacketStack];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
     const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    const int count = min(counters[cntRays(level)], lv.cap);
+    if (kGen && blockIdx.x == 0 && threadIdx.x == 0) counters[cntRays(level)] = ra.nPaths;  // (k_raygen's count)
+    const int count = kGen ? min(ra.nPaths, lv.cap) : min(counters[cntRays(level)], lv.cap);
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
-    tracePacket<kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, waveStacks[threadIdx.x / 64]);
+    if constexpr (kGen)
+        tracePacket<kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, waveStacks[threadIdx.x / 64], NoPost(),
+                                   PacketRaysStore{&ra, lv});
+    else
+        tracePacket<kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, waveStacks[threadIdx.x / 64]);
     if (kCount) {
         reduceCounts<kCount>(cnt, stats, kStatNodes, kStatTris, kStatLeaves);
         reduceCounts<kCount>(cnt, stats, kStatLevelNodes + level - 1, kStatLevelTris + level - 1, kStatLevelLeaves + level - 1);
@@ -665,9 +690,11 @@ __device__ __forceinline__ v3 firstChildDir(const ShadeState& v) {
 // which the hit, ray and shading-record gathers keep busy.  (kShadeLdsTable: the launch falls
 // back to the general kernel for scenes whose tables do not fit.)
 constexpr int kShadeLdsTable = 256;  // float4: 4 per material, then 4 per light
-template <int kShader, bool kFull>
+// kRegen (level 1, tuning key 33 = 2): the camera rays regenerated here (cameraRay on ra, the
+// function the packet walk generated them with: the same bits) instead of read from lv's records
+template <int kShader, bool kFull, bool kRegen>
 __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a,
-                                                  int deadNext) {
+                                                  int deadNext, RaygenArgs ra) {
     __shared__ float4 tab[kFull ? 1 : kShadeLdsTable];
     if constexpr (!kFull) {
         const int nm = 4 * s.nMats, nt = nm + 4 * s.nLights;
@@ -696,7 +723,16 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
                 lv.kd[i] = kw;
                 lv.last[i] = kw;
             }
-            v = shadePrepare<kShader>(s, lv.rO[i], lv.rD[i], h, lv.tree[i], level, a, kw, mats, lights);
+            float4 o4, d4;
+            uint32_t tc = 1u;
+            if constexpr (kRegen) {
+                cameraRay(ra, i, &o4, &d4);
+            } else {
+                o4 = lv.rO[i];
+                d4 = lv.rD[i];
+                tc = lv.tree[i];
+            }
+            v = shadePrepare<kShader>(s, o4, d4, h, tc, level, a, kw, mats, lights);
             if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
         }
         int childBase, shadowBase;
@@ -862,12 +898,13 @@ __global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int
 // kTex: a textured scene (the Kd replay below); untextured scenes run the lean instantiation
 // Vertex i of level `level`: its radiance from its shadow rays' flags and its children's results,
 // in the reference's float-op order (Whitted.cpp:36-92, PathTracer.cpp:22-142).
-template <int kShader, bool kTex>
-__device__ __forceinline__ void resolveVertex(const DScene& s, const Level& lv, const Level& nx, int i, int level,
-                                              const ShadeArgs& a, int deadChildren) {
+// Returns the radiance (w: the hit-a-light flag), or for a terminal vertex (va.x < 0) the record
+// k_shade wrote; kLast: write the textured scenes' last-texel record for the level above.
+template <int kShader, bool kTex, bool kLast>
+__device__ __forceinline__ float4 resolveValue(const DScene& s, const Level& lv, const Level& nx, int i, int level,
+                                               const ShadeArgs& a, int deadChildren, int4 va) {
     {
-        const int4 va = lv.vtx[i];
-        if (va.x < 0) return;  // terminal: res written by k_shade
+        if (va.x < 0) return lv.res[i];  // terminal: res written by k_shade
         // children (consecutive from va.z in the order diffuse, specular, transmission); an
         // index past the queue only occurs in an overflowed pass, which is redone
         int c = va.z;
@@ -939,9 +976,17 @@ __device__ __forceinline__ void resolveVertex(const DScene& s, const Level& lv, 
             rgb = rgb + LiT;
             out = make_float4(rgb.x, rgb.y, rgb.z, hitLight ? 1.0F : 0.0F);
         }
-        lv.res[i] = out;
-        if (kTex) lv.last[i] = lT.w >= 0.0F ? lT : (lS.w >= 0.0F ? lS : (lD.w >= 0.0F ? lD : own));
+        if (kTex && kLast) lv.last[i] = lT.w >= 0.0F ? lT : (lS.w >= 0.0F ? lS : (lD.w >= 0.0F ? lD : own));
+        return out;
     }
+}
+
+template <int kShader, bool kTex>
+__device__ __forceinline__ void resolveVertex(const DScene& s, const Level& lv, const Level& nx, int i, int level,
+                                              const ShadeArgs& a, int deadChildren) {
+    const int4 va = lv.vtx[i];
+    if (va.x < 0) return;  // terminal: res written by k_shade
+    lv.res[i] = resolveValue<kShader, kTex, true>(s, lv, nx, i, level, a, deadChildren, va);
 }
 
 template <int kShader, bool kTex>
@@ -1159,26 +1204,38 @@ int persistentGrid(K kernel, int slot, int maxThreads) {
         else MRT_LAUNCH_ONE(KERNEL, 1, kCullNone, SLOT + 3);                                                   \
     } while (0)
 
+bool packetLevel1(const DScene& s) {
+    return s.accel == kAccBVH && s.packet != 0 && s.variant == 1 && (s.cull == kCullNone || s.cull == kCullExact);
+}
+
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
-                 unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st) {
+                 unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st, const RaygenArgs* gen) {
     if (s.accel != kAccBVH) {
         hipLaunchKernelGGL((k_trace_other<false>), dim3(1024), dim3(256), 0, st, s, lv, counters, level);
         return;
     }
     const int gridPct = 100;
-    if (level == 1 && s.packet != 0 && s.variant == 1 && (s.cull == kCullNone || s.cull == kCullExact)) {
-        const int g = std::max(1, persistentGrid(k_trace_packet<false, kCullExact>, 10, maxThreads));
+    if (level == 1 && packetLevel1(s)) {
+        const int g = std::max(1, gen != nullptr ? persistentGrid(k_trace_packet<false, kCullExact, true>, 11, maxThreads)
+                                                  : persistentGrid(k_trace_packet<false, kCullExact, false>, 10, maxThreads));
+        const RaygenArgs ra = gen != nullptr ? *gen : RaygenArgs{};
+#define MRT_LAUNCH_PACKET(CNT, C, GEN)                                                                        \
+        hipLaunchKernelGGL((k_trace_packet<CNT, C, GEN>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, \
+                           gstack, gdepth, stats, ra)
+#define MRT_LAUNCH_PACKET_GEN(CNT, C)                     \
+        do {                                              \
+            if (gen != nullptr) MRT_LAUNCH_PACKET(CNT, C, true); \
+            else MRT_LAUNCH_PACKET(CNT, C, false);        \
+        } while (0)
         if (s.cull == kCullExact) {
-            if (countStats)
-                hipLaunchKernelGGL((k_trace_packet<true, kCullExact>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats);
-            else
-                hipLaunchKernelGGL((k_trace_packet<false, kCullExact>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+            if (countStats) MRT_LAUNCH_PACKET_GEN(true, kCullExact);
+            else MRT_LAUNCH_PACKET_GEN(false, kCullExact);
         } else {
-            if (countStats)
-                hipLaunchKernelGGL((k_trace_packet<true, kCullNone>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats);
-            else
-                hipLaunchKernelGGL((k_trace_packet<false, kCullNone>), dim3(g), dim3(kWalkThreads), 0, st, s, lv, counters, level, gstack, gdepth, stats);
+            if (countStats) MRT_LAUNCH_PACKET_GEN(true, kCullNone);
+            else MRT_LAUNCH_PACKET_GEN(false, kCullNone);
         }
+#undef MRT_LAUNCH_PACKET_GEN
+#undef MRT_LAUNCH_PACKET
         return;
     }
     MRT_LAUNCH_WALK(k_trace, 0);
@@ -1221,22 +1278,33 @@ void launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const L
 }
 
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
-                 const ShadeArgs& a, int grid, hipStream_t st, bool deadNext) {
+                 const ShadeArgs& a, int grid, hipStream_t st, bool deadNext, const RaygenArgs* regen) {
     const int dead = deadNext ? 1 : 0;
+    const RaygenArgs ra = regen != nullptr ? *regen : RaygenArgs{};
+    // (a separate instantiation: the regeneration in the shared one cost 8 VGPRs and a wave per SIMD)
+#define MRT_LAUNCH_SHADE(SH, FULL)                                                                          \
+    do {                                                                                                    \
+        if (regen != nullptr)                                                                               \
+            hipLaunchKernelGGL((k_shade<SH, FULL, true>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, \
+                               level, a, dead, ra);                                                         \
+        else                                                                                                \
+            hipLaunchKernelGGL((k_shade<SH, FULL, false>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, \
+                               level, a, dead, ra);                                                         \
+    } while (0)
     const bool full = s.textured != 0 || a.stats != nullptr || s.leanShade == 0 ||
                       4 * (s.nMats + s.nLights) > kShadeLdsTable;
     switch (shader) {
         case kShaderWhitted:
             if (full)
-                hipLaunchKernelGGL((k_shade<kShaderWhitted, true>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a, dead);
+                MRT_LAUNCH_SHADE(kShaderWhitted, true);
             else
-                hipLaunchKernelGGL((k_shade<kShaderWhitted, false>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a, dead);
+                MRT_LAUNCH_SHADE(kShaderWhitted, false);
             break;
         case kShaderPathTracer:
             if (full)
-                hipLaunchKernelGGL((k_shade<kShaderPathTracer, true>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a, dead);
+                MRT_LAUNCH_SHADE(kShaderPathTracer, true);
             else
-                hipLaunchKernelGGL((k_shade<kShaderPathTracer, false>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a, dead);
+                MRT_LAUNCH_SHADE(kShaderPathTracer, false);
             break;
         case kShaderDepthMap:
             hipLaunchKernelGGL(k_shade_simple<kShaderDepthMap>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, a);
@@ -1248,6 +1316,7 @@ void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, 
             hipLaunchKernelGGL(k_shade_simple<kShaderNoShadows>, dim3(grid), dim3(kBlock), 0, st, s, lv, counters, level, a);
             break;
     }
+#undef MRT_LAUNCH_SHADE
 }
 
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
@@ -1265,6 +1334,66 @@ void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx
         else
             hipLaunchKernelGGL((k_resolve<kShaderWhitted, false>), dim3(grid), dim3(256), 0, st, s, lv, nx, counters, level, a, dead);
     }  // single-level shaders: k_shade_simple wrote the final results
+}
+
+// Level 1's resolve and the accumulation in one launch (round 6, tuning key 34): a thread per path
+// (q * spp + s, level 1) resolves its camera-ray vertex as k_resolve does, and the first lane of each
+// pixel slot's spp consecutive lanes (spp divides 64, so a slot's samples share a wave) pulls the
+// others' radiance and averages them in sample order as k_accumulate does, so level 1's radiance
+// records are never written or re-read.  The same resolveValue and incrementalAvg on the same
+// inputs: the same bits.  (A thread per slot resolving its samples one after another measured
+// slower, C4 13.65 -> 13.78 ms: four dependent gather chains per thread.)
+template <int kShader, bool kTex>
+__global__ __launch_bounds__(256) void k_resolve_accumulate(DScene s, Level lv, Level nx, ShadeArgs sa, int deadChildren,
+                                                            AccumArgs a, int32_t* bitmap, int32_t* packed) {
+    const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    const int n = a.nSlots * a.spp;
+    float4 r = make_float4(0.0F, 0.0F, 0.0F, 0.0F);
+    if (i < n) r = resolveValue<kShader, kTex, false>(s, lv, nx, i, 1, sa, deadChildren, lv.vtx[i]);
+    const int k = i % a.spp;  // this path's sample; lanes i - k .. i - k + spp - 1 hold its slot's
+    int32_t c = 0;
+    for (int j = 0; j < a.spp; ++j) {  // (wave-uniform trip count)
+        const int from = static_cast<int>(threadIdx.x & 63u) + j;  // lane of sample j when k == 0
+        const float x = __shfl(r.x, from, 64), y = __shfl(r.y, from, 64), z = __shfl(r.z, from, 64);
+        if (k == 0 && i < n) {
+            if (j == 0 && a.sampleBase > 0) {  // the running average (progressive passes)
+                const int slot = a.slotBase + i / a.spp;
+                int px, py;
+                slotToXY(a.map, slot, &px, &py);
+                c = bitmap != nullptr ? bitmap[py * a.width + px] : (packed != nullptr ? packed[slot] : 0);
+            }
+            c = incrementalAvg(v3{x, y, z}, c, a.sampleBase + j + 1);
+        }
+    }
+    if (k == 0 && i < n) {
+        const int slot = a.slotBase + i / a.spp;
+        int px, py;
+        slotToXY(a.map, slot, &px, &py);
+        if (bitmap != nullptr) bitmap[py * a.width + px] = c;
+        if (packed != nullptr) packed[slot] = c;
+    }
+}
+
+bool launchResolveAccumulate(int shader, const DScene& s, const Level& lv, const Level& nx, const ShadeArgs& sa,
+                             bool deadChildren, const AccumArgs& a, int32_t* bitmap, int32_t* packed, hipStream_t st) {
+    if (a.spp <= 0 || 64 % a.spp != 0) return false;  // a slot's samples must share a wave
+    const int dead = deadChildren ? 1 : 0;
+    const int blocks = std::max(1, (a.nSlots * a.spp + 255) / 256);
+#define MRT_LAUNCH_RA(SH, TEX)                                                                                  \
+    hipLaunchKernelGGL((k_resolve_accumulate<SH, TEX>), dim3(blocks), dim3(256), 0, st, s, lv, nx, sa, dead, a, \
+                       bitmap, packed)
+    const bool tex = s.textured != 0;
+    if (shader == kShaderPathTracer) {
+        if (tex) MRT_LAUNCH_RA(kShaderPathTracer, true);
+        else MRT_LAUNCH_RA(kShaderPathTracer, false);
+    } else if (shader == kShaderWhitted) {
+        if (tex) MRT_LAUNCH_RA(kShaderWhitted, true);
+        else MRT_LAUNCH_RA(kShaderWhitted, false);
+    } else {
+        return false;
+    }
+#undef MRT_LAUNCH_RA
+    return true;
 }
 
 void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, int32_t* packed, hipStream_t st) {
@@ -1301,8 +1430,8 @@ int traceResidentThreadsPerCU() {
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullCertified>),
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullNone>),
                              reinterpret_cast<const void*>(k_shadow<false, 1, kCullExact>),
-                             reinterpret_cast<const void*>(k_trace_packet<false, kCullExact>),
-                             reinterpret_cast<const void*>(k_trace_packet<false, kCullNone>)};
+                             reinterpret_cast<const void*>(k_trace_packet<false, kCullExact, false>),
+                             reinterpret_cast<const void*>(k_trace_packet<false, kCullNone, false>)};
     for (const void* k : kernels) {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWalkThreads, 0) == hipSuccess)

@@ -109,6 +109,10 @@ struct RaygenArgs {
     // (every draw constJitter); C_wrapper.cpp:144-148 picks StaticHaltonSeq iff samplesPixel > 1
     int tableJitter;
     float constJitter;
+    // the level-1 packet walk generating these rays (tuning key 33): 1 also stores their records,
+    // 0 leaves them to k_shade to regenerate
+    int storeRays;
+    int pad;
 };
 
 struct ShadeArgs {
@@ -131,8 +135,12 @@ struct AccumArgs {
 
 
 void launchRaygen(const RaygenArgs& a, const Level& lv, int* counters, hipStream_t st);
+// gen (level 1 with the packet walk, packetLevel1): the walk generates the camera rays itself and
+// stores their records, replacing launchRaygen
+bool packetLevel1(const DScene& s);
 void launchTrace(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
-                 unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st);
+                 unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st,
+                 const RaygenArgs* gen = nullptr);
 void launchShadow(const DScene& s, const Level& lv, int* counters, int level, int2* gstack, int gdepth,
                   unsigned long long* stats, bool countStats, int maxThreads, hipStream_t st, int gridPct = 100);
 // deadNext: level + 1 is the depth-capped last level (its rays are counted, never written)
@@ -143,13 +151,19 @@ bool canFuseLevel1(int shader, const DScene& s, const ShadeArgs& a);
 void launchTraceShadeFused(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                            const ShadeArgs& a, int2* gstack, int gdepth, int maxThreads, hipStream_t st, bool deadNext,
                            const RaygenArgs& ra);
+// regen (level 1, Whitted / PathTracer): the camera rays are regenerated from *regen (cameraRay)
+// instead of read from lv's records, which the packet walk then does not store
 void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
-                 const ShadeArgs& a, int grid, hipStream_t st, bool deadNext = false);
+                 const ShadeArgs& a, int grid, hipStream_t st, bool deadNext = false,
+                 const RaygenArgs* regen = nullptr);
 // deadChildren: level + 1 is the depth-capped last level, whose results are all zero; its
 // records are then not read (a zero child adds exactly nothing, section 3 of DESIGN.md)
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,
                    const ShadeArgs& a, int grid, hipStream_t st, bool deadChildren = false);
 void launchAccumulate(const AccumArgs& a, const float4* res, int32_t* bitmap, int32_t* packed, hipStream_t st);
+// level 1's resolve and the accumulation in one launch (Whitted / PathTracer; false: not launched)
+bool launchResolveAccumulate(int shader, const DScene& s, const Level& lv, const Level& nx, const ShadeArgs& sa,
+                             bool deadChildren, const AccumArgs& a, int32_t* bitmap, int32_t* packed, hipStream_t st);
 // rank 0's frame assembly: up to kUnpackRanks shards per launch (rank first + k reads row first + k
 // of the gathered array, stride entries apart)
 constexpr int kUnpackRanks = 16;

@@ -266,6 +266,9 @@ struct mrt_renderer {
     int skipLast = 1;                    // tuning key 7: no closest-hit walk for the depth-capped last level
     int shadowGridPct = 0;               // tuning key 6: shadow walk grid, percent of its occupancy grid (0 auto)
     int fuseL1Mode = -1;                 // tuning key 17: level 1 fused (1), in separate launches (0), -1 auto
+    int genL1 = 2;                       // tuning key 33: the unfused level-1 packet walk generates its camera rays
+                                         // (1: and stores them; 2: k_shade regenerates them; 0: k_raygen)
+    int resolveAcc = 1;                  // tuning key 34: level 1's resolve and the accumulation in one launch
     int refill = 0;                      // tuning key 9: walk refill threshold (0 auto: by paths per lane)
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
@@ -802,7 +805,15 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         const bool fuseL1 = nLevels >= 1 && !(skipLast && nLevels == 1) && !(skipLastShade && nLevels == 1) &&
                             canFuseLevel1(shader, r->ds, sa);
         r->fusedL1 = fuseL1;
-        if (!fuseL1) launchRaygen(ra, pp.levels[1], pp.counters, st);
+        // Unfused, the packet walk generates the camera rays and stores the records k_shade reads
+        // (tuning key 33): no k_raygen launch, no ray reads in the walk
+        const bool genL1 = !fuseL1 && r->genL1 != 0 && nLevels >= 1 && !(skipLast && nLevels == 1) &&
+                           packetLevel1(r->ds);
+        // ... and with key 33 = 2 k_shade regenerates them instead of reading stored records
+        const bool regenL1 = genL1 && r->genL1 == 2 && (shader == kShaderWhitted || shader == kShaderPathTracer) &&
+                             !(skipLastShade && nLevels == 1);
+        ra.storeRays = regenL1 ? 0 : 1;
+        if (!fuseL1 && !genL1) launchRaygen(ra, pp.levels[1], pp.counters, st);
         // the walk launches' thread cap (tuning key 28 narrows it; the spill stacks hold traceThreads)
         const int walkThreads = r->walkGridCap > 0 ? std::min(r->traceThreads, r->walkGridCap * kBlock)
                                                    : r->traceThreads;
@@ -850,13 +861,13 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
             }
             if (!fused && !(skipLast && l == nLevels))
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting,
-                            walkThreads, st);
+                            walkThreads, st, genL1 && l == 1 ? &ra : nullptr);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
             if (!fused && !(skipLastShade && l == nLevels)) {
                 launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa,
                             shadePerCU > 0 ? r->cus * shadePerCU : r->workGrid, st,
-                            skipLastShade && l + 1 == nLevels);
+                            skipLastShade && l + 1 == nLevels, regenL1 && l == 1 ? &ra : nullptr);
                 ++r->shadeLaunches;
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
@@ -885,10 +896,6 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // the resolves wait for every shadow walk on the shadow stream
         const int lastOnShadowStream = lastOnRender ? nLevels - 2 : nLevels;
         if (sb != st && lastOnShadowStream >= 1) MRT_HIP(hipStreamWaitEvent(st, shadowDone[lastOnShadowStream], 0));
-        for (int l = skipLastShade ? nLevels - 1 : nLevels; l >= 1; --l) {
-            launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, st,
-                          skipLastShade && l == nLevels - 1);
-        }
         AccumArgs aa{};
         aa.map = map;
         aa.width = r->cfg.width;
@@ -896,7 +903,20 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         aa.nSlots = nChunk;
         aa.spp = spp;
         aa.sampleBase = sampleBase;
-        launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, st);
+        const int topResolve = skipLastShade ? nLevels - 1 : nLevels;
+        // level 1's resolve folded into the accumulation (tuning key 34): no level-1 radiance records
+        const bool resolveAcc = r->resolveAcc != 0 && topResolve >= 1;
+        for (int l = topResolve; l >= (resolveAcc ? 2 : 1); --l) {
+            launchResolve(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa, r->workGrid, st,
+                          skipLastShade && l == nLevels - 1);
+        }
+        if (!resolveAcc || !launchResolveAccumulate(shader, r->ds, pp.levels[1], pp.levels[2], sa,
+                                                    skipLastShade && 1 == nLevels - 1, aa, dBitmap, dPacked, st)) {
+            if (resolveAcc)  // (single-level shaders: nothing to resolve)
+                launchResolve(shader, r->ds, pp.levels[1], pp.levels[2], pp.counters, 1, sa, r->workGrid, st,
+                              skipLastShade && 1 == nLevels - 1);
+            launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, st);
+        }
         launchTally(pp.counters, nLevels, pp.stats, st, skipLast ? nLevels : 0);
     }
 }
@@ -1624,6 +1644,14 @@ static int setTuningOne(mrt_renderer* r, int32_t key, int32_t value) {
         r->lastShadowRender = value;
         return 0;
     }
+    if (key == 33 && value >= 0 && value <= 2) {
+        r->genL1 = value;
+        return 0;
+    }
+    if (key == 34 && (value == 0 || value == 1)) {
+        r->resolveAcc = value;
+        return 0;
+    }
     if (key == 28 && value >= 0 && value <= 65536) {
         r->walkGridCap = value;
         return 0;
@@ -1806,6 +1834,8 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 16: *value = r->ds.packet; return 0;
         case 17: *value = r->fuseL1Mode; return 0;
         case 27: *value = r->lastShadowRender; return 0;
+        case 33: *value = r->genL1; return 0;
+        case 34: *value = r->resolveAcc; return 0;
         case 28: *value = r->walkGridCap; return 0;
         default: break;
     }

@@ -394,7 +394,10 @@ def test_fused_level1_shading_is_invariant():
     """Level 1's packet walk shading its own hits (tuning key 17, on by default:
     k_trace_packet_shade, one launch instead of the walk and k_shade) gives the separate
     launches' bitmap, ray counts and primary hits: Whitted and PathTracer, 2 light samples,
-    both cull modes that walk packets, a textured scene (which keeps the separate launches)."""
+    both cull modes that walk packets, a textured scene (which keeps the separate launches).
+    Unfused, the packet walk generating the camera rays itself (tuning key 33: 1 storing their
+    records, 2 leaving them to k_shade to regenerate) gives k_raygen's rays: the same bitmap, ray
+    counts and primary hits with it off."""
     import mobileraytracer_amd as m
     cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
              make_cfg(128, 128, shader=1, scene="water", max_depth=4),
@@ -405,9 +408,11 @@ def test_fused_level1_shading_is_invariant():
         outs = []
         with m.Renderer(cfg) as r:
             assert r.get_tuning(17) == -1  # auto (by paths per walk lane) since round 6
-            for fuse, cull in ((1, 3), (0, 3), (1, 0), (0, 0)):
+            assert r.get_tuning(33) == 2
+            for fuse, cull, gen in ((1, 3, 1), (0, 3, 1), (0, 3, 0), (0, 3, 2), (1, 0, 1), (0, 0, 2), (0, 0, 0)):
                 r.set_tuning(17, fuse)
                 r.set_tuning(2, cull)
+                r.set_tuning(33, gen)
                 bm = np.zeros(cfg.width * cfg.height, np.int32)
                 r.render_frame(bm)
                 st = r.frame_stats()
@@ -416,6 +421,37 @@ def test_fused_level1_shading_is_invariant():
             assert np.array_equal(outs[0][0], other[0]), cfg
             assert outs[0][1:4] == other[1:4], cfg
             assert all(np.array_equal(a, b) for a, b in zip(outs[0][4], other[4])), cfg
+
+
+def test_resolve_accumulate_fusion_is_invariant(oracle_mod):
+    """Level 1's resolve folded into the per-pixel accumulation (tuning key 34, on by default): the
+    same bitmap as the separate k_resolve + k_accumulate launches for Whitted and PathTracer, a
+    textured scene, 2 light samples, the depth cap at 1 (level 2 shaded dead), a single-level shader
+    (nothing to resolve), progressive passes (the running average carried between samples) and a
+    multi-pass frame (maxPathsPerPass); and the oracle's bitmap where it is cheap."""
+    import dataclasses
+    import mobileraytracer_amd as m
+    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+             make_cfg(128, 128, shader=1, scene="water", max_depth=4),
+             make_cfg(96, 96, shader=2, scene="water", spp=2, max_depth=1, spl=2),
+             make_cfg(128, 128, shader=2, scene="teapot", spp=3, max_depth=3),
+             make_cfg(64, 64, shader=0, spp=2),
+             make_cfg(64, 64, shader=2, spp=3, max_depth=6, progressive=1),
+             make_cfg(96, 64, shader=2, spp=4, max_depth=4, maxPathsPerPass=5000))
+    for cfg in cases:
+        outs = []
+        with m.Renderer(cfg) as r:
+            assert r.get_tuning(34) == 1
+            for v in (1, 0):
+                r.set_tuning(34, v)
+                bm = np.full(cfg.width * cfg.height, SENTINEL, np.int32)
+                r.render_frame(bm)
+                outs.append(bm)
+        assert np.array_equal(outs[0], outs[1]), cfg
+    cfg = cases[-2]  # progressive, key 34 on: the oracle's bitmap
+    ref, _ = oracle_for(oracle_mod, dataclasses.replace(cfg, progressive=0)).render(threads=4)
+    bm, _, _ = gpu_render(cfg)
+    assert np.array_equal(bm, ref)
 
 
 def test_last_shadow_walk_on_render_stream_is_invariant(oracle_mod):
