@@ -68,11 +68,28 @@ struct DeviceMem {
 // 91.4; C4 13.94-13.97 -> 13.68-13.70 ms, N = 8 shard 2.53 -> 2.47 ms, the flat stand-in unchanged
 // (profiles/r06_ray_collapse_ab.txt).  MOBILERT_COLLAPSE=area: surface areas (an empty vector);
 // =greedy: round 1's greedy collapse.  Any cost gives an exact walk.
-std::vector<double> walkCollapseCosts(const std::vector<mrt::HBVHNode>& wn, const mrt::HScene& sc, const mrt::GCamera& cam,
-                                      int width, int height, int maxDepth) {
+// The same sample first rotates the walk tree's BVH2 where that lowers the collapse's cost under it
+// (mrt::rotateForRays, MOBILERT_RAY_ROT sweeps, default kRayRotSweeps; round 6), and the costs are
+// those of the rotated tree.  Returns the tree to collapse; *cost empty: collapse by area.
+#ifndef MRT_RAY_ROT_SWEEPS
+#define MRT_RAY_ROT_SWEEPS 1
+#endif
+constexpr int kRayRotSweeps = MRT_RAY_ROT_SWEEPS;
+std::vector<mrt::HBVHNode> frameWalkTree(const std::vector<mrt::HBVHNode>& wn, const mrt::HScene& sc, const mrt::GCamera& cam,
+                                         int width, int height, int maxDepth, std::vector<double>* cost) {
+    cost->clear();
     const char* ce = std::getenv("MOBILERT_COLLAPSE");
-    if (ce != nullptr && (std::string(ce) == "area" || std::string(ce) == "greedy")) return {};
-    return mrt::frameRayNodeCosts(wn, sc, cam, width, height, maxDepth);
+    if (ce != nullptr && (std::string(ce) == "area" || std::string(ce) == "greedy")) return wn;
+    if (wn.empty() || sc.triangles.empty() || width <= 0 || height <= 0) {
+        cost->assign(wn.size(), 0.0);
+        return wn;
+    }
+    const std::vector<mrt::SampleRay> rays = mrt::sampleFrameRays(wn, sc, cam, maxDepth);
+    const char* re = std::getenv("MOBILERT_RAY_ROT");
+    const int sweeps = re != nullptr ? std::atoi(re) : kRayRotSweeps;
+    std::vector<mrt::HBVHNode> out = sweeps > 0 ? mrt::rotateForRays(wn, rays, sweeps) : wn;
+    *cost = mrt::sampleRayNodeCosts(out, rays);
+    return out;
 }
 
 int bvhDepth(const std::vector<mrt::HBVHNode>& nodes) {
@@ -385,7 +402,10 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     // the walk tree: the reference leaves regrouped by a full-sweep SAH (rebuildOverLeaves; the
     // reference tree itself with MOBILERT_WALK_TREE=0).  Rays with a non-finite 1/d and the
     // per-wave reference walk use the reference tree, appended after it in the same node array.
-    const std::vector<HBVHNode> wn = walkTreeOver(tn);
+    // ... rotated for the frame's ray sample, whose node costs the wide collapse below uses
+    std::vector<double> rayCost;
+    const std::vector<HBVHNode> wn =
+        frameWalkTree(walkTreeOver(tn), sc, r->cam, r->cfg.width, r->cfg.height, r->maxDepth, &rayCost);
     r->nTri = static_cast<int64_t>(sc.triangles.size());
     r->nPlanes = static_cast<int64_t>(sc.planes.size());
     r->nSpheres = static_cast<int64_t>(sc.spheres.size());
@@ -407,7 +427,6 @@ void uploadScene(mrt_renderer* r, mrt::HScene& sc) {
     // the walk tree, numbered (top breadth-first), then quantized; the reference tree in its own
     // GNode array
     std::vector<QNode4> qn;
-    const std::vector<double> rayCost = walkCollapseCosts(wn, sc, r->cam, r->cfg.width, r->cfg.height, r->maxDepth);
     d.qEnabled = toQuantizedBVH4(wn, sc.triangles.size(), &d.triRoot, kTopNodesMax, &d.triTop, &d.qgrid, &qn, nullptr,
                                  rayCost.empty() ? nullptr : &rayCost) ? 1 : 0;
     if (d.qEnabled == 0 || qn.empty()) qn.resize(1);  // (a leaf or empty root: no inner node)
@@ -1714,14 +1733,14 @@ int64_t mrt_walk_tree(const mrt_config* cfg, uint32_t* nodes, float* grid, int32
         }
         std::vector<int32_t> perm;
         const std::vector<HBVHNode> tn = buildBVH(&sc.triangles, &perm);
-        const std::vector<HBVHNode> wn = walkTreeOver(tn);
         GRoot r{};
         QGrid g{};
         std::vector<QNode4> qn;
         int top = 0;
         const int maxDepth = cfg->maxDepth > 0 ? cfg->maxDepth : kRayDepthMaxDefault;
-        const std::vector<double> cost =
-            haveCam ? walkCollapseCosts(wn, sc, cam, cfg->width, cfg->height, maxDepth) : std::vector<double>{};
+        std::vector<double> cost;
+        const std::vector<HBVHNode> wn = haveCam ? frameWalkTree(walkTreeOver(tn), sc, cam, cfg->width, cfg->height, maxDepth, &cost)
+                                                 : walkTreeOver(tn);
         if (!toQuantizedBVH4(wn, sc.triangles.size(), &r, kTopNodesMax, &top, &g, &qn, nullptr,
                              cost.empty() ? nullptr : &cost))
             throw std::runtime_error("walk tree not quantizable (non-finite boxes)");

@@ -1973,11 +1973,19 @@ std::vector<SampleRay> sampleFrameRays(const std::vector<HBVHNode>& nodes, const
 
 std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
                                       int width, int height, int maxDepth) {
+    if (nodes.empty() || sc.triangles.empty() || width <= 0 || height <= 0) return std::vector<double>(nodes.size(), 0.0);
+    return sampleRayNodeCosts(nodes, sampleFrameRays(nodes, sc, cam, maxDepth));
+}
+
+// the share of the root's area every node's cost carries besides its sample rays (so that nodes no
+// sample ray reaches are still ordered)
+constexpr float kRayCostFloor = 0.01F;
+
+std::vector<double> sampleRayNodeCosts(const std::vector<HBVHNode>& nodes, const std::vector<SampleRay>& rays) {
     std::vector<double> cost(nodes.size(), 0.0);
-    if (nodes.empty() || sc.triangles.empty() || width <= 0 || height <= 0) return cost;
-    const std::vector<SampleRay> rays = sampleFrameRays(nodes, sc, cam, maxDepth);
+    if (nodes.empty() || rays.empty()) return cost;
     auto inner = [&](size_t i) { return nodes[i].numPrimitives == 0 && nodes.size() > 1; };
-    constexpr float floorW = 0.01F;
+    constexpr float floorW = kRayCostFloor;
     // every node whose box each sample ray's half-line passes (the exact walk culls no inner node)
     const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::vector<double>> part(hw, std::vector<double>(nodes.size(), 0.0));
@@ -2018,6 +2026,206 @@ std::vector<double> frameRayNodeCosts(const std::vector<HBVHNode>& nodes, const 
         cost[i] = s + floorW * total * area(i) / rootArea;
     }
     return cost;
+}
+
+// Rotations of the walk tree's BVH2 (Kopta et al.'s four per inner node, as rotateForWide) kept where
+// they lower the optimal 4-wide collapse's cost under the frame's ray sample: a node costs the summed
+// weight of the sample half-lines that pass its box, plus kRayCostFloor of its share of the root's
+// area (sampleRayNodeCosts' cost, the one toQuantizedBVH4 collapses with).  A rotation at n changes
+// one box, that of n's child m, and every ray passing m's new box passes n's: m's rays are re-counted
+// from n's list.  Leaves and their boxes are untouched and inner boxes stay exact unions (the walk
+// tree's exactness argument); no rotation makes a subtree taller than it was.
+std::vector<HBVHNode> rotateForRays(const std::vector<HBVHNode>& in, const std::vector<SampleRay>& rays, int sweeps) {
+    if (in.size() < 8 || sweeps <= 0 || rays.empty() || in[0].numPrimitives > 0) return in;
+    constexpr int W1 = kWalkWidth + 1;
+    struct R {
+        HAABB box;
+        int32_t l = -1, r = -1, parent = -1, first = 0, count = 0;
+        int32_t height = 0, maxHeight = 0;  // maxHeight: the input's height of this node (a bound)
+        double cost = 0.0;
+        double F[W1] = {};
+    };
+    std::vector<R> t;
+    {
+        std::vector<std::pair<int32_t, int32_t>> st{{0, -1}};
+        while (!st.empty()) {
+            const auto [i, parent] = st.back();
+            st.pop_back();
+            const int32_t k = static_cast<int32_t>(t.size());
+            t.emplace_back();
+            R& n = t.back();
+            const HBVHNode& h = in[static_cast<size_t>(i)];
+            n.box = h.box;
+            n.parent = parent;
+            if (parent >= 0) {
+                R& pn = t[static_cast<size_t>(parent)];
+                (pn.l < 0 ? pn.l : pn.r) = k;
+            }
+            if (h.numPrimitives > 0) {
+                n.first = h.indexOffset;
+                n.count = h.numPrimitives;
+            } else {
+                st.push_back({h.indexOffset + 1, k});
+                st.push_back({h.indexOffset, k});
+            }
+        }
+    }
+    const size_t nn = t.size();
+    auto inner = [&](int32_t i) { return t[static_cast<size_t>(i)].count == 0; };
+    for (size_t k = nn; k-- > 0;) {  // heights, children after parents
+        R& n = t[k];
+        if (n.count == 0)
+            n.height = 1 + std::max(t[static_cast<size_t>(n.l)].height, t[static_cast<size_t>(n.r)].height);
+        n.maxHeight = n.height;
+    }
+    auto area = [](const HAABB& b) {
+        const double dx = static_cast<double>(b.mx.x) - b.mn.x, dy = static_cast<double>(b.mx.y) - b.mn.y,
+                     dz = static_cast<double>(b.mx.z) - b.mn.z;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    double total = 0.0;
+    for (const SampleRay& ry : rays) total += ry.w;
+    const double rootArea = std::max(1e-30, area(t[0].box));
+    const double floorK = kRayCostFloor * total / rootArea;
+    std::vector<v3> inv(rays.size());
+    for (size_t k = 0; k < rays.size(); ++k) inv[k] = v3{1.0F / rays[k].d.x, 1.0F / rays[k].d.y, 1.0F / rays[k].d.z};
+    auto passes = [&](const HAABB& b, int32_t k) {
+        return halfLineEntry(b, rays[static_cast<size_t>(k)].o, inv[static_cast<size_t>(k)]) < std::numeric_limits<float>::infinity();
+    };
+    // every inner node's sample rays (ids), by one walk per ray over the tree (threads over rays)
+    std::vector<std::vector<int32_t>> list(nn);
+    {
+        const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::vector<std::vector<int32_t>>> part(hw);
+        std::vector<std::thread> pool;
+        for (unsigned w = 0; w < hw; ++w)
+            pool.emplace_back([&, w] {
+                std::vector<std::vector<int32_t>>& pl = part[w];
+                pl.assign(nn, {});
+                std::vector<int32_t> st;
+                for (size_t k = w; k < rays.size(); k += hw) {
+                    st.assign(1, 0);
+                    while (!st.empty()) {
+                        const int32_t i = st.back();
+                        st.pop_back();
+                        const R& n = t[static_cast<size_t>(i)];
+                        if (n.count > 0 || !passes(n.box, static_cast<int32_t>(k))) continue;
+                        pl[static_cast<size_t>(i)].push_back(static_cast<int32_t>(k));
+                        st.push_back(n.l);
+                        st.push_back(n.r);
+                    }
+                }
+            });
+        for (std::thread& th : pool) th.join();
+        for (size_t i = 0; i < nn; ++i) {
+            size_t sz = 0;
+            for (unsigned w = 0; w < hw; ++w) sz += part[w][i].size();
+            list[i].reserve(sz);
+            for (unsigned w = 0; w < hw; ++w) list[i].insert(list[i].end(), part[w][i].begin(), part[w][i].end());
+            std::sort(list[i].begin(), list[i].end());
+        }
+    }
+    auto weigh = [&](const std::vector<int32_t>& ids, const HAABB& b) {
+        double c = 0.0;
+        for (const int32_t k : ids) c += rays[static_cast<size_t>(k)].w;
+        return c + floorK * area(b);
+    };
+    for (size_t i = 0; i < nn; ++i)
+        if (t[i].count == 0) t[i].cost = weigh(list[i], t[i].box);
+    auto dp = [&](int32_t i) {  // collapseForests' recurrence, node costs instead of areas
+        R& n = t[static_cast<size_t>(i)];
+        if (n.count > 0) return;
+        const R& a = t[static_cast<size_t>(n.l)];
+        const R& b = t[static_cast<size_t>(n.r)];
+        n.height = 1 + std::max(a.height, b.height);
+        auto best = [&](int j) {
+            double c = std::numeric_limits<double>::infinity();
+            for (int q = 1; q < j; ++q) c = std::min(c, a.F[q] + b.F[j - q]);
+            return c;
+        };
+        const double asWide = n.cost + best(kWalkWidth);
+        n.F[1] = asWide;
+        for (int j = 2; j < W1; ++j) n.F[j] = std::min(asWide, best(j));
+    };
+    for (size_t k = nn; k-- > 0;) dp(static_cast<int32_t>(k));
+    auto up = [&](int32_t i) {
+        for (; i >= 0; i = t[static_cast<size_t>(i)].parent) dp(i);
+    };
+    std::vector<int32_t> keep;
+    double cur = t[0].F[1];
+    for (int sweep = 0; sweep < sweeps; ++sweep) {
+        int improved = 0;
+        for (int32_t n = 0; n < static_cast<int32_t>(nn); ++n) {
+            if (!inner(n)) continue;
+            for (int side = 0; side < 2; ++side) {
+                const int32_t x = side == 0 ? t[static_cast<size_t>(n)].l : t[static_cast<size_t>(n)].r;
+                const int32_t m = side == 0 ? t[static_cast<size_t>(n)].r : t[static_cast<size_t>(n)].l;
+                if (!inner(m)) continue;
+                bool done = false;
+                for (int g = 0; g < 2 && !done; ++g) {
+                    const int32_t y = g == 0 ? t[static_cast<size_t>(m)].l : t[static_cast<size_t>(m)].r;
+                    const int32_t z = g == 0 ? t[static_cast<size_t>(m)].r : t[static_cast<size_t>(m)].l;  // stays under m
+                    // after the swap m holds x and z, n holds y and m: the heights must stay within bounds
+                    const int32_t hm = 1 + std::max(t[static_cast<size_t>(x)].height, t[static_cast<size_t>(z)].height);
+                    if (hm > t[static_cast<size_t>(m)].maxHeight ||
+                        1 + std::max(hm, t[static_cast<size_t>(y)].height) > t[static_cast<size_t>(n)].maxHeight)
+                        continue;
+                    const HAABB mb{vmin(t[static_cast<size_t>(x)].box.mn, t[static_cast<size_t>(z)].box.mn),
+                                   vmax(t[static_cast<size_t>(x)].box.mx, t[static_cast<size_t>(z)].box.mx)};
+                    keep.clear();
+                    for (const int32_t k : list[static_cast<size_t>(n)])
+                        if (passes(mb, k)) keep.push_back(k);
+                    const double newCost = weigh(keep, mb);
+                    R& rn = t[static_cast<size_t>(n)];
+                    R& rm = t[static_cast<size_t>(m)];
+                    const HAABB oldBox = rm.box;
+                    const double oldCost = rm.cost;
+                    auto link = [&](int32_t a, int32_t b) {  // swap a (under n) with b (under m)
+                        (rn.l == a ? rn.l : rn.r) = b;
+                        (rm.l == b ? rm.l : rm.r) = a;
+                        t[static_cast<size_t>(a)].parent = m;
+                        t[static_cast<size_t>(b)].parent = n;
+                    };
+                    link(x, y);
+                    rm.box = mb;
+                    rm.cost = newCost;
+                    dp(m);
+                    up(n);
+                    if (t[0].F[1] < cur * (1.0 - 1e-9)) {
+                        cur = t[0].F[1];
+                        list[static_cast<size_t>(m)].swap(keep);
+                        ++improved;
+                        done = true;
+                    } else {  // undo
+                        link(y, x);
+                        rm.box = oldBox;
+                        rm.cost = oldCost;
+                        dp(m);
+                        up(n);
+                    }
+                }
+                if (done) break;
+            }
+        }
+        if (improved == 0) break;
+    }
+    std::vector<HBVHNode> out(1);
+    std::vector<std::pair<int32_t, int32_t>> st{{0, 0}};
+    while (!st.empty()) {
+        const auto [i, slot] = st.back();
+        st.pop_back();
+        const R& n = t[static_cast<size_t>(i)];
+        if (n.count > 0) {
+            out[static_cast<size_t>(slot)] = HBVHNode{n.box, n.first, n.count};
+            continue;
+        }
+        const int32_t left = static_cast<int32_t>(out.size());
+        out.resize(out.size() + 2);
+        out[static_cast<size_t>(slot)] = HBVHNode{n.box, left, 0};
+        st.push_back({n.r, left + 1});
+        st.push_back({n.l, left});
+    }
+    return out;
 }
 
 static std::vector<HBVHNode> walkTreeBuild(const std::vector<HBVHNode>& ref, int rounds, int rotSweeps) {

@@ -170,6 +170,12 @@ struct SampleRay {
 };
 std::vector<SampleRay> sampleFrameRays(const std::vector<HBVHNode>& nodes, const HScene& sc, const GCamera& cam,
                                        int maxDepth);
+// frameRayNodeCosts over a given sample
+std::vector<double> sampleRayNodeCosts(const std::vector<HBVHNode>& nodes, const std::vector<SampleRay>& rays);
+// The walk tree's BVH2 rotated where that lowers its 4-wide collapse's cost under the sample
+// (sampleRayNodeCosts' node cost), up to `sweeps` sweeps; same leaves, exact-union inner boxes, no
+// subtree taller than in `in`.
+std::vector<HBVHNode> rotateForRays(const std::vector<HBVHNode>& in, const std::vector<SampleRay>& rays, int sweeps);
 // A tree over the same leaves (primitive ranges and boxes) as the reference tree `ref`, grouped
 // by a full-sweep SAH; its inner boxes are exact unions of the leaf boxes (reference numbering:
 // node 0 the root, an inner node's children at indexOffset and indexOffset + 1).

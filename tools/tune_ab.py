@@ -1,7 +1,7 @@
 """A/B of tuning settings on the C4 frame: one renderer per setting in one process, interleaved
 rounds, no per-launch events, images compared.  VARIANTS="6=100,6=75+3=1,W=0" (key=value pairs joined
-by '+', settings separated by ','; W / C / O / R set MOBILERT_WALK_TREE / MOBILERT_COLLAPSE / MOBILERT_TREE_OPT /
-MOBILERT_TREE_ROT for the upload, P Config.maxPathsPerPass); RANKS=N renders rank 0's shard of an N-GPU frame."""
+by '+', settings separated by ','; W / C / O / R / Y set MOBILERT_WALK_TREE / MOBILERT_COLLAPSE / MOBILERT_TREE_OPT /
+MOBILERT_TREE_ROT / MOBILERT_RAY_ROT for the upload, P Config.maxPathsPerPass); RANKS=N renders rank 0's shard of an N-GPU frame."""
 import os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -18,7 +18,8 @@ def main():
     rs = {}
     for v in variants:
         # W=0: MOBILERT_WALK_TREE, C=greedy: MOBILERT_COLLAPSE, O=rounds: MOBILERT_TREE_OPT for this renderer's scene upload
-        env = {"W": "MOBILERT_WALK_TREE", "C": "MOBILERT_COLLAPSE", "O": "MOBILERT_TREE_OPT", "R": "MOBILERT_TREE_ROT"}
+        env = {"W": "MOBILERT_WALK_TREE", "C": "MOBILERT_COLLAPSE", "O": "MOBILERT_TREE_OPT", "R": "MOBILERT_TREE_ROT",
+               "Y": "MOBILERT_RAY_ROT"}
         for kv in filter(None, v.split("+")):
             k, val = kv.split("=")
             if k in env:
