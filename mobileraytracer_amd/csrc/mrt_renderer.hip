@@ -10,7 +10,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <exception>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -18,6 +20,7 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "mobilert_amd.h"
@@ -75,6 +78,25 @@ struct DeviceMem {
 #define MRT_RAY_ROT_SWEEPS 1
 #endif
 constexpr int kRayRotSweeps = MRT_RAY_ROT_SWEEPS;
+// Renderers of one scene and camera in one process (a device group's shards, which sample the whole
+// frame's rays, re-created renderers, the test suite) share the result: keyed by a 64-bit FNV-1a
+// digest of everything the sample reads (the walk tree, the triangles, materials and lights, the
+// camera, width, height, depth, sweeps), built once - a build in flight is waited for, as
+// walkTreeOver's - and the last kFrameTreeCache kept.
+constexpr size_t kFrameTreeCache = 4;
+struct FrameTree {
+    std::vector<mrt::HBVHNode> nodes;
+    std::vector<double> cost;
+};
+struct Fnv64 {
+    uint64_t h = 1469598103934665603ull;
+    void add(const void* p, size_t n) {
+        const auto* b = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    }
+    template <class T>
+    void pod(const T& v) { add(&v, sizeof(v)); }
+};
 std::vector<mrt::HBVHNode> frameWalkTree(const std::vector<mrt::HBVHNode>& wn, const mrt::HScene& sc, const mrt::GCamera& cam,
                                          int width, int height, int maxDepth, std::vector<double>* cost) {
     cost->clear();
@@ -84,12 +106,70 @@ std::vector<mrt::HBVHNode> frameWalkTree(const std::vector<mrt::HBVHNode>& wn, c
         cost->assign(wn.size(), 0.0);
         return wn;
     }
-    const std::vector<mrt::SampleRay> rays = mrt::sampleFrameRays(wn, sc, cam, maxDepth);
     const char* re = std::getenv("MOBILERT_RAY_ROT");
     const int sweeps = re != nullptr ? std::atoi(re) : kRayRotSweeps;
-    std::vector<mrt::HBVHNode> out = sweeps > 0 ? mrt::rotateForRays(wn, rays, sweeps) : wn;
-    *cost = mrt::sampleRayNodeCosts(out, rays);
-    return out;
+    Fnv64 f;
+    f.add(wn.data(), wn.size() * sizeof(mrt::HBVHNode));
+    for (const mrt::HTriangle& t : sc.triangles) {
+        f.pod(t.AC);
+        f.pod(t.AB);
+        f.pod(t.A);
+        f.pod(t.mat);
+    }
+    for (const mrt::HMaterial& m : sc.materials) {
+        f.pod(m.Le);
+        f.pod(m.Kd);
+        f.pod(m.Ks);
+    }
+    for (const mrt::HLight& l : sc.lights) {
+        f.pod(l.kind);
+        f.pod(l.tri.A);
+        f.pod(l.tri.AB);
+        f.pod(l.tri.AC);
+    }
+    f.pod(cam);
+    const int dims[4] = {width, height, maxDepth, sweeps};
+    f.pod(dims);
+    using Entry = std::shared_ptr<const FrameTree>;
+    static std::mutex mu;
+    static std::unordered_map<uint64_t, std::shared_future<Entry>> cache;
+    static std::deque<uint64_t> order;
+    std::promise<Entry> mine;
+    std::shared_future<Entry> pending;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        const auto it = cache.find(f.h);
+        if (it != cache.end()) {
+            pending = it->second;
+        } else {
+            cache.emplace(f.h, mine.get_future().share());
+            order.push_back(f.h);
+            while (order.size() > kFrameTreeCache) {
+                cache.erase(order.front());
+                order.pop_front();
+            }
+        }
+    }
+    if (pending.valid()) {
+        const Entry e = pending.get();
+        *cost = e->cost;
+        return e->nodes;
+    }
+    try {
+        auto e = std::make_shared<FrameTree>();
+        const std::vector<mrt::SampleRay> rays = mrt::sampleFrameRays(wn, sc, cam, maxDepth);
+        e->nodes = sweeps > 0 ? mrt::rotateForRays(wn, rays, sweeps) : wn;
+        e->cost = mrt::sampleRayNodeCosts(e->nodes, rays);
+        mine.set_value(e);
+        *cost = e->cost;
+        return e->nodes;
+    } catch (...) {
+        mine.set_exception(std::current_exception());
+        std::lock_guard<std::mutex> lock(mu);
+        cache.erase(f.h);
+        order.erase(std::remove(order.begin(), order.end(), f.h), order.end());
+        throw;
+    }
 }
 
 int bvhDepth(const std::vector<mrt::HBVHNode>& nodes) {
