@@ -24,12 +24,12 @@ tail -1 $OUT/flat.log > $OUT/flat.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python $R/bench.py --steps 10 --no-cpu-baseline > $OUT/prof.log 2>&1 || { tail $OUT/prof.log; exit 8; }
 f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); cp $f $OUT/kernel_stats.csv; head -8 $OUT/kernel_stats.csv | cut -c1-150
-tail -1 $OUT/prof.log > $OUT/prof_bench.json
+grep "^{\"metric\"" $OUT/prof.log | tail -1 > $OUT/prof_bench.json
 # every frame with the shadow walks on the render stream (--overlap 0): each launch runs alone, as in
 # bench's serialised roofline frames, so roofline.avg_launch_ms recomputes from this summary
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_serial -o run -- python $R/bench.py --steps 10 --overlap 0 --no-cpu-baseline > $OUT/prof_serial.log 2>&1 || { tail $OUT/prof_serial.log; exit 11; }
 f=$(find $OUT/prof_serial -name "*kernel_stats.csv" | head -1); cp $f $OUT/kernel_stats_serial.csv; head -8 $OUT/kernel_stats_serial.csv | cut -c1-150
-tail -1 $OUT/prof_serial.log > $OUT/prof_serial_bench.json
+grep "^{\"metric\"" $OUT/prof_serial.log | tail -1 > $OUT/prof_serial_bench.json
 cd $R && bash tools/timeline.sh ${N}_tl > $OUT/tl.log 2>&1 || { tail $OUT/tl.log; exit 9; }
 cp $R/gpurun_out/${N}_tl/n1.timeline $R/gpurun_out/${N}_tl/n8.timeline $OUT/ 2>/dev/null
 timeout -k 10 200 python tools/phase_occupancy.py conference flat > $OUT/phases.jsonl 2>$OUT/phases.err || { tail $OUT/phases.err; exit 10; }

@@ -16,9 +16,11 @@ from collections import defaultdict
 # roofline names them: level 1's packet walk (k_trace_packet; k_trace_packet_shade where level 1 is
 # fused, tuning key 17), the per-lane closest-hit walk of the deeper levels, the shadow walk and the
 # lean PathTracer shading kernel
+# (k_trace_packet<false, 3, kGen>: kGen, round 6, the walk generating its camera rays; k_shade<2, false,
+# kRegen>: kRegen, level 1's shading regenerating them - both instantiations are the k_shade of levels 1-5)
 PRODUCT = {"k_trace": (r"k_trace<false, 1, 3>",), "k_trace_packet_shade": (r"k_trace_packet_shade<2, 3>",),
-           "k_trace_packet": (r"k_trace_packet<false, 3>",),
-           "k_shadow": (r"k_shadow<false, 1, 3>",), "k_shade": (r"k_shade<2, false>",)}
+           "k_trace_packet": (r"k_trace_packet<false, 3, ",),
+           "k_shadow": (r"k_shadow<false, 1, 3>",), "k_shade": (r"k_shade<2, false, ",)}
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import kernel_source_stamp, workload_key  # noqa: E402
 

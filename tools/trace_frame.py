@@ -1,5 +1,6 @@
 """Prints the kernel timeline of the last product frame in a rocprofv3 kernel trace (CSV or rocpd
-.db): frames start at k_raygen or, with level 1 fused, at k_trace_packet_shade; the last frame that
+.db): frames start at k_raygen, at the level-1 packet walk that generates its rays, or, with level 1
+fused, at k_trace_packet_shade; the last frame that
 starts with the fused kernel is a timed frame of bench.py (its profiling frames after the timed
 ones run level 1 unfused), else the last frame."""
 import csv, sqlite3, sys
@@ -17,7 +18,10 @@ def rows_of(path):
 
 
 rows = sorted(rows_of(sys.argv[1]), key=lambda r: r[1])
-starts = [i for i, r in enumerate(rows) if "k_raygen" in r[0] or "k_trace_packet_shade" in r[0]]
+# (round 6: with level 1 unfused the packet walk generates the camera rays itself, tuning key 33, and
+# starts the frame; after a k_raygen it does not)
+starts = [i for i, r in enumerate(rows)
+          if "k_raygen" in r[0] or ("k_trace_packet" in r[0] and not (i > 0 and "k_raygen" in rows[i - 1][0]))]
 fused = [i for i in starts if "k_trace_packet_shade" in rows[i][0]]
 first = fused[-1] if fused else starts[-1]
 end = next((i for i in starts if i > first), len(rows))
