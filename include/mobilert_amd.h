@@ -234,7 +234,9 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  *          stores the records the shading reads (1), or k_shade regenerates them too (2, Whitted /
  *          PathTracer; default), or the walk reads those of a k_raygen launch (0),
  * key 34 = level 1's resolve folded into the per-pixel accumulation, one launch (1, default), or the
- *          resolve and k_accumulate launched separately (0).
+ *          resolve and k_accumulate launched separately (0),
+ * key 35 = the shading of level L waits for the shadow walk of level L - 2 (1: round 1's order, when
+ *          shadow queues alternated by level parity) or not (0, default).
  * (Keys 4, 12-15, 18, 19-25, 29, 30, 32 - binned emission, queue sorting, graph replay, the tile
  * kernel, a shadow-occluder probe, the deeper levels' walk and shading in one launch, a CU-masked
  * shadow stream, k_shade's vertices binned by shading class, the shadow walks yielding to the next

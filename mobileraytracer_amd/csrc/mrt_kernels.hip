@@ -1282,14 +1282,13 @@ void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, 
     const int dead = deadNext ? 1 : 0;
     const RaygenArgs ra = regen != nullptr ? *regen : RaygenArgs{};
     // (a separate instantiation: the regeneration in the shared one cost 8 VGPRs and a wave per SIMD)
-#define MRT_LAUNCH_SHADE(SH, FULL)                                                                          \
-    do {                                                                                                    \
-        if (regen != nullptr)                                                                               \
-            hipLaunchKernelGGL((k_shade<SH, FULL, true>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, \
-                               level, a, dead, ra);                                                         \
-        else                                                                                                \
-            hipLaunchKernelGGL((k_shade<SH, FULL, false>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, \
-                               level, a, dead, ra);                                                         \
+#define MRT_LAUNCH_SHADE_ONE(SH, FULL, RG)                                                                 \
+    hipLaunchKernelGGL((k_shade<SH, FULL, RG>), dim3(grid), dim3(kBlock), 0, st, s, lv, nx, counters, level, a, \
+                       dead, ra)
+#define MRT_LAUNCH_SHADE(SH, FULL)                         \
+    do {                                                   \
+        if (regen != nullptr) MRT_LAUNCH_SHADE_ONE(SH, FULL, true); \
+        else MRT_LAUNCH_SHADE_ONE(SH, FULL, false);        \
     } while (0)
     const bool full = s.textured != 0 || a.stats != nullptr || s.leanShade == 0 ||
                       4 * (s.nMats + s.nLights) > kShadeLdsTable;
@@ -1317,6 +1316,7 @@ void launchShade(int shader, const DScene& s, const Level& lv, const Level& nx, 
             break;
     }
 #undef MRT_LAUNCH_SHADE
+#undef MRT_LAUNCH_SHADE_ONE
 }
 
 void launchResolve(int shader, const DScene& s, const Level& lv, const Level& nx, int* counters, int level,

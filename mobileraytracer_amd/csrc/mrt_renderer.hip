@@ -366,6 +366,7 @@ struct mrt_renderer {
     int genL1 = 2;                       // tuning key 33: the unfused level-1 packet walk generates its camera rays
                                          // (1: and stores them; 2: k_shade regenerates them; 0: k_raygen)
     int resolveAcc = 1;                  // tuning key 34: level 1's resolve and the accumulation in one launch
+    int shadeWaitsShadow = 0;            // tuning key 35: shade(L) waits for shadow(L - 2) (round 1's order)
     int refill = 0;                      // tuning key 9: walk refill threshold (0 auto: by paths per lane)
     int64_t shadeLaunches = 0;           // k_shade launches of the current pass
     bool walkSkipped = false;            // the last pass skipped that walk
@@ -962,7 +963,12 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 launchTrace(r->ds, pp.levels[l], pp.counters, l, pp.gstack, r->gdepth, pp.stats, counting,
                             walkThreads, st, genL1 && l == 1 ? &ra : nullptr);
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-            if (sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
+            // (round 1's shadow queues alternated by level parity, so shade(L) waited for shadow(L - 2);
+            // every level has its own queues since, and the wait - an event packet, ~6 us of command
+            // processing on the critical path - only with tuning key 35 = 1)
+            if (r->shadeWaitsShadow != 0 && sb != st && l >= 3) MRT_HIP(hipStreamWaitEvent(st, shadowDone[l - 2], 0));
+            const bool onRender = lastOnRender && l + 1 >= nLevels;  // the last shadow walk, and the level after it
+            const hipStream_t ss = onRender ? st : sb;
             if (!fused && !(skipLastShade && l == nLevels)) {
                 launchShade(shader, r->ds, pp.levels[l], pp.levels[l + 1], pp.counters, l, sa,
                             shadePerCU > 0 ? r->cus * shadePerCU : r->workGrid, st,
@@ -970,8 +976,9 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                 ++r->shadeLaunches;
             }
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
-            const bool onRender = lastOnRender && l + 1 >= nLevels;  // the last shadow walk, and the level after it
-            const hipStream_t ss = onRender ? st : sb;
+            // (the hand-off event completed by k_shade's own launch - hipExtLaunchKernel's stop event -
+            // instead of this marker measured the same: the ~5 us before the next walk stay,
+            // profiles/r06_event_gap_ab.txt)
             if (sb != st && !onRender) {
                 const hipEvent_t shaded = syncEvent(pp, sync++);
                 MRT_HIP(hipEventRecord(shaded, st));
@@ -1751,6 +1758,11 @@ static int setTuningOne(mrt_renderer* r, int32_t key, int32_t value) {
         r->resolveAcc = value;
         return 0;
     }
+    if (key == 35 && (value == 0 || value == 1)) {
+        r->shadeWaitsShadow = value;
+        return 0;
+    }
+
     if (key == 28 && value >= 0 && value <= 65536) {
         r->walkGridCap = value;
         return 0;
@@ -1935,6 +1947,7 @@ int mrt_get_tuning(const mrt_renderer* r, int32_t key, int32_t* value) {
         case 27: *value = r->lastShadowRender; return 0;
         case 33: *value = r->genL1; return 0;
         case 34: *value = r->resolveAcc; return 0;
+        case 35: *value = r->shadeWaitsShadow; return 0;
         case 28: *value = r->walkGridCap; return 0;
         default: break;
     }

@@ -454,6 +454,33 @@ def test_resolve_accumulate_fusion_is_invariant(oracle_mod):
     assert np.array_equal(bm, ref)
 
 
+def test_shadow_hand_off_is_invariant(oracle_mod):
+    """The shading -> shadow-walk hand-off without shade(L) waiting for shadow(L - 2) (tuning key
+    35 = 0, default; every level has its own shadow queue) gives the bitmaps and ray counts of round
+    1's order (key 35 = 1), frame after frame, and the oracle's bitmap."""
+    import mobileraytracer_amd as m
+    cases = (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+             make_cfg(128, 128, shader=1, scene="water", max_depth=4, spl=2),
+             make_cfg(128, 128, shader=2, scene="teapot", spp=2, max_depth=3))
+    for cfg in cases:
+        with m.Renderer(cfg) as r:
+            assert r.get_tuning(35) == 0
+            outs = []
+            for wait in (0, 1, 0):
+                r.set_tuning(35, wait)
+                for _ in range(3):
+                    bm = np.full(cfg.width * cfg.height, SENTINEL, np.int32)
+                    r.render_frame(bm)
+                    st = r.frame_stats()
+                    outs.append((bm, st["rays"], st["shadowRays"]))
+        for o in outs[1:]:
+            assert np.array_equal(outs[0][0], o[0]), cfg
+            assert outs[0][1:] == o[1:], cfg
+    cfg = cases[0]
+    ref, _ = oracle_for(oracle_mod, cfg).render(threads=4)
+    assert np.array_equal(gpu_render(cfg)[0], ref)
+
+
 def test_last_shadow_walk_on_render_stream_is_invariant(oracle_mod):
     """The last shadow walk on the render stream with the closest-hit spill stacks (tuning key 27,
     on by default) instead of the shadow stream: the same bitmap and ray counts with the key off,
