@@ -1063,19 +1063,35 @@ void launchSpin(unsigned long long* out, int slot, unsigned long long ticks, hip
     hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, st, out, slot, ticks);
 }
 
-__global__ void k_tally(int* counters, int maxLevel, unsigned long long* stats, int skippedLevel) {
-    unsigned long long rays = 0, shadows = 0;
-    for (int l = 1; l <= maxLevel; ++l) {
-        rays += static_cast<unsigned long long>(counters[cntRays(l)]);
-        shadows += static_cast<unsigned long long>(counters[cntShadows(l)]);
-        stats[kStatLevelRays + l - 1] += static_cast<unsigned long long>(counters[cntRays(l)]);
-        stats[kStatLevelShadows + l - 1] += static_cast<unsigned long long>(counters[cntShadows(l)]);
+// A chunk's ray counts into the pass statistics (thread 0), then (round 6) the statistics into the
+// renderer's pinned host block (hostOut: read by the host after its stream synchronisation, instead
+// of a device-to-host copy) and the device state reset for the next chunk or pass: the counters
+// always, the statistics after the pass's last chunk (zeroStats) - so that no memset launch starts
+// the next pass.
+__global__ __launch_bounds__(256) void k_tally(int* counters, int maxLevel, unsigned long long* stats, int skippedLevel,
+                                               unsigned long long* hostOut, int zeroStats) {
+    if (threadIdx.x == 0) {
+        unsigned long long rays = 0, shadows = 0;
+        for (int l = 1; l <= maxLevel; ++l) {
+            rays += static_cast<unsigned long long>(counters[cntRays(l)]);
+            shadows += static_cast<unsigned long long>(counters[cntShadows(l)]);
+            stats[kStatLevelRays + l - 1] += static_cast<unsigned long long>(counters[cntRays(l)]);
+            stats[kStatLevelShadows + l - 1] += static_cast<unsigned long long>(counters[cntShadows(l)]);
+        }
+        stats[kStatRays] += rays;
+        stats[kStatShadowRays] += shadows;
+        stats[kStatPrimary] += static_cast<unsigned long long>(counters[cntRays(1)]);
+        if (skippedLevel > 0) stats[kStatSkipped] += static_cast<unsigned long long>(counters[cntRays(skippedLevel)]);
+        if (counters[kCntOverflow] != 0) stats[kStatOverflow] |= static_cast<unsigned long long>(counters[kCntOverflow]);
     }
-    stats[kStatRays] += rays;
-    stats[kStatShadowRays] += shadows;
-    stats[kStatPrimary] += static_cast<unsigned long long>(counters[cntRays(1)]);
-    if (skippedLevel > 0) stats[kStatSkipped] += static_cast<unsigned long long>(counters[cntRays(skippedLevel)]);
-    if (counters[kCntOverflow] != 0) stats[kStatOverflow] |= static_cast<unsigned long long>(counters[kCntOverflow]);
+    __syncthreads();
+    if (hostOut != nullptr) {
+        for (int k = static_cast<int>(threadIdx.x); k < kNumStats; k += static_cast<int>(blockDim.x)) {
+            hostOut[k] = stats[k];
+            if (zeroStats != 0) stats[k] = 0ull;
+        }
+        for (int k = static_cast<int>(threadIdx.x); k < kNumCounters; k += static_cast<int>(blockDim.x)) counters[k] = 0;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1413,8 +1429,10 @@ void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float
     hipLaunchKernelGGL(k_dump_hits, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, lv, n, kind, index, t);
 }
 
-void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel) {
-    hipLaunchKernelGGL(k_tally, dim3(1), dim3(1), 0, st, counters, maxLevel, stats, skippedLevel);
+void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel,
+                 unsigned long long* hostOut, bool zeroStats) {
+    hipLaunchKernelGGL(k_tally, dim3(1), dim3(256), 0, st, counters, maxLevel, stats, skippedLevel, hostOut,
+                       zeroStats ? 1 : 0);
 }
 
 int traceResidentThreadsPerCU() {

@@ -178,7 +178,10 @@ struct UnpackArgs {
 void launchUnpackRanks(const UnpackArgs& a, int ranks, int maxN, const int32_t* gathered, int32_t* bitmap,
                        hipStream_t st);
 void launchDumpHits(const Level& lv, int n, int32_t* kind, int32_t* index, float* t, hipStream_t st);
-void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel = 0);
+// hostOut (pinned host memory, kNumStats entries): the statistics copied there and the counters reset
+// (and with zeroStats the statistics too), for the next chunk or pass
+void launchTally(int* counters, int maxLevel, unsigned long long* stats, hipStream_t st, int skippedLevel = 0,
+                 unsigned long long* hostOut = nullptr, bool zeroStats = false);
 // known-answer kernels (device slab / triangle tests) and arbitrary-ray loading for tests
 void launchKatSlab(const float* boxes, const float* orig, const float* dir, int n, int32_t* out, hipStream_t st);
 void launchKatTriangle(const float* tris, const float* orig, const float* dir, int n, int32_t* hit, float* t,

@@ -373,7 +373,10 @@ struct mrt_renderer {
     bool fusedL1 = false;                // the last pass ran level 1 as k_trace_packet_shade
     int lastShadowRender = 1;            // tuning key 27: the last shadow walk on the render stream
     int walkGridCap = 0;                 // tuning key 28: at most this many workgroups per walk launch (0: none)
-    unsigned long long* hostStats = nullptr;  // pinned: the per-pass statistics read back by DMA
+    unsigned long long* hostStats = nullptr;  // pinned, coherent: the per-pass statistics, written by k_tally
+    // the device counters / statistics are all zero once the work enqueued so far has run (the last
+    // k_tally reset them): the next pass needs no memset launch
+    bool countersClean = false, statsClean = false;
 
     // host copies for the GL preview of the Android front end (mrt_preview_arrays; kept only for
     // renderers made by mrt_create_from_memory): triangles in BVH order and the materials
@@ -771,6 +774,7 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     }
     pp.counters = r->queueMem.alloc<int>(kNumCounters);
     pp.stats = r->queueMem.alloc<unsigned long long>(kNumStats + kWaveLogEntries);
+    r->countersClean = r->statsClean = false;  // (fresh allocations: not zeroed)
     pp.gstack = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
     pp.gstackShadow = r->queueMem.alloc<int2>(static_cast<size_t>(r->traceThreads) * static_cast<size_t>(r->gdepth));
 }
@@ -853,7 +857,12 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     ShadeArgs sa{r->maxDepth, spl, {r->maxPoint.x, r->maxPoint.y, r->maxPoint.z}, counting ? pp.stats : nullptr};
     const int nLevels = r->nLevels;
     const mrt::PixelMap& map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
-    MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * (kNumStats + (counting ? kWaveLogEntries : 0)), st));
+    if (!r->statsClean || counting)
+        MRT_HIP(hipMemsetAsync(pp.stats, 0, sizeof(unsigned long long) * (kNumStats + (counting ? kWaveLogEntries : 0)), st));
+    r->statsClean = false;
+    if (r->hostStats == nullptr)
+        MRT_HIP(hipHostMalloc(&r->hostStats, sizeof(unsigned long long) * kNumStats, hipHostMallocCoherent));
+    std::memset(r->hostStats, 0, sizeof(unsigned long long) * kNumStats);  // (no chunk run: zeros)
     pp.evCount = 0;
     r->shadeLaunches = 0;
     // Any-hit (shadow) rays of level L run on a second stream, overlapped with the closest-hit
@@ -876,7 +885,8 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
     const bool skipLastShade = skipLast && nLevels >= 2 && r->ds.matsFinite != 0;
     for (int slot0 = 0; slot0 < r->nSlots && !r->stopFlag.load(); slot0 += r->chunkSlots) {
         const int nChunk = std::min(r->chunkSlots, r->nSlots - slot0);
-        MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
+        if (!r->countersClean) MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
+        r->countersClean = false;
         RaygenArgs ra{};
         ra.cam = r->cam;
         ra.map = map;
@@ -1023,7 +1033,12 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
                               skipLastShade && 1 == nLevels - 1);
             launchAccumulate(aa, pp.levels[1].res, dBitmap, dPacked, st);
         }
-        launchTally(pp.counters, nLevels, pp.stats, st, skipLast ? nLevels : 0);
+        // the statistics so far into the pinned host block, the counters reset; after the last chunk
+        // the statistics too
+        const bool lastChunk = slot0 + nChunk >= r->nSlots;
+        launchTally(pp.counters, nLevels, pp.stats, st, skipLast ? nLevels : 0, r->hostStats, lastChunk);
+        r->countersClean = true;
+        if (lastChunk) r->statsClean = true;
     }
 }
 
@@ -1034,9 +1049,7 @@ bool runPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t st
     using namespace mrt;
     const auto t0 = std::chrono::steady_clock::now();
     renderPass(r, dBitmap, dPacked, st, sampleBase, spp);
-    if (r->hostStats == nullptr) MRT_HIP(hipHostMalloc(&r->hostStats, sizeof(unsigned long long) * kNumStats));
-    MRT_HIP(hipMemcpyAsync(r->hostStats, r->pipe.stats, sizeof(unsigned long long) * kNumStats, hipMemcpyDeviceToHost, st));
-    MRT_HIP(hipStreamSynchronize(st));
+    MRT_HIP(hipStreamSynchronize(st));  // (k_tally wrote the pass's statistics into r->hostStats)
     unsigned long long hs[kNumStats];
     std::memcpy(hs, r->hostStats, sizeof(hs));
     const auto t1 = std::chrono::steady_clock::now();
@@ -2000,6 +2013,7 @@ static void primaryHitsOne(mrt_renderer* r, int32_t* kind, int32_t* index, float
             for (int slot0 = 0; slot0 < r->nSlots; slot0 += cap) {
                 const int n = std::min(cap, r->nSlots - slot0);
                 MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
+                r->countersClean = false;  // (left in use: the next pass resets them)
                 RaygenArgs ra{};
                 ra.cam = r->cam;
                 ra.map = r->mapByRank[static_cast<size_t>(r->rankIndex)];
@@ -2126,6 +2140,7 @@ int mrt_trace_rays(mrt_renderer* r, const float* orig, const float* dir, const f
             if (any) MRT_HIP(hipMemcpyAsync(ds.p, dist + base, M * 4, hipMemcpyHostToDevice, st));
             MRT_HIP(hipMemcpyAsync(sc.p, codes.data() + base, M * 4, hipMemcpyHostToDevice, st));
             MRT_HIP(hipMemsetAsync(pp.counters, 0, sizeof(int) * kNumCounters, st));
+            r->countersClean = false;  // (left in use: the next pass resets them)
             launchLoadRays(lv, o.as<float>(), d.as<float>(), ds.as<float>(), sc.as<uint32_t>(), m, any != 0, pp.counters, st);
             if (any) {
                 launchShadow(r->ds, lv, pp.counters, 1, pp.gstackShadow, r->gdepth, pp.stats, false, r->traceThreads, st);

@@ -291,6 +291,46 @@ def test_chunked_passes_are_invariant():
     assert np.array_equal(bm, bm2) and rays == rays2
 
 
+def test_pass_state_is_reset_between_uses():
+    """The device counters and statistics are reset by each pass's last kernel (k_tally, round 6)
+    instead of memsets at the next pass's start, and the statistics come back through the pinned
+    host block it writes: frame after frame, after primary_hits / trace_rays (which use the
+    counters), after a counting frame, after a stop, and over multi-chunk passes, every frame has
+    the first frame's bitmap and ray counts."""
+    import mobileraytracer_amd as m
+    for cfg in (make_cfg(160, 96, shader=2, scene="conference", spp=2, max_depth=5),
+                make_cfg(96, 64, shader=2, scene="water", spp=4, max_depth=4, maxPathsPerPass=5000)):
+        with m.Renderer(cfg) as r:
+            def frame():
+                bm = np.full(cfg.width * cfg.height, SENTINEL, np.int32)
+                r.render_frame(bm)
+                st = r.frame_stats()
+                return bm, (st["rays"], st["shadowRays"], st["walkedRays"], list(st["levelRays"]))
+            first = frame()
+            outs = [frame()]
+            r.primary_hits()
+            outs.append(frame())
+            rng = np.random.default_rng(5)
+            r.trace_rays(rng.normal(size=(300, 3)) * 0.1, rng.normal(size=(300, 3)))
+            outs.append(frame())
+            r.trace_rays(rng.normal(size=(300, 3)) * 0.1, rng.normal(size=(300, 3)), dist=np.ones(300), any_hit=True)
+            outs.append(frame())
+            r.set_profiling(counting=True)
+            outs.append(frame())
+            r.set_profiling()
+            outs.append(frame())
+            r.stop_render()
+            frame()  # (a stopped frame: no chunk runs)
+        with m.Renderer(cfg) as r2:
+            bm = np.full(cfg.width * cfg.height, SENTINEL, np.int32)
+            r2.render_frame(bm)
+            st = r2.frame_stats()
+            outs.append((bm, (st["rays"], st["shadowRays"], st["walkedRays"], list(st["levelRays"]))))
+        for o in outs:
+            assert np.array_equal(first[0], o[0]), cfg
+            assert first[1] == o[1], cfg
+
+
 def test_trace_walks_are_identical():
     """The per-wave reference walk (tuning key 1 = 0: 64-ray batches, plain DFS of
     BVH.hpp:327-384) and the persistent while-while walk (1) return the same hits, images and
