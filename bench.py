@@ -514,11 +514,16 @@ def main():
     packed = torch.zeros(slots_max, dtype=torch.int32, device="cuda")
     gathered = torch.zeros((world, slots_max), dtype=torch.int32, device="cuda") if rank == 0 else None
 
-    def step():
+    # Single-process frames run on the renderer's own stream (stream 0), as RayTrace renders: a
+    # caller's stream costs a join event per frame (the frame then waits for the caller's earlier
+    # work); the buffers are settled by torch.cuda.synchronize() before and after every timed loop.
+    # The RCCL path keeps torch's stream (the gather follows the frame on it), and so does the loop
+    # that copies every frame to the host (each frame after the previous frame's copy).
+    def step(own=0):
         if shard_of:
-            r.render_frame_device(0, packed.data_ptr(), sh)
+            r.render_frame_device(0, packed.data_ptr(), own)
         elif not dist_on:
-            r.render_frame_device(bitmap.data_ptr(), 0, sh)
+            r.render_frame_device(bitmap.data_ptr(), 0, own)
         else:
             r.render_frame_device(0, packed.data_ptr(), sh)
             if backend == "gloo":
@@ -532,6 +537,7 @@ def main():
             if rank == 0:
                 r.unpack_gathered(gathered.data_ptr(), bitmap.data_ptr(), sh)
 
+    torch.cuda.synchronize()  # (the buffers' fills on torch's stream, before frames on the renderer's)
     for _ in range(args.warmup):
         step()
     kernels, per_ray = kernel_roofline(r, step, args.overlap)
@@ -545,8 +551,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        st = r.frame_stats()
-        walked += st["walkedRays"] + st["shadowRays"]
+        w, sr = r.frame_rays()  # (frame_stats()'s dict costs ~20 us of Python per frame)
+        walked += w + sr
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -561,7 +567,7 @@ def main():
     k2 = max(1, min(args.steps, 10))
     t2 = time.perf_counter()
     for _ in range(k2):
-        step()
+        step(sh)  # (on torch's stream: each frame after the previous frame's copy)
         if rank == 0:
             host_bm.copy_(bitmap, non_blocking=True)
     torch.cuda.synchronize()

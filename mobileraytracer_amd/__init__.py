@@ -174,6 +174,15 @@ class Renderer:
             out[k] = list(getattr(s, k))
         return out
 
+    def frame_rays(self):
+        """(walkedRays, shadowRays) of the last frame: frame_stats()'s two ray counts without building
+        its dict (a per-frame call in bench.py's timed loop)."""
+        s = getattr(self, "_rays_buf", None)
+        if s is None:
+            s = self._rays_buf = _native.MrtFrameStats()
+        _native.check(self._lib.mrt_get_frame_stats(self._h, ctypes.byref(s)))
+        return s.walkedRays, s.shadowRays
+
     def primary_hits(self):
         """(kind, index, t) per pixel, index in the scene's input order (config C2)."""
         n = self.config.width * self.config.height

@@ -1588,12 +1588,16 @@ int mrt_render_frame_device(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked,
             return;
         }
         // the frame on the renderer's stream (its hardware queue is known to differ from the shadow
-        // stream's), ordered after the caller's work and before the caller's next
+        // stream's), ordered after the caller's work and before the caller's next.  (A single
+        // renderer's frame ends with its stream synchronised - runPass reads the pass's statistics -
+        // so only a device group's assembly, queued after its shards, needs the second event.)
         MRT_HIP(hipEventRecord(r->joinIn, st));
         MRT_HIP(hipStreamWaitEvent(r->stream, r->joinIn, 0));
         renderFrameDevice(r, dBitmap, dPacked, r->stream);
-        MRT_HIP(hipEventRecord(r->joinOut, r->stream));
-        MRT_HIP(hipStreamWaitEvent(st, r->joinOut, 0));
+        if (!r->peers.empty()) {
+            MRT_HIP(hipEventRecord(r->joinOut, r->stream));
+            MRT_HIP(hipStreamWaitEvent(st, r->joinOut, 0));
+        }
     });
 }
 
