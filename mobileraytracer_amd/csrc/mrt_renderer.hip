@@ -954,11 +954,10 @@ void renderPass(mrt_renderer* r, int32_t* dBitmap, int32_t* dPacked, hipStream_t
         // is skipped, or follows it on the same stream), so it may overlap the previous level's
         // shadow walk, still running on the shadow stream.
         const bool lastOnRender = r->lastShadowRender != 0 && sb != st && nLevels >= 2;
-        if (sb != st) {
-            const hipEvent_t start = syncEvent(pp, sync++);
-            MRT_HIP(hipEventRecord(start, st));
-            MRT_HIP(hipStreamWaitEvent(sb, start, 0));
-        }
+        // (No event orders the shadow stream after the render stream's earlier work: every shadow
+        // launch waits for its level's shading, recorded on the render stream, and the previous
+        // chunk's shadow walks all finished before its resolves.  Round 6 dropped that marker, one
+        // event packet before each pass's first kernel.)
         for (int l = 1; l <= nLevels; ++l) {
             if (timing) MRT_HIP(hipEventRecord(poolEvent(pp), st));
             // level 1 without per-launch events or counting: the packet walk generates its camera rays
