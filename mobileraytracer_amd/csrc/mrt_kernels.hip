@@ -151,7 +151,7 @@ __device__ __forceinline__ void cameraRay(const RaygenArgs& a, int p, float4* o4
 
 __global__ __launch_bounds__(256) void k_raygen(RaygenArgs a, Level lv, int* counters) {
     const int p = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
-    if (p == 0) counters[cntRays(1)] = a.nPaths;
+    if (p == 0) denseCounts(counters, 1, false, a.nPaths, lv.segCap);
     if (p >= a.nPaths) return;
     float4 o4, d4;
     cameraRay(a, p, &o4, &d4);
@@ -244,22 +244,23 @@ __global__ __launch_bounds__(kWalkThreads, MRT_WALK_WAVES) void k_trace(DScene s
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
     const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    const int count = min(counters[cntRays(level)], lv.cap);
+    const SegMap map = segMap(counters, level, false, lv.segCap);
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
     if (kVariant == 1) {
         __shared__ QNode4 ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, count, fetch, st, &cnt, ldsTop, tailBest);
+        traceWhileWhile<false, kCount, kCull>(s, lv.rO, lv.rD, lv.hit, map, fetch, st, &cnt, ldsTop, tailBest);
     }
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
         base = __shfl(base, 0, 64);
-        if (base >= count) break;
-        const int i = base + laneId();
-        if (i < count) {
+        if (base >= map.total()) break;
+        const int v = base + laneId();
+        if (v < map.total()) {
+            const int i = map.phys(v);
             const float4 o4 = lv.rO[i];
             const float4 d4 = lv.rD[i];
             const Best b = closestHit(s, xyz(o4), xyz(d4), fbits(d4.w), st, &cnt);
@@ -303,8 +304,9 @@ __global__ __launch_bounds__(kWalkThreads, kGen ? 7 : 8) void k_trace_packet(DSc
     __shared__ int waveStacks[kWalkThreads / 64][kPacketStack];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
     const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    if (kGen && blockIdx.x == 0 && threadIdx.x == 0) counters[cntRays(level)] = ra.nPaths;  // (k_raygen's count)
-    const int count = kGen ? min(ra.nPaths, lv.cap) : min(counters[cntRays(level)], lv.cap);
+    if (kGen && blockIdx.x == 0 && threadIdx.x == 0) denseCounts(counters, level, false, ra.nPaths, lv.segCap);  // (k_raygen's)
+    // (level 1 is dense: [0, count))
+    const int count = kGen ? min(ra.nPaths, lv.cap) : segMap(counters, level, false, lv.segCap).total();
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
     if constexpr (kGen)
@@ -333,22 +335,23 @@ __global__ __launch_bounds__(kWalkThreads, MRT_SHADOW_WAVES) void k_shadow(DScen
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
     const unsigned long long t0 = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    const int count = min(counters[cntShadows(level)], lv.shadowCap);
+    const SegMap map = segMap(counters, level, true, lv.shadowSegCap);
     int* fetch = counters + kCntFetchShards + (kMaxLevels + level) * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
     if (kVariant == 1) {
         __shared__ QNode4 ldsTop[kWalkTop];
         __shared__ int tailBest[kWalkThreads];
         stageTop<kWalkThreads>(s, ldsTop);
-        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, count, fetch, st, &cnt, ldsTop, tailBest);
+        traceWhileWhile<true, kCount, kCull>(s, lv.sO, lv.sD, lv.sC, map, fetch, st, &cnt, ldsTop, tailBest);
     }
     while (kVariant == 0) {
         int base = 0;
         if (laneId() == 0) base = atomicAdd(fetch, 64);
         base = __shfl(base, 0, 64);
-        if (base >= count) break;
-        const int i = base + laneId();
-        if (i < count) {
+        if (base >= map.total()) break;
+        const int v = base + laneId();
+        if (v < map.total()) {
+            const int i = map.phys(v);
             const float4 o4 = lv.sO[i];
             const float4 d4 = lv.sD[i];
             const bool occ = anyHit(s, xyz(o4), xyz(d4), fbits(o4.w), d4.w, st, &cnt);
@@ -371,9 +374,10 @@ __global__ __launch_bounds__(kWalkThreads, MRT_SHADOW_WAVES) void k_shadow(DScen
 // lights can be hit.
 template <bool kAny>
 __global__ __launch_bounds__(256) void k_trace_other(DScene s, Level lv, int* counters, int level) {
-    const int count = kAny ? min(counters[cntShadows(level)], lv.shadowCap) : min(counters[cntRays(level)], lv.cap);
-    for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
-         i += static_cast<int>(gridDim.x * blockDim.x)) {
+    const SegMap map = segMap(counters, level, kAny, kAny ? lv.shadowSegCap : lv.segCap);
+    for (int v = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); v < map.total();
+         v += static_cast<int>(gridDim.x * blockDim.x)) {
+        const int i = map.phys(v);
         const float4 o4 = kAny ? lv.sO[i] : lv.rO[i];
         const float4 d4 = kAny ? lv.sD[i] : lv.rD[i];
         const v3 o = xyz(o4), d = xyz(d4);
@@ -620,9 +624,10 @@ __device__ __forceinline__ ShadeState shadePrepare(const DScene& s, float4 o4, f
 // then redone in smaller passes).  deadNext: level + 1 is the depth-capped last level, whose
 // rays are counted (the reference constructs them) but never traced, shaded or read, so their
 // payloads are not written and their directions not computed.
+// shadowEnd / childEnd: the end of the queue segments the bases lie in (slots from there on overflow)
 __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, int i, const Level& lv, const Level& nx,
-                                          int shadowBase, int childBase, int* counters, const ShadeArgs& a,
-                                          bool deadNext, const float4* lights) {
+                                          int shadowBase, int childBase, int shadowEnd, int childEnd, int* counters,
+                                          const ShadeArgs& a, bool deadNext, const float4* lights) {
     if (v.terminal) {
         lv.res[i] = v.leaf;
         lv.vtx[i] = make_int4(-1, 0, 0, 0);
@@ -643,7 +648,7 @@ __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, 
             }
             const int j = shadowBase + written;
             ++written;
-            if (j < lv.shadowCap) {
+            if (j < shadowEnd) {
                 lv.sO[j] = make_float4(v.g.P.x, v.g.P.y, v.g.P.z, bitsf(v.g.src));
                 lv.sD[j] = make_float4(ld.x, ld.y, ld.z, dist);
                 lv.sC[j] = make_float4(lc.x, lc.y, lc.z, 0.0F);
@@ -658,7 +663,7 @@ __device__ __forceinline__ void shadeEmit(const DScene& s, const ShadeState& v, 
         int c = childBase;
         auto emit = [&](v3 dir, uint32_t slot) {
             const int j = c++;
-            if (j >= nx.cap) {
+            if (j >= childEnd) {
                 atomicOr(counters + kCntOverflow, 1);
                 return;
             }
@@ -703,17 +708,17 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
     }
     const float4* const mats = kFull ? s.mats : tab;
     const float4* const lights = kFull ? s.lights : tab + 4 * s.nMats;
-    const int count = min(counters[cntRays(level)], lv.cap);
-    // {rays of level+1, shadow rays of level}: one 64-bit allocation per block and iteration
-    auto* pair = reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1));
-    static_assert(cntShadows(1) == cntRays(2) + 1, "pair layout");
+    const SegMap map = segMap(counters, level, false, lv.segCap);
+    const int count = map.total();
+    static_assert(cntShadows(1, 1) == cntRays(2, 1) + 1, "pair layout");
     __shared__ unsigned long long allocLds[2 * (kBlock / 64 + 1)];
     const bool dead = deadNext != 0;
     int parity = 0;
     for (int base = static_cast<int>(blockIdx.x * blockDim.x); base < count;
          base += static_cast<int>(gridDim.x * blockDim.x)) {
-        const int i = base + static_cast<int>(threadIdx.x);
-        const bool active = i < count;
+        const int vi = base + static_cast<int>(threadIdx.x);
+        const bool active = vi < count;
+        const int i = active ? map.phys(vi) : 0;  // the vertex's slot
         ShadeState v{};
         if (active) {
             const float4 h = lv.hit[i];
@@ -735,11 +740,20 @@ __global__ __launch_bounds__(kBlock) void k_shade(DScene s, Level lv, Level nx, 
             v = shadePrepare<kShader>(s, o4, d4, h, tc, level, a, kw, mats, lights);
             if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
         }
+        // {rays of level+1, shadow rays of level}: one 64-bit allocation per block and iteration, in
+        // the queue segment of this 256-vertex chunk (Queue segments, mrt_kernels.hpp: chunk c in
+        // segment c % kQueueSegs, an even split whatever the grid; with a grid of a multiple of 8
+        // workgroups, the segment of the workgroup's XCD)
+        const int seg = static_cast<int>((static_cast<unsigned>(base) / blockDim.x) % kQueueSegs);
+        auto* pair = reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1, seg));
+        const int childOff = seg * nx.segCap, shadowOff = seg * lv.shadowSegCap;
         int childBase, shadowBase;
         const int nC = active ? v.nChild : 0, nS = active ? v.nShadow : 0;
         blockAllocPair(pair, nC, nS, &childBase, &shadowBase, allocLds, parity);
         parity ^= 1;
-        if (active) shadeEmit(s, v, i, lv, nx, shadowBase, childBase, counters, a, dead, lights);
+        if (active)
+            shadeEmit(s, v, i, lv, nx, shadowOff + shadowBase, childOff + childBase, shadowOff + lv.shadowSegCap,
+                      childOff + nx.segCap, counters, a, dead, lights);
         if (kFull && a.stats != nullptr) {  // counting pass: shaded (non-terminal) vertices
             const uint64_t m = __ballot(active && !v.terminal);
             if (laneId() == 0 && m != 0) {
@@ -790,9 +804,14 @@ struct PacketShade {
             if (!v.terminal && v.nChild > 0 && !dead) v.dir0 = firstChildDir(v);
         }
         int childBase, shadowBase;
-        waveAllocPair(reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1)), valid ? v.nChild : 0,
+        // the packet's queue segment (Queue segments, mrt_kernels.hpp): its 64 paths' block
+        const int seg = static_cast<int>((static_cast<unsigned>(__builtin_amdgcn_readfirstlane(i)) >> 6) % kQueueSegs);
+        waveAllocPair(reinterpret_cast<unsigned long long*>(counters + cntRays(level + 1, seg)), valid ? v.nChild : 0,
                       valid ? v.nShadow : 0, &childBase, &shadowBase);
-        if (valid) shadeEmit(*s, v, i, lv, nx, shadowBase, childBase, counters, a, dead, s->lights);
+        const int childOff = seg * nx.segCap, shadowOff = seg * lv.shadowSegCap;
+        if (valid)
+            shadeEmit(*s, v, i, lv, nx, shadowOff + shadowBase, childOff + childBase, shadowOff + lv.shadowSegCap,
+                      childOff + nx.segCap, counters, a, dead, s->lights);
     }
 };
 
@@ -813,7 +832,7 @@ __global__ __launch_bounds__(kWalkThreads, MRT_FUSED_WAVES) void k_trace_packet_
     __shared__ int2 ldsStack[kWalkStack * kWalkThreads];  // per-lane fallback walks only
     __shared__ int waveStacks[kWalkThreads / 64][kPacketStack];
     auto st = makeWalkStack<kCull>(ldsStack, gstack, gdepth);
-    if (blockIdx.x == 0 && threadIdx.x == 0) counters[cntRays(level)] = ra.nPaths;  // (k_raygen's count)
+    if (blockIdx.x == 0 && threadIdx.x == 0) denseCounts(counters, level, false, ra.nPaths, lv.segCap);  // (k_raygen's)
     const int count = min(ra.nPaths, lv.cap);
     int* fetch = counters + kCntFetchShards + level * kMaxFetchShards * kFetchStride;
     TravCount cnt{0u, 0u};
@@ -827,9 +846,10 @@ __global__ __launch_bounds__(kWalkThreads, MRT_FUSED_WAVES) void k_trace_packet_
 //   NoShadows (NoShadows.cpp:13-44: direct light without shadow rays + ambient).
 template <int kShader>
 __global__ __launch_bounds__(kBlock) void k_shade_simple(DScene s, Level lv, int* counters, int level, ShadeArgs a) {
-    const int count = min(counters[cntRays(level)], lv.cap);
-    for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
-         i += static_cast<int>(gridDim.x * blockDim.x)) {
+    const SegMap map = segMap(counters, level, false, lv.segCap);
+    for (int vi = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); vi < map.total();
+         vi += static_cast<int>(gridDim.x * blockDim.x)) {
+        const int i = map.phys(vi);
         const float4 o4 = lv.rO[i];
         const float4 d4 = lv.rD[i];
         const float4 h = lv.hit[i];
@@ -992,10 +1012,10 @@ __device__ __forceinline__ void resolveVertex(const DScene& s, const Level& lv, 
 template <int kShader, bool kTex>
 __global__ __launch_bounds__(256) void k_resolve(DScene s, Level lv, Level nx, int* counters, int level, ShadeArgs a,
                                                  int deadChildren) {
-    const int count = min(counters[cntRays(level)], lv.cap);
-    for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < count;
-         i += static_cast<int>(gridDim.x * blockDim.x))
-        resolveVertex<kShader, kTex>(s, lv, nx, i, level, a, deadChildren);
+    const SegMap map = segMap(counters, level, false, lv.segCap);
+    for (int vi = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); vi < map.total();
+         vi += static_cast<int>(gridDim.x * blockDim.x))
+        resolveVertex<kShader, kTex>(s, lv, nx, map.phys(vi), level, a, deadChildren);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1072,16 +1092,24 @@ __global__ __launch_bounds__(256) void k_tally(int* counters, int maxLevel, unsi
                                                unsigned long long* hostOut, int zeroStats) {
     if (threadIdx.x == 0) {
         unsigned long long rays = 0, shadows = 0;
+        // a level's rays: the sum over its queue segments (the capped last level's are counted, never written)
+        auto levelRays = [&](int l, bool sh) {
+            unsigned long long n = 0;
+            for (int g = 0; g < kQueueSegs; ++g)
+                n += static_cast<unsigned long long>(counters[sh ? cntShadows(l, g) : cntRays(l, g)]);
+            return n;
+        };
         for (int l = 1; l <= maxLevel; ++l) {
-            rays += static_cast<unsigned long long>(counters[cntRays(l)]);
-            shadows += static_cast<unsigned long long>(counters[cntShadows(l)]);
-            stats[kStatLevelRays + l - 1] += static_cast<unsigned long long>(counters[cntRays(l)]);
-            stats[kStatLevelShadows + l - 1] += static_cast<unsigned long long>(counters[cntShadows(l)]);
+            const unsigned long long r = levelRays(l, false), sh = levelRays(l, true);
+            rays += r;
+            shadows += sh;
+            stats[kStatLevelRays + l - 1] += r;
+            stats[kStatLevelShadows + l - 1] += sh;
         }
         stats[kStatRays] += rays;
         stats[kStatShadowRays] += shadows;
-        stats[kStatPrimary] += static_cast<unsigned long long>(counters[cntRays(1)]);
-        if (skippedLevel > 0) stats[kStatSkipped] += static_cast<unsigned long long>(counters[cntRays(skippedLevel)]);
+        stats[kStatPrimary] += levelRays(1, false);
+        if (skippedLevel > 0) stats[kStatSkipped] += levelRays(skippedLevel, false);
         if (counters[kCntOverflow] != 0) stats[kStatOverflow] |= static_cast<unsigned long long>(counters[kCntOverflow]);
     }
     __syncthreads();
@@ -1140,7 +1168,7 @@ void launchKatTriangle(const float* tris, const float* orig, const float* dir, i
 __global__ __launch_bounds__(256) void k_load_rays(Level lv, const float* orig, const float* dir, const float* dist,
                                                    const uint32_t* src, int n, int any, int* counters) {
     const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
-    if (i == 0) counters[any ? cntShadows(1) : cntRays(1)] = n;
+    if (i == 0) denseCounts(counters, 1, any != 0, n, any ? lv.shadowSegCap : lv.segCap);
     if (i >= n) return;
     const uint32_t code = src != nullptr ? src[i] : kNoPrim;
     if (any) {

@@ -18,17 +18,32 @@ constexpr int kAccGrid = 2;
 constexpr int kAccBVH = 3;
 constexpr int kTopNodesMax = 64 * 4 / kWalkWidth;  // walk-tree nodes numbered breadth-first (4 KB staged in LDS by the walk)
 
-// Device counters (ints).  Pair l = {rays of level l+1, shadow rays of level l} sits on two
-// adjacent ints so k_shade allocates both with one 64-bit atomic per block.
-constexpr int kCntPairs = 0;                          // 2 * (kMaxLevels + 1) ints
-constexpr int kCntOverflow = 64;
+// Queue segments (round 6).  Every queue a level's shading fills - the next level's rays, this level's
+// shadow rays - is kQueueSegs segments of segCap / shadowSegCap slots (Level), each with its own
+// counter pair on its own 256-B line: workgroup b allocates in segment b % kQueueSegs.  One counter
+// for the whole queue made every allocation a same-address atomic, which queue at the memory side
+// (a second such atomic per allocation cost +8.1 ms per C4 frame, spread over 8 lines +0.03 ms:
+// profiles/r06_alloc_atomic_probe.txt).  A segment's rays are [g * segCap, g * segCap + count_g);
+// consumers walk the segments (LevelQueue's cursors) or map a dense index over them (SegMap).
+// Level 1 is one dense range [0, n) cut into segments of segCap (denseCounts).
+#ifndef MRT_QUEUE_SEGS
+#define MRT_QUEUE_SEGS 8
+#endif
+constexpr int kQueueSegs = MRT_QUEUE_SEGS;
+// Device counters (ints).  Segment g's pair l = {rays of level l+1, shadow rays of level l} sits on
+// two adjacent ints so k_shade allocates both with one 64-bit atomic per workgroup iteration.
+constexpr int kCntSegStride = 64;                     // ints between segments' pair tables (>= 2 * (kMaxLevels + 1))
+constexpr int kCntPairs = 0;                          // kQueueSegs tables
+constexpr int kCntOverflow = kQueueSegs * kCntSegStride;
 constexpr int kPacketStack = 128;  // the packet walk's wave-uniform stack entries (mrt_trace_packet.hpp)
 constexpr int kMaxFetchShards = 8;                    // work cursors per level (one per XCD group)
 constexpr int kFetchStride = 32;                      // ints between cursors (a 128-byte line each)
-constexpr int kCntFetchShards = 128;                  // 2 kinds x kMaxLevels x kMaxFetchShards lines
+constexpr int kCntFetchShards = kCntOverflow + kFetchStride;  // 2 kinds x kMaxLevels x kMaxFetchShards lines
 constexpr int kNumCounters = kCntFetchShards + 2 * kMaxLevels * kMaxFetchShards * kFetchStride;
-MRT_HD constexpr int cntRays(int level) { return kCntPairs + 2 * (level - 1); }
-MRT_HD constexpr int cntShadows(int level) { return kCntPairs + 2 * level + 1; }
+MRT_HD constexpr int cntRays(int level, int seg = 0) { return kCntPairs + seg * kCntSegStride + 2 * (level - 1); }
+MRT_HD constexpr int cntShadows(int level, int seg = 0) { return kCntPairs + seg * kCntSegStride + 2 * level + 1; }
+static_assert(kQueueSegs >= 1 && kQueueSegs <= kMaxFetchShards, "queue segments: one work cursor each at most");
+static_assert(cntShadows(kMaxLevels) < kCntSegStride, "a segment's pairs within its line");
 
 // 64-bit statistics accumulated on the device across a frame
 constexpr int kStatRays = 0;        // rays of every level (camera + diffuse + specular + transmission)
@@ -81,8 +96,10 @@ struct Level {
     // material index, -1 none), and the last such write in the vertex's subtree (Shader.cpp:112-120)
     float4* kd;
     float4* last;
-    int cap;
-    int shadowCap;
+    int cap;        // physical slots: kQueueSegs * segCap (level 1: its dense paths)
+    int shadowCap;  // kQueueSegs * shadowSegCap
+    int segCap;     // slots per segment (Queue segments above)
+    int shadowSegCap;
 };
 
 // Work units: rectangles of pixels (a reference tile cut into 8-row bands).  prefix[u] is
@@ -121,6 +138,41 @@ struct ShadeArgs {
     float maxPoint[3]; // DepthMap::maxPoint_ (C_wrapper.cpp:79-131 maxDist)
     unsigned long long* stats;  // counting pass only (else null): kStatShaded
 };
+
+// A level's segmented queue seen as one dense index range (k_shade, k_resolve, the per-wave walk):
+// dense index v -> slot g * segCap + (v - pre[g]) of the segment holding it.  Counts are clamped to
+// the segment (an overflowed pass is redone).
+struct SegMap {
+    int pre[kQueueSegs + 1];
+    int segCap;
+    __device__ __forceinline__ int total() const { return pre[kQueueSegs]; }
+    __device__ __forceinline__ int phys(int v) const {
+        int slot = v;  // segment 0: v - pre[0]
+#pragma unroll
+        for (int g = 1; g < kQueueSegs; ++g)
+            if (v >= pre[g]) slot = g * segCap + (v - pre[g]);
+        return slot;
+    }
+};
+__device__ __forceinline__ SegMap segMap(const int* counters, int level, bool shadows, int segCap) {
+    SegMap m;
+    m.segCap = segCap;
+    int acc = 0;
+#pragma unroll
+    for (int g = 0; g < kQueueSegs; ++g) {
+        m.pre[g] = acc;
+        acc += min(counters[shadows ? cntShadows(level, g) : cntRays(level, g)], segCap);
+    }
+    m.pre[kQueueSegs] = acc;
+    return m;
+}
+// a dense range [0, n) as segments of segCap slots: the counts of level 1 (camera rays) and of
+// rays loaded from the host (mrt_trace_rays)
+__device__ __forceinline__ void denseCounts(int* counters, int level, bool shadows, int n, int segCap) {
+#pragma unroll
+    for (int g = 0; g < kQueueSegs; ++g)
+        counters[shadows ? cntShadows(level, g) : cntRays(level, g)] = max(0, min(n - g * segCap, segCap));
+}
 
 struct AccumArgs {
     PixelMap map;

@@ -751,22 +751,38 @@ void allocQueues(mrt_renderer* r, int chunkSlots, int growth) {
     // but one set per level keeps the shadow stream's overlap free of reuse hazards.
     for (int l = 1; l <= nLevels + 1 && l < kMaxLevels; ++l) {
         Level& lv = pp.levels[l];
-        const size_t cap = (l == 1) ? n1 : capN;
         const bool real = l <= nLevels;
+        // Queue segments (mrt_kernels.hpp): level 1 is its dense paths cut into kQueueSegs pieces;
+        // a deeper level's segments each hold an eighth of the level's rays plus slack for the uneven
+        // split over the shading workgroups (an overflow re-renders with smaller chunks, as before)
+        size_t segCap, shadowSegCap;
+        if (kQueueSegs == 1) {
+            segCap = (l == 1) ? n1 : capN;
+            shadowSegCap = segCap * spl;
+        } else if (l == 1) {
+            segCap = (n1 + kQueueSegs - 1) / kQueueSegs;
+            shadowSegCap = (n1 * spl * 5 / 4 + kQueueSegs - 1) / kQueueSegs + static_cast<size_t>(spl) * 4 * 256;
+        } else {
+            segCap = (capN * 5 / 4 + kQueueSegs - 1) / kQueueSegs + 3 * 4 * 256;
+            shadowSegCap = (capN * spl * 5 / 4 + kQueueSegs - 1) / kQueueSegs + static_cast<size_t>(spl) * 4 * 256;
+        }
+        const size_t cap = segCap * kQueueSegs;
         lv = Level{};
         lv.cap = real ? static_cast<int>(cap) : 0;
-        lv.shadowCap = real ? static_cast<int>(cap * spl) : 0;
+        lv.shadowCap = real ? static_cast<int>(shadowSegCap * kQueueSegs) : 0;
+        lv.segCap = real ? static_cast<int>(segCap) : 0;
+        lv.shadowSegCap = real ? static_cast<int>(shadowSegCap) : 0;
         const size_t rays = real ? cap : 0;  // level nLevels + 1: no rays (its parents are terminal)
         lv.rO = r->queueMem.alloc<float4>(rays);
         lv.rD = r->queueMem.alloc<float4>(rays);
         lv.tree = r->queueMem.alloc<uint32_t>(rays);
         lv.hit = r->queueMem.alloc<float4>(rays);
         if (real) {
-            lv.sO = r->queueMem.alloc<float4>(cap * spl);
-            lv.sD = r->queueMem.alloc<float4>(cap * spl);
+            lv.sO = r->queueMem.alloc<float4>(shadowSegCap * kQueueSegs);
+            lv.sD = r->queueMem.alloc<float4>(shadowSegCap * kQueueSegs);
             lv.vtx = r->queueMem.alloc<int4>(cap);
             lv.res = r->queueMem.alloc<float4>(cap);
-            lv.sC = r->queueMem.alloc<float4>(cap * spl);
+            lv.sC = r->queueMem.alloc<float4>(shadowSegCap * kQueueSegs);
         }
         const bool tex = real && r->ds.textured != 0;
         lv.kd = tex ? r->queueMem.alloc<float4>(cap) : nullptr;

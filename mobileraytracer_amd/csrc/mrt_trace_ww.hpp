@@ -513,17 +513,31 @@ __device__ __forceinline__ int interleavedIndex(int j, int seg, int shift) {
 // (kFetchStride ints apart), one per XCD group of workgroups (blockIdx % 8), each over its
 // interleaved chunks of the queue (above); a drained cursor is left for the next (speed only: any
 // placement gives the same results).
+// Round 6: with queue segments (kQueueSegs == kWalkShards, mrt_kernels.hpp) cursor s serves segment
+// s - the rays k_shade's workgroups b % 8 == s allocated, a mix of the image like the interleaved
+// chunks - from its most recently written end; with one segment the interleaved chunks above.
+static_assert(kQueueSegs == 1 || kQueueSegs == kWalkShards, "queue segments: one per work cursor");
 struct LevelQueue {
     const float4* __restrict__ rO;
     const float4* __restrict__ rD;
     float4* out;
+    SegMap map;
     int count;
     int* fetch;
     int seg = static_cast<int>(blockIdx.x % kWalkShards);  // wave-uniform cursor state
     int segsLeft = walkSegments();
     int shift;  // the cursors' chunks: 2^shift rays
-    __device__ __forceinline__ LevelQueue(const float4* o_, const float4* d_, float4* out_, int count_, int* fetch_)
-        : rO(o_), rD(d_), out(out_), count(count_), fetch(fetch_), shift(segChunkShift(count_, kSegChunkLog)) {}
+    __device__ __forceinline__ LevelQueue(const float4* o_, const float4* d_, float4* out_, const SegMap& map_, int* fetch_)
+        : rO(o_), rD(d_), out(out_), map(map_), count(map_.total()), fetch(fetch_),
+          shift(segChunkShift(map_.total(), kSegChunkLog)) {}
+    // segment g's ray count (g wave-uniform)
+    __device__ __forceinline__ int segCount(int g) const {
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < kQueueSegs; ++k)
+            if (k == g) c = map.pre[k + 1] - map.pre[k];
+        return c;
+    }
     __device__ __forceinline__ float4 o(int i) const { return rO[i]; }
     __device__ __forceinline__ float4 d(int i) const { return rD[i]; }
     __device__ __forceinline__ void hit(int i, float4 h) const { out[i] = h; }
@@ -541,7 +555,13 @@ struct LevelQueue {
             if (lane == leader) base = atomicAdd(fetch + seg * kFetchStride, n);
             base = __shfl(base, leader, 64);
             const bool mine = ((pending >> lane) & 1ull) != 0;
-            if (mine) {
+            if (kQueueSegs > 1) {
+                (void)segStart;
+                (void)segEnd;
+                const int idx = base + lanesBelowIn(pending);
+                const int cnt = segCount(seg);
+                if (mine && idx < cnt) got = seg * map.segCap + (cnt - 1 - idx);  // most recently written first
+            } else if (mine) {
 #if MRT_SEG_INTERLEAVE
                 (void)segStart;
                 (void)segEnd;
@@ -1111,9 +1131,10 @@ __device__ __forceinline__ void traceWhileWhileQ(const DScene& s, Queue& q, Stac
 // A level's queue arrays (k_trace / k_shadow): rays [0, count) of rOs / rDs, results into out.
 template <bool kAny, bool kCount, int kCull, class Stack>
 __device__ __forceinline__ void traceWhileWhile(const DScene& s, const float4* __restrict__ rOs,
-                                                const float4* __restrict__ rDs, float4* out, int count, int* fetch,
-                                                Stack& st, TravCount* cnt, const QNode4* ldsTop, int* tailBest) {
-    LevelQueue q(rOs, rDs, out, count, fetch);
+                                                const float4* __restrict__ rDs, float4* out, const SegMap& map,
+                                                int* fetch, Stack& st, TravCount* cnt, const QNode4* ldsTop,
+                                                int* tailBest) {
+    LevelQueue q(rOs, rDs, out, map, fetch);
     traceWhileWhileQ<kAny, kCount, kCull>(s, q, st, cnt, ldsTop, tailBest);
 }
 
