@@ -237,10 +237,11 @@ int mrt_set_max_point(mrt_renderer *r, const float *maxPoint);
  *          resolve and k_accumulate launched separately (0),
  * key 35 = the shading of level L waits for the shadow walk of level L - 2 (1: round 1's order, when
  *          shadow queues alternated by level parity) or not (0, default).
- * (Keys 4, 12-15, 18, 19-25, 29, 30, 32 - binned emission, queue sorting, graph replay, the tile
+ * (Keys 4, 12-15, 18, 19-25, 29, 30, 32, 36 - binned emission, queue sorting, graph replay, the tile
  * kernel, a shadow-occluder probe, the deeper levels' walk and shading in one launch, a CU-masked
  * shadow stream, k_shade's vertices binned by shading class, the shadow walks yielding to the next
- * level's shading - measured slower and were removed.) */
+ * level's shading, a level's closest-hit and shadow walks in one launch - measured slower and were
+ * removed.) */
 int mrt_set_tuning(mrt_renderer *r, int32_t key, int32_t value);
 int mrt_get_tuning(const mrt_renderer *r, int32_t key, int32_t *value);
 /* per pixel (width*height host arrays): kind 0 miss / 1 plane / 2 sphere / 3 triangle /
