@@ -36,7 +36,10 @@ constexpr int kCntSegStride = 64;                     // ints between segments' 
 constexpr int kCntPairs = 0;                          // kQueueSegs tables
 constexpr int kCntOverflow = kQueueSegs * kCntSegStride;
 constexpr int kPacketStack = 128;  // the packet walk's wave-uniform stack entries (mrt_trace_packet.hpp)
-constexpr int kMaxFetchShards = 8;                    // work cursors per level (one per XCD group)
+#ifndef MRT_WALK_CURSORS
+#define MRT_WALK_CURSORS 8
+#endif
+constexpr int kMaxFetchShards = MRT_WALK_CURSORS;     // work cursors per level (a multiple of the 8 XCD groups)
 constexpr int kFetchStride = 32;                      // ints between cursors (a 128-byte line each)
 constexpr int kCntFetchShards = kCntOverflow + kFetchStride;  // 2 kinds x kMaxLevels x kMaxFetchShards lines
 constexpr int kNumCounters = kCntFetchShards + 2 * kMaxLevels * kMaxFetchShards * kFetchStride;

@@ -32,7 +32,7 @@ namespace mrt {
 
 constexpr int kRefDone = 0x7FFFFFFF;  // sentinel: no node (never a valid inner index)
 constexpr int kWalkRefill = 32;       // idle lanes before a wave fetches new rays (DScene::refill at upload; frames set it by paths per lane)
-constexpr int kWalkShards = 8;        // work cursors per level (one per XCD group of workgroups)
+constexpr int kWalkShards = kMaxFetchShards;  // work cursors per level (cursor c: XCD group c % 8)
 // Cursors a wave tries (its own XCD group's first) before it stops fetching.  When a level's queue
 // runs dry every resident wave polls the cursors it has left with an atomic each, and same-address
 // atomics serialise at the memory side: a walk launch with no rays to walk took 100 us with 8
@@ -516,7 +516,7 @@ __device__ __forceinline__ int interleavedIndex(int j, int seg, int shift) {
 // Round 6: with queue segments (kQueueSegs == kWalkShards, mrt_kernels.hpp) cursor s serves segment
 // s - the rays k_shade's workgroups b % 8 == s allocated, a mix of the image like the interleaved
 // chunks - from its most recently written end; with one segment the interleaved chunks above.
-static_assert(kQueueSegs == 1 || kQueueSegs == kWalkShards, "queue segments: one per work cursor");
+static_assert(kQueueSegs == 1 || kWalkShards % kQueueSegs == 0, "queue segments: whole cursors each");
 struct LevelQueue {
     const float4* __restrict__ rO;
     const float4* __restrict__ rD;
@@ -558,9 +558,14 @@ struct LevelQueue {
             if (kQueueSegs > 1) {
                 (void)segStart;
                 (void)segEnd;
+                // cursor seg: segment seg % kQueueSegs, its part seg / kQueueSegs of kWalkShards / kQueueSegs
+                constexpr int kParts = kWalkShards / kQueueSegs;
+                const int g = seg % kQueueSegs, part = seg / kQueueSegs;
+                const int cnt = segCount(g);
+                const int lo = static_cast<int>((static_cast<long long>(cnt) * part) / kParts);
+                const int hi = static_cast<int>((static_cast<long long>(cnt) * (part + 1)) / kParts);
                 const int idx = base + lanesBelowIn(pending);
-                const int cnt = segCount(seg);
-                if (mine && idx < cnt) got = seg * map.segCap + (cnt - 1 - idx);  // most recently written first
+                if (mine && idx < hi - lo) got = g * map.segCap + (hi - 1 - idx);  // most recently written first
             } else if (mine) {
 #if MRT_SEG_INTERLEAVE
                 (void)segStart;
